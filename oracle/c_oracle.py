@@ -1,0 +1,99 @@
+"""ctypes binding of oracle/_build/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ and bench.py's cpu_baseline leg as the large-N checker; the
+product library never loads it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        L.oracle_bin.argtypes = [_P, ctypes.c_int, ctypes.c_int, _I64, _I64, ctypes.c_int, _P, _P,
+                                 ctypes.c_int, _P, _P]
+        L.oracle_bin.restype = None
+        L.oracle_partition.argtypes = [_P, _I64, _I64, _P, _I64, _P, _P]
+        L.oracle_partition.restype = _I64
+        L.oracle_synth_uniform.argtypes = [ctypes.c_uint64, _I64, _I64, ctypes.c_int, _P, _P, _P]
+        L.oracle_synth_uniform.restype = None
+        L.oracle_fnv1a.argtypes = [_P, _I64]
+        L.oracle_fnv1a.restype = ctypes.c_uint64
+        L.oracle_pymod.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.oracle_pymod.restype = ctypes.c_double
+        L.oracle_trunc_i64.argtypes = [ctypes.c_double]
+        L.oracle_trunc_i64.restype = ctypes.c_int64
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def bin_positions(position, grid_topology, box_length, periodic=True, compute_f32=None,
+                  want_idx=False):
+    """Bin ``position`` ((N, >=dim) float32/float64, C-contiguous rows) in place.
+
+    Returns int64 cell ids (and per-dim indexes when ``want_idx``)."""
+    assert position.ndim == 2 and position.strides[1] == position.itemsize
+    topo = np.ascontiguousarray(np.asarray(grid_topology).astype(np.int64))
+    box_arr = np.asarray(box_length)
+    dim = len(topo)
+    is_f32 = position.dtype == np.float32
+    assert is_f32 or position.dtype == np.float64
+    if compute_f32 is None:
+        compute_f32 = is_f32 and np.result_type(position.dtype, box_arr.dtype) == np.float32
+    box = np.ascontiguousarray(box_arr.astype(np.float64))
+    n = position.shape[0]
+    row_stride = position.strides[0] // position.itemsize
+    cell = np.empty(n, dtype=np.int64)
+    idx = np.empty((n, dim), dtype=np.int64) if want_idx else None
+    lib().oracle_bin(_ptr(position), int(is_f32), int(bool(compute_f32)), n, row_stride, dim,
+                     _ptr(box), _ptr(topo), int(bool(periodic)), _ptr(cell), _ptr(idx))
+    return (cell, idx) if want_idx else cell
+
+
+def partition(data, dest, nbins):
+    """Stable partition of rows of ``data`` by ``dest`` (int64); returns (out, offsets)."""
+    data = np.ascontiguousarray(data)
+    dest = np.ascontiguousarray(np.asarray(dest, dtype=np.int64))
+    n = data.shape[0]
+    row_bytes = data.itemsize * (int(np.prod(data.shape[1:])) if data.ndim > 1 else 1)
+    out = np.empty_like(data)
+    offsets = np.zeros(nbins + 1, dtype=np.int64)
+    total = lib().oracle_partition(_ptr(data), n, row_bytes, _ptr(dest), nbins, _ptr(out),
+                                   _ptr(offsets))
+    return out[:total], offsets
+
+
+def synth_uniform(seed, gid0, n, dim=3, box=1.0):
+    box = np.ascontiguousarray(np.broadcast_to(np.asarray(box, dtype=np.float64), (dim,)))
+    pos = np.empty((n, dim), dtype=np.float64)
+    ids = np.empty(n, dtype=np.int64)
+    lib().oracle_synth_uniform(seed, gid0, n, dim, _ptr(box), _ptr(pos), _ptr(ids))
+    return pos, ids
+
+
+def fnv1a(arr):
+    arr = np.ascontiguousarray(arr)
+    return int(lib().oracle_fnv1a(_ptr(arr), arr.nbytes))

@@ -1,0 +1,163 @@
+/*
+ * CPU oracle (C restatement) of the reference redistribution path.
+ *
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg as the checker / large-N verifier.  The product
+ * library (libmgr.so) never links or calls anything here.
+ *
+ * Restates redist.py (dkorytov/mpi_grid_redistribute) from SURVEY.md §0 S11:
+ *   pymod(a,b){m=fmod(a,b); if(m!=0){if((b<0)!=(m<0)) m+=b;} else m=copysign(0,b);}
+ *   t = pymod(pymod(x,L)+L, L)                 redist.py:68, :328-329 (S1)
+ *   k = trunc_i64(t/L*(double)n)               redist.py:69-70        (S2, S10)
+ *   k = ((k%n)+n)%n  (floor-mod)               redist.py:83-84, :90   (S3)
+ *   cell = sum_d offset[d]*k[d], row-major     redist.py:53-58, :84   (S4)
+ * float32 positions: wrap in f64, round to f32 on write-back, bin from the
+ * f32 value in f64 (S9); f32 positions with an f32 box compute the wrap and
+ * the quotient in f32 (numpy result_type), the *n in f64.
+ * Stable split + source-ordered concat: redist.py:195-199 (S6, S7).
+ *
+ * Build: gcc -O2 -ffp-contract=off -fPIC -shared (oracle/Makefile).  No
+ * -ffast-math: every operation must be IEEE-exact.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* x86 cvttsd2si semantics of numpy astype(int64): NaN/out-of-range -> INT64_MIN (S10). */
+static int64_t trunc_i64(double v) {
+    if (v >= -9223372036854775808.0 && v < 9223372036854775808.0) return (int64_t)v;
+    return INT64_MIN;
+}
+
+/* numpy npy_remainder for doubles (floor-remainder, result takes the divisor's sign). */
+static double pymod(double a, double b) {
+    double m = fmod(a, b);
+    if (b == 0.0) return m;
+    if (m != 0.0) {
+        if ((b < 0) != (m < 0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+
+static float pymodf(float a, float b) {
+    float m = fmodf(a, b);
+    if (b == 0.0f) return m;
+    if (m != 0.0f) {
+        if ((b < 0) != (m < 0)) m += b;
+    } else {
+        m = copysignf(0.0f, b);
+    }
+    return m;
+}
+
+/* numpy int64 remainder (Python floor-mod); n == 0 -> 0 like numpy. */
+static int64_t floormod_i64(int64_t a, int64_t n) {
+    if (n == 0) return 0;
+    if (n == -1) return 0;
+    int64_t r = a % n;
+    if (r != 0 && ((r < 0) != (n < 0))) r += n;
+    return r;
+}
+
+double oracle_pymod(double a, double b) { return pymod(a, b); }
+float oracle_pymodf(float a, float b) { return pymodf(a, b); }
+int64_t oracle_trunc_i64(double v) { return trunc_i64(v); }
+
+/*
+ * Bin n rows of positions (row r, coordinate d at pos[r*row_stride + d]).
+ *   pos_is_f32  : element type float (else double)
+ *   compute_f32 : only with pos_is_f32 -- box is float32 (numpy f32 % f32)
+ *   periodic    : wrap + in-place write-back (redist.py:67-68)
+ * Outputs: cell[r] (int64, row-major cell id), idx[r*dim+d] (optional).
+ */
+void oracle_bin(void* pos, int pos_is_f32, int compute_f32, int64_t n, int64_t row_stride,
+                int dim, const double* box, const int64_t* topo, int periodic,
+                int64_t* cell, int64_t* idx) {
+    int64_t offset[64];
+    int64_t off = 1;
+    for (int d = dim - 1; d >= 0; --d) { offset[d] = off; off *= topo[d]; }
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t c = 0;
+        for (int d = 0; d < dim; ++d) {
+            int64_t k;
+            if (pos_is_f32) {
+                float* p = (float*)pos + r * row_stride + d;
+                if (compute_f32) {
+                    float L = (float)box[d];
+                    if (periodic) *p = pymodf(pymodf(*p, L) + L, L);
+                    float q = *p / L;
+                    k = trunc_i64((double)q * (double)topo[d]);
+                } else {
+                    double L = box[d];
+                    if (periodic) *p = (float)pymod(pymod((double)*p, L) + L, L);
+                    k = trunc_i64((double)*p / L * (double)topo[d]);
+                }
+            } else {
+                double* p = (double*)pos + r * row_stride + d;
+                double L = box[d];
+                if (periodic) *p = pymod(pymod(*p, L) + L, L);
+                k = trunc_i64(*p / L * (double)topo[d]);
+            }
+            if (idx) idx[r * dim + d] = k;
+            c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
+        }
+        cell[r] = c;
+    }
+}
+
+/*
+ * Stable counting-sort partition of n rows of row_bytes by dest[r] in
+ * [0, nbins); rows with dest outside are dropped (redist.py:195-198, S6).
+ * offsets[nbins+1] receives the segment starts.  Returns rows written.
+ */
+int64_t oracle_partition(const void* data, int64_t n, int64_t row_bytes, const int64_t* dest,
+                         int64_t nbins, void* out, int64_t* offsets) {
+    int64_t* cur = (int64_t*)calloc((size_t)nbins + 1, sizeof(int64_t));
+    for (int64_t r = 0; r < n; ++r)
+        if (dest[r] >= 0 && dest[r] < nbins) cur[dest[r] + 1]++;
+    for (int64_t b = 0; b < nbins; ++b) cur[b + 1] += cur[b];
+    for (int64_t b = 0; b <= nbins; ++b) offsets[b] = cur[b];
+    const char* src = (const char*)data;
+    char* dst = (char*)out;
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t b = dest[r];
+        if (b < 0 || b >= nbins) continue;
+        memcpy(dst + (cur[b]++) * row_bytes, src + r * row_bytes, (size_t)row_bytes);
+    }
+    int64_t total = offsets[nbins];
+    free(cur);
+    return total;
+}
+
+/* splitmix64 finaliser and the §8d uniform generator (same stream as the device one). */
+static uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+uint64_t oracle_splitmix64(uint64_t x) { return splitmix64(x); }
+
+void oracle_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const double* box,
+                          double* pos, int64_t* ids) {
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t gid = (uint64_t)(gid0 + i);
+        for (int d = 0; d < dim; ++d) {
+            uint64_t h = splitmix64(seed ^ (3ULL * gid + (uint64_t)d));
+            pos[i * dim + d] = (double)(h >> 11) * 0x1.0p-53 * box[d];
+        }
+        if (ids) ids[i] = (int64_t)gid;
+    }
+}
+
+/* FNV-1a over a byte range: order-sensitive digest for large-N parity. */
+uint64_t oracle_fnv1a(const void* p, int64_t nbytes) {
+    const unsigned char* b = (const unsigned char*)p;
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (int64_t i = 0; i < nbytes; ++i) { h ^= b[i]; h *= 0x100000001b3ULL; }
+    return h;
+}

@@ -1,0 +1,318 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Run in the survey container only (needs /root/reference, never on the GPU
+box):   python tests/golden/make_golden.py
+
+How the reference is run (SURVEY.md §8c recipe; nothing is copied):
+  * stub ``mpi4py`` / ``mpi4py.MPI`` modules are placed in ``sys.modules``
+    (mpi4py is not installed here);
+  * ``np.int = int`` and ``np.product = np.prod`` restore the two numpy<1.24
+    aliases the reference uses (S14);
+  * ``MPLBACKEND=Agg``;
+  * ``/root/reference/redist.py`` is loaded read-only with importlib;
+  * ranks run as threads on a fake communicator whose ``alltoall`` is a
+    barrier-synchronised slot exchange returning a list indexed by source rank
+    (mpi4py lowercase semantics, redist.py:199).
+
+Each fixture is an .npz of inputs and the reference's outputs (data only):
+per-rank positions before/after the call (the reference mutates them in place,
+S1), the cell ids, and the per-rank redistributed data.
+"""
+from __future__ import annotations
+
+import importlib.util
+import os
+import sys
+import threading
+import types
+
+import numpy as np
+
+REF_PATH = "/root/reference/redist.py"
+OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_reference():
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    mpi4py = types.ModuleType("mpi4py")
+    mpi = types.ModuleType("mpi4py.MPI")
+    mpi.COMM_WORLD = None
+    mpi4py.MPI = mpi
+    sys.modules["mpi4py"] = mpi4py
+    sys.modules["mpi4py.MPI"] = mpi
+    np.int = int  # noqa: S14 shim
+    np.product = np.prod
+    spec = importlib.util.spec_from_file_location("redist_reference", REF_PATH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+class FakeWorld:
+    def __init__(self, size):
+        self.size = size
+        self.barrier = threading.Barrier(size)
+        self.slots = [None] * size
+
+
+class FakeComm:
+    """mpi4py-comm duck type: Get_rank/Get_size/alltoall (redist.py:41-42, :199)."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank = world, rank
+
+    def Get_rank(self):
+        return self.rank
+
+    def Get_size(self):
+        return self.world.size
+
+    def alltoall(self, sendobj):
+        w = self.world
+        assert len(sendobj) == w.size
+        w.slots[self.rank] = [np.array(x, copy=True) for x in sendobj]  # pickle == copy
+        w.barrier.wait()
+        out = [w.slots[s][self.rank] for s in range(w.size)]
+        w.barrier.wait()
+        return out
+
+
+def run_ranks(size, fn):
+    world = FakeWorld(size)
+    results = [None] * size
+    errors = []
+
+    def body(r):
+        try:
+            results[r] = fn(FakeComm(world, r), r)
+        except BaseException as e:  # pragma: no cover
+            errors.append((r, e))
+            world.barrier.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(size)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errors:
+        raise errors[0][1]
+    return results
+
+
+class SingleComm:
+    """Rank 0 of a ``size``-rank world; binning needs no transport."""
+
+    def __init__(self, size):
+        self.size = size
+
+    def Get_rank(self):
+        return 0
+
+    def Get_size(self):
+        return self.size
+
+
+def edge_values(L, rng):
+    L = float(L)
+    v = [0.0, -0.0, L, 2 * L, -L, -2 * L, np.nextafter(L, 0), np.nextafter(L, 2 * L),
+         np.nextafter(0.0, 1.0), -np.nextafter(0.0, 1.0), 1e-300, -1e-300, 1e-10, -1e-10,
+         0.49999999999999994 * L, 0.5 * L, 0.25 * L, -0.25 * L, -0.75 * L, 2.6 * L,
+         L / 3, 2 * L / 3, 1e20, -1e20, 1e300, -1e300, np.nan, np.inf, -np.inf, 6 * L - 1e-9]
+    v = np.array(v, dtype=np.float64)
+    u = rng.uniform(-6 * L, 6 * L, 200)
+    w = rng.uniform(0, L, 200)
+    return np.concatenate([v, u, w])
+
+
+def make_bin_edges(ref, rng):
+    """Single-rank binning of edge values (S1-S3, S9-S11) over several (L, n)."""
+    out = {}
+    combos = [(1.0, 2), (1.0, 3), (0.3, 3), (62.5, 2), (1000.0, 3), (7.0, 3), (10.0, 7),
+              (1e-3, 5), (3, 4)]  # (3, 4): integer box (S11a)
+    for ci, (L, n) in enumerate(combos):
+        vals = edge_values(L, rng)
+        for mode in ("f64", "f32_boxf64", "f32_boxf32", "f64_nonperiodic", "f32_nonperiodic"):
+            if isinstance(L, int) and mode == "f32_boxf32":
+                continue
+            pos_dtype = np.float64 if mode.startswith("f64") else np.float32
+            periodic = not mode.endswith("nonperiodic")
+            if mode == "f32_boxf32":
+                box = np.array([L], dtype=np.float32)
+            elif isinstance(L, int):
+                box = [L]
+            else:
+                box = [L]
+            with np.errstate(all="ignore"):
+                pos = vals.astype(pos_dtype).reshape(-1, 1)
+            pos_in = pos.copy()
+
+            R = ref.MPIGridRedistributor(SingleComm(n), [n], box)
+            p2 = pos.copy()
+            with np.errstate(all="ignore"):
+                idx = R.get_cell_indexes_from_position(p2, periodic=periodic)
+                cell = R.get_cell_number_from_position(pos, periodic=periodic)
+            key = f"c{ci}_{mode}"
+            out[key + "_L"] = np.asarray(box)
+            out[key + "_n"] = np.int64(n)
+            out[key + "_pos_in"] = pos_in
+            out[key + "_pos_out"] = pos
+            out[key + "_idx"] = idx
+            out[key + "_cell"] = cell
+    np.savez_compressed(os.path.join(OUT_DIR, "bin_edges.npz"), **out)
+    return len(out)
+
+
+def rec32(pos, gid0):
+    rec = np.zeros(len(pos), dtype=[("x", "f8"), ("y", "f8"), ("z", "f8"), ("id", "i8")])
+    rec["x"], rec["y"], rec["z"] = pos[:, 0], pos[:, 1], pos[:, 2]
+    rec["id"] = np.arange(gid0, gid0 + len(pos))
+    return rec
+
+
+def rec36(pos, rng, gid0):
+    dt = np.dtype([("pos", "f4", 3), ("vel", "f4", 3), ("mass", "f4"), ("id", "i8")])
+    assert dt.itemsize == 36
+    rec = np.zeros(len(pos), dtype=dt)
+    rec["pos"] = pos
+    rec["vel"] = rng.normal(size=(len(pos), 3)).astype(np.float32)
+    rec["mass"] = rng.uniform(1, 2, len(pos)).astype(np.float32)
+    rec["id"] = np.arange(gid0, gid0 + len(pos))
+    return rec
+
+
+def positions(rng, n, dim, box, frac_out=0.05, dtype=np.float64):
+    box = np.asarray(box, dtype=np.float64)
+    p = rng.uniform(0, 1, (n, dim)) * box
+    k = rng.random(n) < frac_out
+    p[k] = rng.uniform(-2, 3, (int(k.sum()), dim)) * box
+    return p.astype(dtype)
+
+
+CASES = [
+    # name, topology, box, size, dim, pos dtype, payload kind, periodic, alias
+    ("p8_f64_rec32", [2, 2, 2], [1.0, 1.0, 1.0], 8, 3, np.float64, "rec32", True, False),
+    ("p1_f64_rec32", [1, 1, 1], [1.0, 1.0, 1.0], 1, 3, np.float64, "rec32", True, False),
+    ("p2_f32_rec36", [2, 1, 1], [1.0, 1.0, 1.0], 2, 3, np.float32, "rec36", True, False),
+    ("p4_2d_intbox_mat", [2, 2], [10, 10], 4, 2, np.float64, "mat3", True, False),
+    ("p27_333_ids", [3, 3, 3], [0.3, 62.5, 7.0], 27, 3, np.float64, "ids", True, False),
+    ("p9_421_rec32", [4, 2, 1], [4.0, 2.0, 1.0], 9, 3, np.float64, "rec32", True, False),
+    ("p4_f32box_rec36", [2, 2, 1], np.array([1.0, 2.0, 1.0], np.float32), 4, 3, np.float32,
+     "rec36", True, False),
+    ("p8_nonperiodic_rec32", [2, 2, 2], [1.0, 1.0, 1.0], 8, 3, np.float64, "rec32", False, False),
+    ("p4_2d_alias", [2, 2], [10.0, 10.0], 4, 2, np.float64, "alias", True, False),
+    ("p6_321_f32_mat", [3, 2, 1], [3.0, 2.0, 1.5], 6, 3, np.float32, "mat_i32", True, False),
+    # Cfg5 shape: position is the strided f32 (N,3) view of a 36 B record (S9)
+    ("p8_rec36_view", [2, 2, 2], [1.0, 1.0, 1.0], 8, 3, np.float32, "rec36_view", True, False),
+]
+
+
+def make_redistribute(ref, rng):
+    n_files = 0
+    for name, topo, box, size, dim, pdt, kind, periodic, _ in CASES:
+        n_per = rng.integers(50, 400, size)
+        pos_in, data_in = [], []
+        gid = 0
+        for r in range(size):
+            p = positions(rng, int(n_per[r]), dim, box, dtype=pdt)
+            if kind == "rec32":
+                d = rec32(p.astype(np.float64), gid)
+            elif kind in ("rec36", "rec36_view"):
+                d = rec36(p, rng, gid)
+            elif kind == "mat3":
+                d = rng.normal(size=(len(p), 3))
+            elif kind == "ids":
+                d = np.arange(gid, gid + len(p), dtype=np.int64)
+            elif kind == "mat_i32":
+                d = rng.integers(-1000, 1000, (len(p), 5)).astype(np.int32)
+            elif kind == "alias":
+                d = None
+            gid += len(p)
+            pos_in.append(p)
+            data_in.append(d)
+
+        pos_work = [p.copy() for p in pos_in]
+        data_work = [pos_work[r] if kind == "alias" else data_in[r] for r in range(size)]
+        if kind == "rec36_view":
+            data_work = [d.copy() for d in data_in]
+            pos_work = [d["pos"] for d in data_work]
+        cell_pos = [p.copy() for p in pos_in]
+
+        def fn(comm, r):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            with np.errstate(all="ignore"):
+                cell = R.get_cell_number_from_position(cell_pos[r], periodic=periodic)
+                out = R.redistribute_by_position(data_work[r], pos_work[r], periodic=periodic)
+            return cell, out
+
+        res = run_ranks(size, fn)
+        f = {"topology": np.asarray(topo, dtype=np.int64), "box": np.asarray(box),
+             "size": np.int64(size), "periodic": np.bool_(periodic),
+             "alias": np.bool_(kind == "alias")}
+        for r in range(size):
+            f[f"r{r}_pos_in"] = pos_in[r]
+            f[f"r{r}_pos_out"] = pos_work[r]
+            if kind != "alias":
+                f[f"r{r}_data"] = data_in[r]
+            f[f"r{r}_cell"] = res[r][0]
+            f[f"r{r}_out"] = res[r][1]
+        np.savez_compressed(os.path.join(OUT_DIR, f"redist_{name}.npz"), **f)
+        n_files += 1
+
+    # redistribute_by_cell_number with caller ids incl. out-of-range (S6)
+    size = 5
+    ids_in, data_in = [], []
+    for r in range(size):
+        n = int(rng.integers(30, 300))
+        ids_in.append(rng.integers(-2, size + 3, n).astype(np.int64))
+        data_in.append(rng.normal(size=(n, 3)).astype(np.float32))
+
+    def fn2(comm, r):
+        R = ref.MPIGridRedistributor(comm, [size], [1.0])
+        return R.redistribute_by_cell_number(data_in[r], ids_in[r])
+
+    res = run_ranks(size, fn2)
+    f = {"size": np.int64(size)}
+    for r in range(size):
+        f[f"r{r}_ids"] = ids_in[r]
+        f[f"r{r}_data"] = data_in[r]
+        f[f"r{r}_out"] = res[r]
+    np.savez_compressed(os.path.join(OUT_DIR, "cellnum_p5_f32mat.npz"), **f)
+    n_files += 1
+
+    # constructor geometry (redist.py:16-61) for a few topologies
+    g = {}
+    for i, (topo, box, size) in enumerate([([2, 2, 2], [1.0, 1.0, 1.0], 8),
+                                           ([3, 3, 3], [0.3, 62.5, 7.0], 27),
+                                           ([4, 2, 1], [4.0, 2.0, 1.0], 9),
+                                           ([2.0, 2.0], [10, 40], 4), ([5], [2.5], 5)]):
+        def fn3(comm, r, topo=topo, box=box):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            return (R.cell_index_offset.copy(), R.cell_length.copy(), R.rank_cell_index.copy(),
+                    R.rank_cell_limits.copy(),
+                    R.get_indexes_from_cell_number(np.arange(int(np.prod(topo)))),
+                    R.get_cell_number_from_indexes(
+                        np.array([[-1] * len(topo), [3] * len(topo), [0] * len(topo)]),
+                        periodic=False))
+        res = run_ranks(size, fn3)
+        for r in range(size):
+            for j, nm in enumerate(("offset", "cell_length", "rank_cell_index",
+                                    "rank_cell_limits", "indexes_from_cell", "cellnum_nonper")):
+                g[f"g{i}_r{r}_{nm}"] = res[r][j]
+        g[f"g{i}_topology"] = np.asarray(topo)
+        g[f"g{i}_box"] = np.asarray(box)
+        g[f"g{i}_size"] = np.int64(size)
+    np.savez_compressed(os.path.join(OUT_DIR, "geometry.npz"), **g)
+    return n_files + 1
+
+
+def main():
+    ref = load_reference()
+    rng = np.random.default_rng(20261015)
+    a = make_bin_edges(ref, rng)
+    b = make_redistribute(ref, rng)
+    print(f"bin_edges arrays: {a}; redistribute fixtures: {b}")
+
+
+if __name__ == "__main__":
+    main()

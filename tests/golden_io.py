@@ -1,0 +1,32 @@
+"""Helpers to read the golden fixtures (tests/golden/*.npz, made by make_golden.py)."""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def redist_cases():
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "redist_*.npz")))
+
+
+def bin_edge_keys(f):
+    return sorted({k[: k.rindex("_pos_in")] for k in f.keys() if k.endswith("_pos_in")})
+
+
+def per_rank(f, key, size):
+    return [f[f"r{r}_{key}"] for r in range(size)]
+
+
+def same_bytes(a, b):
+    """Bit-exact comparison (NaN-safe): dtype, shape and raw bytes."""
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()

@@ -1,0 +1,142 @@
+"""Pin the CPU oracle (NumPy + C restatements) against the reference's own outputs.
+
+The fixtures were produced by running /root/reference/redist.py itself
+(tests/golden/make_golden.py); these tests run anywhere (no reference, no GPU).
+"""
+import numpy as np
+import pytest
+
+from oracle import c_oracle
+from oracle import redist_oracle as ro
+from tests import golden_io as G
+
+
+@pytest.fixture(scope="module")
+def edges():
+    return G.load("bin_edges.npz")
+
+
+def _box_for(f, key):
+    return f[key + "_L"]
+
+
+def test_bin_edges_numpy(edges):
+    for key in G.bin_edge_keys(edges):
+        n = int(edges[key + "_n"])
+        box = _box_for(edges, key)
+        periodic = not key.endswith("nonperiodic")
+        geo = ro.Geometry([n], box, n)
+        pos = edges[key + "_pos_in"].copy()
+        p2 = pos.copy()
+        with np.errstate(all="ignore"):
+            idx = ro.cell_indexes_from_position(geo, p2, periodic)
+            cell = ro.cell_number_from_position(geo, pos, periodic)
+        assert G.same_bytes(pos, edges[key + "_pos_out"]), key
+        assert np.array_equal(idx, edges[key + "_idx"]), key
+        assert np.array_equal(cell, edges[key + "_cell"]), key
+
+
+def test_bin_edges_c(edges):
+    for key in G.bin_edge_keys(edges):
+        n = int(edges[key + "_n"])
+        box = _box_for(edges, key)
+        periodic = not key.endswith("nonperiodic")
+        pos = edges[key + "_pos_in"].copy()
+        cell, idx = c_oracle.bin_positions(pos, [n], box, periodic=periodic, want_idx=True)
+        assert G.same_bytes(pos, edges[key + "_pos_out"]), key
+        assert np.array_equal(idx, edges[key + "_idx"]), key
+        assert np.array_equal(cell, edges[key + "_cell"]), key
+
+
+@pytest.mark.parametrize("case", G.redist_cases())
+def test_redistribute_numpy(case):
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, periodic = f["topology"], f["box"], bool(f["periodic"])
+    pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
+    if bool(f["alias"]):
+        data = pos
+    elif f["r0_data"].dtype.names and "pos" in f["r0_data"].dtype.names and "view" in case:
+        data = [d.copy() for d in G.per_rank(f, "data", size)]
+        pos = [d["pos"] for d in data]
+    else:
+        data = G.per_rank(f, "data", size)
+    outs = ro.redistribute_by_position_all_ranks(topo, box, size, data, pos, periodic)
+    for r in range(size):
+        assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), (case, r)
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
+
+
+@pytest.mark.parametrize("case", G.redist_cases())
+def test_redistribute_c(case):
+    """C binning + C stable partition + source-ordered concat == reference."""
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, periodic = f["topology"], f["box"], bool(f["periodic"])
+    sends = []
+    for r in range(size):
+        pin = f[f"r{r}_pos_in"].copy()
+        cell = c_oracle.bin_positions(pin, topo, box, periodic=periodic)
+        assert G.same_bytes(pin, f[f"r{r}_pos_out"]), (case, r)
+        assert np.array_equal(cell, f[f"r{r}_cell"]), (case, r)
+        if bool(f["alias"]):
+            data = pin
+        elif "view" in case:
+            data = f[f"r{r}_data"].copy()
+            data["pos"] = pin
+        else:
+            data = f[f"r{r}_data"]
+        part, off = c_oracle.partition(data, cell, size)
+        sends.append([part[off[d]:off[d + 1]] for d in range(size)])
+    for r in range(size):
+        out = np.concatenate([sends[s][r] for s in range(size)])
+        assert G.same_bytes(out, f[f"r{r}_out"]), (case, r)
+
+
+def test_cell_number_redistribute():
+    f = G.load("cellnum_p5_f32mat.npz")
+    size = int(f["size"])
+    outs = ro.redistribute_by_cell_number_all_ranks(size, G.per_rank(f, "data", size),
+                                                    G.per_rank(f, "ids", size))
+    for r in range(size):
+        assert G.same_bytes(outs[r], f[f"r{r}_out"])
+
+
+def test_geometry():
+    g = G.load("geometry.npz")
+    i = 0
+    while f"g{i}_size" in g:
+        size = int(g[f"g{i}_size"])
+        for r in range(size):
+            geo = ro.Geometry(g[f"g{i}_topology"], g[f"g{i}_box"], size, r)
+            assert np.array_equal(geo.cell_index_offset, g[f"g{i}_r{r}_offset"])
+            assert G.same_bytes(geo.cell_length, g[f"g{i}_r{r}_cell_length"])
+            assert np.array_equal(geo.rank_cell_index, g[f"g{i}_r{r}_rank_cell_index"])
+            assert G.same_bytes(geo.rank_cell_limits, g[f"g{i}_r{r}_rank_cell_limits"])
+            ncell = int(np.prod(geo.grid_topology))
+            assert np.array_equal(ro.indexes_from_cell_number(geo, np.arange(ncell)),
+                                  g[f"g{i}_r{r}_indexes_from_cell"])
+            probe = np.array([[-1] * geo.dim, [3] * geo.dim, [0] * geo.dim])
+            assert np.array_equal(ro.cell_number_from_indexes(geo, probe, periodic=False),
+                                  g[f"g{i}_r{r}_cellnum_nonper"])
+        i += 1
+    assert i == 5
+
+
+def test_synth_numpy_matches_c():
+    p_np = ro.synth_uniform(20261015, 12345, 1000, 3, 1.0)
+    p_c, ids = c_oracle.synth_uniform(20261015, 12345, 1000, 3, 1.0)
+    assert G.same_bytes(p_np, p_c)
+    assert np.array_equal(ids, np.arange(12345, 13345))
+    assert p_np.min() >= 0 and p_np.max() < 1
+
+
+def test_partition_matches_masks():
+    rng = np.random.default_rng(1)
+    data = rng.integers(0, 1 << 30, (5000, 3)).astype(np.int64)
+    dest = rng.integers(-1, 9, 5000)
+    out, off = c_oracle.partition(data, dest, 8)
+    ref = np.concatenate(ro.stable_split(data, dest, 8))
+    assert G.same_bytes(out, ref)
+    out2, off2 = ro.stable_partition(data, dest, 8)
+    assert G.same_bytes(out2, ref) and np.array_equal(off, off2)
