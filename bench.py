@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark: particles redistributed/sec (whole node), HBM / xGMI roofline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+One step = one pass of the hot path over one batch of synthetic particles
+already resident in HBM (SURVEY §8d generator, generated on the device):
+  N = 1  BASELINE config 2: 64M (2^26) uniform particles, 2x2x2 virtual
+         subdomains, local bin + scan + stable pack (no exchange);
+         positions (N,3) f64 wrapped in place, payload 32-byte records
+         [x, y, z f64, id i64].
+  N > 1  BASELINE config 3 per GPU: 1B/8 = 125M particles per GPU (weak
+         scaling), one GPU per grid cell (2x1x1, 2x2x1, 2x2x2), the full
+         MPIGridRedistributor.redistribute_by_position: bin, scan, RCCL count
+         all-to-all, pack, RCCL grouped send/recv over xGMI.
+
+Rank 0 prints ONE JSON line.  ``roofline`` is the dominant kernel's
+algorithmic bytes per launch over its average launch
+time, measured with HIP events on its own stream during the timed steps;
+``cpu_baseline`` times the NumPy restatement of the reference algorithm
+(oracle/, the checker) on a bounded sample on this host's cores (N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_PEAK_GBS = 7 * 153.0        # per GPU: 7 links x ~153 GB/s (task statement)
+SEED = 20261015
+N_CFG2 = 1 << 26                 # config 2: 64M on one GPU
+N_CFG3_PER_GPU = 1_000_000_000 // 8  # config 3: 1B over 8 GPUs
+
+# Algorithmic bytes per particle, 24-byte f64 positions,
+# 32-byte records, 1-byte destinations:
+BYTES_PER_PARTICLE = {
+    "bin_count": 24 + 24 + 1,    # read pos, write wrapped pos, write dest
+    "pack": 1 + 32 + 32,         # read dest, read record, write record
+}
+
+
+def topology_for(n):
+    dims = [1, 1, 1]
+    k = 0
+    while int(np.prod(dims)) < n:
+        dims[k % 3] *= 2
+        k += 1
+    assert int(np.prod(dims)) == n, f"--gpus {n} must be a power of two"
+    return dims
+
+
+def cpu_baseline(seconds_budget=10.0):
+    """NumPy restatement of the reference path (oracle/, 1 core): in-place
+    wrap + bin, one mask pass per destination, concatenate (redist.py:157-199),
+    on 2x2x2 destinations, timed on a bounded sample."""
+    from oracle import redist_oracle as ro
+
+    n = 1 << 22
+    pos = ro.synth_uniform(SEED, 0, n, 3, 1.0)
+    rec = np.zeros(n, dtype=[("x", "f8"), ("y", "f8"), ("z", "f8"), ("id", "i8")])
+    rec["x"], rec["y"], rec["z"] = pos.T
+    rec["id"] = np.arange(n)
+    geo = ro.Geometry([2, 2, 2], [1.0, 1.0, 1.0], 8, 0)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        cell = ro.cell_number_from_position(geo, pos)
+        parts = ro.stable_split(rec, cell, 8)
+        np.concatenate(parts)
+        done += n
+        el = time.perf_counter() - t0
+        if el > seconds_budget or done >= 8 * n:
+            break
+    return {"value": done / el, "unit": "particles/s", "cores": 1, "kind": "port",
+            "sample": f"{done // n} x {n} uniform particles, 2x2x2 destinations, f64 (N,3) "
+                      f"positions + 32-byte records, numpy {np.__version__} single thread, "
+                      f"{el:.1f} s"}
+
+
+def load_traffic(kernel, workload):
+    """HBM bytes/launch from a committed rocprofv3 PMC pass (profiles/traffic.json)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+        e = t.get(workload, {}).get(kernel)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=0, help="particles per GPU (default: config size)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import mpi_grid_redistribute_amd as mgr
+    from mpi_grid_redistribute_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if world == 1:
+        n = args.n or N_CFG2
+        workload = "cfg2_64M_uniform_2x2x2_local_partition"
+        part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
+        pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=0)
+        flat = rec.reshape(-1)
+
+        def step():
+            part.partition_device(flat, 32, pos)
+    else:
+        n = args.n or N_CFG3_PER_GPU
+        workload = "cfg3_uniform_per_gpu_125M_full_exchange"
+        comm = mgr.RcclComm.from_torch_distributed()
+        topo = topology_for(world)
+        R = mgr.MPIGridRedistributor(comm, topo, [1.0, 1.0, 1.0])
+        pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=rank * n)
+
+        def step():
+            R.redistribute_by_position(rec, pos)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kernels = {}
+    for k in ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack"):
+        ms, cnt = _lib.profile_read(k)
+        if cnt:
+            kernels[k] = {"avg_ms": ms / cnt, "launches": cnt}
+    dom = max(("bin_count", "pack"), key=lambda k: kernels.get(k, {"avg_ms": 0})["avg_ms"])
+    avg_s = kernels[dom]["avg_ms"] / 1e3
+    alg_bytes = BYTES_PER_PARTICLE[dom] * n
+    achieved = alg_bytes / avg_s / 1e9
+    for k in ("bin_count", "pack"):
+        if k in kernels:
+            kernels[k]["alg_GBps"] = BYTES_PER_PARTICLE[k] * n / (kernels[k]["avg_ms"] / 1e3) / 1e9
+    traffic = load_traffic(dom, workload)
+
+    total = n * world * args.steps
+    value = total / elapsed
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline()
+        line = {
+            "metric": "particles redistributed/sec (whole node)",
+            "value": value, "unit": "particles/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (splitmix64 uniform, generated on device)",
+            "config": {"workload": workload, "particles_per_gpu": n,
+                       "grid": topology_for(world) if world > 1 else [2, 2, 2],
+                       "payload_bytes": 32, "position": "(N,3) float64, wrapped in place",
+                       "parallelism": f"{world} rank(s), one GPU per grid cell" if world > 1
+                       else "1 GPU, 8 virtual subdomains"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes},
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

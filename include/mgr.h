@@ -1,0 +1,190 @@
+/*
+ * mgr.h -- C ABI of libmgr.so, the MI355X (gfx950) particle -> Cartesian grid
+ * of ranks redistribution library.
+ *
+ * Drop-in boundary for the hot path of dkorytov/mpi_grid_redistribute
+ * (redist.py).  The reference is pure Python (mpi4py + numpy); its "FFI" for
+ * this path is the set of numpy/mpi4py calls listed per entry point below.
+ * The package's Python layer (mpi_grid_redistribute_amd/) keeps the reference
+ * API (MPIGridRedistributor, redistribute_by_position, ...) and binds exactly
+ * these symbols with ctypes.  No torch types cross this boundary: device
+ * buffers are plain pointers (hipMalloc'd or torch-owned), sizes are int64,
+ * streams are hipStream_t passed as void*.
+ *
+ * Conventions
+ *   - every function returns int: MGR_OK (0) or a negative mgr_status; the
+ *     message of the last failure on the calling thread is mgr_last_error();
+ *   - everything that takes a stream is stream-ordered and asynchronous: no
+ *     host synchronisation, no allocation (graph-capturable), except
+ *     mgr_comm_* creation and the explicitly synchronous helpers noted below;
+ *   - workspaces are caller-owned device memory sized by mgr_workspace_bytes;
+ *   - a plan is immutable after creation and may be shared by streams; one
+ *     workspace must not be used by two in-flight calls at once.
+ */
+#ifndef MGR_H_
+#define MGR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGR_MAX_DIM 8
+#define MGR_MAX_BINS 4096
+#define MGR_UNIQUE_ID_BYTES 128
+
+typedef enum {
+    MGR_OK = 0,
+    MGR_EINVAL = -1,      /* bad argument (shape, dtype, size)             */
+    MGR_EHIP = -2,        /* HIP runtime error                             */
+    MGR_ERCCL = -3,       /* RCCL error                                    */
+    MGR_EUNSUPPORTED = -4 /* valid request this build does not implement   */
+} mgr_status;
+
+typedef enum {
+    MGR_F32 = 1,
+    MGR_F64 = 2,
+    MGR_I32 = 3,
+    MGR_I64 = 4
+} mgr_dtype;
+
+typedef struct mgr_plan mgr_plan; /* grid geometry of one rank            */
+typedef struct mgr_comm mgr_comm; /* native RCCL communicator (one/GPU)    */
+
+const char* mgr_last_error(void);
+const char* mgr_version(void);
+
+/* ---------------------------------------------------------------- plan --
+ * Replaces MPIGridRedistributor.__init__ (redist.py:16-61): row-major cell
+ * offsets (redist.py:53-58), the box and topology.  box_dtype is the numpy
+ * dtype of the caller's box_length (redist.py:46): with float32 positions a
+ * float32 box makes the wrap and the quotient float32 (numpy promotion), any
+ * other combination computes in float64 (S9, S11a).  nbins = number of
+ * destinations = comm size (redist.py:42, :196); cells >= nbins are invalid
+ * (redist.py:43-44 asserts prod(topology) <= size).                        */
+int mgr_plan_create(int dim, const int64_t* grid_topology, const double* box_length,
+                    int box_dtype, int nbins, mgr_plan** out);
+int mgr_plan_destroy(mgr_plan* plan);
+
+/* Rows per tile used by the histogram / pack kernels for rows of at most
+ * max_row_bytes bytes and nbins destinations (multiple of 256).            */
+int mgr_tile_rows(int64_t max_row_bytes, int nbins);
+/* Device workspace for n rows, nbins bins (incl. a drop bin if any).       */
+int64_t mgr_workspace_bytes(int64_t n, int nbins, int tile_rows);
+/* Byte width of the per-row destination array for nbins bins: 1, 2 or 4.  */
+int mgr_dest_bytes(int nbins);
+
+/* ------------------------------------------------- binning (hot path) --
+ * redist.py:157 -> get_cell_number_from_position (:87-90)
+ *   -> get_cell_indexes_from_position (:63-71): per coordinate
+ *      t = ((x % L) + L) % L written back IN PLACE (:68, :328-329) when
+ *      periodic, then trunc(t / L * n) (:69-70)
+ *   -> get_cell_number_from_indexes(periodic=True) (:73-85, :90): floor-mod
+ *      wrap of every index and the row-major dot.
+ * Bit-exact with numpy 2.2.6 (NaN/out-of-range bins
+ * like x86's INT64_MIN).  pos: n rows, row r coordinate d at
+ * pos[r*row_stride + d] (elements), dtype MGR_F32 or MGR_F64.
+ *
+ * mgr_bin_count : writes dest[r] (mgr_dest_bytes(nbins) wide) and the per
+ *                 tile histogram into the workspace; feeds mgr_scan.
+ * mgr_cell_ids  : writes int64 cell ids (and optionally (n,dim) int64 cell
+ *                 indexes, get_cell_indexes_from_position's output) only.  */
+int mgr_bin_count(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
+                  int periodic, void* dest, int tile_rows, void* workspace, void* stream);
+int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
+                 int periodic, int64_t* cell_out, int64_t* idx_out, void* stream);
+
+/* redist.py:169-198 (redistribute_by_cell_number): caller-supplied rank
+ * ids (MGR_I32/MGR_I64/MGR_F32/MGR_F64); ids outside [0, nbins) -- and
+ * non-integral float ids -- go to the drop bin nbins, never sent (S6).
+ * The histogram has nbins+1 bins; pass nbins+1 to scan/pack.               */
+int mgr_bin_ids(const mgr_plan* plan, const void* ids, int ids_dtype, int64_t n, void* dest,
+                int tile_rows, void* workspace, void* stream);
+
+/* get_cell_number_from_indexes (redist.py:73-85) on device: idx (n,dim)
+ * int64.  periodic: floor-mod wrap (:83-84); else plain dot, and the
+ * reference's range check (:78-81, '&' bug) selects nothing.             */
+int mgr_cell_number_from_indexes(const mgr_plan* plan, const int64_t* idx, int64_t n,
+                                 int periodic, int64_t* cell_out, void* stream);
+
+/* ---------------------------------------------------------------- scan --
+ * Device-wide exclusive scan of the destination-major tile histogram:
+ * segment start of every (bin, tile), bin starts, and per-bin totals
+ * (bin_counts, int64[nbins], device) = the element counts of the
+ * reference's send_buff[i] (redist.py:195-198).                           */
+int mgr_scan(int64_t n, int nbins, int tile_rows, void* workspace, int64_t* bin_counts,
+             void* stream);
+
+/* ---------------------------------------------------------------- pack --
+ * Stable partition of n rows of row_bytes (opaque bytes, redist.py:197
+ * data[rank_to_send==i] for every i, S6/S8) into dst, bin-major, original
+ * order kept inside each bin.  Rows of bin drop_bin (or -1: none) are not
+ * written.  Rows of redirect_bin (or -1) are written to redirect_dst
+ * starting at its row 0 instead (the self segment goes straight into the
+ * caller's output).  Call once per field; all fields share dest/workspace. */
+int mgr_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
+             int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
+             void* redirect_dst, void* stream);
+
+/* One call = bin_count + scan + pack of one field: the 1-GPU local stage
+ * (bin + scan + stable pack, BASELINE config 2).  bin_offsets: int64
+ * [nbins+1] device.                                                       */
+int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n,
+                              int64_t row_stride, int periodic, const void* src,
+                              int64_t row_bytes, void* dst, void* dest, int64_t* bin_counts,
+                              int tile_rows, void* workspace, void* stream);
+/* bin starts (int64[nbins+1], device) left in the workspace by mgr_scan.   */
+int mgr_bin_starts(int64_t n, int nbins, int tile_rows, const void* workspace,
+                   const int64_t** out);
+
+/* ------------------------------------------------------------ exchange --
+ * Replaces comm.alltoall(send_buff) + np.concatenate (redist.py:199):
+ * RCCL over xGMI, one process per GPU.  The unique id is made on one rank
+ * and broadcast by the caller (any channel).  mgr_comm_create is
+ * collective and synchronous; it binds the current HIP device.            */
+int mgr_comm_unique_id(void* out_id /* MGR_UNIQUE_ID_BYTES */);
+int mgr_comm_create(const void* id, int nranks, int rank, mgr_comm** out);
+int mgr_comm_destroy(mgr_comm* comm);
+int mgr_comm_rank(const mgr_comm* comm);
+int mgr_comm_size(const mgr_comm* comm);
+
+/* All-to-all of one int64 per peer (the count row): recv[s] = send_of_s[me]. */
+int mgr_exchange_counts(mgr_comm* comm, const int64_t* send_counts, int64_t* recv_counts,
+                        void* stream);
+
+/* Grouped ncclSend/ncclRecv of nfields packed, bin-major fields.  Counts and
+ * offsets are in ROWS and live on the host.  Rows from source s land at
+ * recv[f] + recv_offsets[s]*row_bytes[f]: source order (S7).  skip_self:
+ * the self segment is already in place (mgr_pack redirect), else it is
+ * copied device-to-device on the stream.                                  */
+int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void* const* recv,
+                      const int64_t* row_bytes, const int64_t* send_counts,
+                      const int64_t* send_offsets, const int64_t* recv_counts,
+                      const int64_t* recv_offsets, int skip_self, void* stream);
+/* Element-wise max all-reduce of count doubles (bench timing, barriers).   */
+int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,
+                               void* stream);
+
+/* ------------------------------------------------------- synthetic data --
+ * SURVEY §8d counter-based generator: u = (splitmix64(seed ^ (3*gid+d))
+ * >> 11) * 2^-53, pos[i*dim+d] = u * box[d], gid = gid0 + i; optional
+ * 32-byte records [x, y, z (f64), id (i64)] (dim must be 3).             */
+int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const double* box,
+                      double* pos, void* rec32, void* stream);
+
+/* ----------------------------------------------------------- profiling --
+ * Per-kernel HIP-event timing of every launch made while enabled, on the
+ * launch's own stream.  mgr_profile_read synchronises those events and
+ * returns the accumulated device time (ms) and launch count of the named
+ * kernel ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack",
+ * "cell_ids", "bin_ids", "synth").                                         */
+int mgr_profile_enable(int on);
+int mgr_profile_reset(void);
+int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGR_H_ */

@@ -1,0 +1,37 @@
+"""mpi_grid_redistribute_amd -- MI355X-native particle -> Cartesian grid of
+ranks redistribution (drop-in for dkorytov/mpi_grid_redistribute redist.py).
+
+    from mpi_grid_redistribute_amd import MPIGridRedistributor, RcclComm
+    comm = RcclComm.from_torch_distributed()          # one process per GPU
+    R = MPIGridRedistributor(comm, [2, 2, 2], [1.0, 1.0, 1.0])
+    local = R.redistribute_by_position(data, position)   # position wrapped in place
+
+Compute: hand-written gfx950 HIP kernels in libmgr.so (C ABI include/mgr.h);
+exchange: native RCCL grouped send/recv.  No CPU fallback.
+"""
+from . import _lib
+from .comm import MpiHostComm, RcclComm, SelfComm, TorchDistComm, Transport
+from .redistributor import GridPartitioner, MPIGridRedistributor, mpi_grid_redistribute
+
+__all__ = ["MPIGridRedistributor", "GridPartitioner", "mpi_grid_redistribute", "RcclComm",
+           "SelfComm", "MpiHostComm", "TorchDistComm", "Transport"]
+__version__ = "0.1.0"
+
+
+def synth_uniform(n, seed=20261015, gid0=0, dim=3, box=1.0, records=True, stream=None):
+    """Device-side SURVEY §8d generator: (positions (n,dim) f64, 32-byte
+    records [x,y,z,id] as an (n,32) uint8 tensor or None) on the GPU."""
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    _lib.require_gpu()
+    b = np.ascontiguousarray(np.broadcast_to(np.asarray(box, dtype=np.float64), (dim,)))
+    pos = torch.empty((n, dim), dtype=torch.float64, device="cuda")
+    rec = torch.empty((n, 32), dtype=torch.uint8, device="cuda") if records else None
+    _lib.call("mgr_synth_uniform", ctypes.c_uint64(seed), int(gid0), int(n), int(dim),
+              b.ctypes.data_as(ctypes.c_void_p), _lib.ptr(pos), _lib.ptr(rec),
+              _lib.stream_handle(stream))
+    torch.cuda.current_stream().synchronize()
+    return pos, rec

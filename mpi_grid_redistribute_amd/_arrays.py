@@ -1,0 +1,170 @@
+"""Adapters between caller arrays (torch GPU/CPU tensors, numpy arrays) and
+the flat device byte buffers the kernels take.
+
+The reference accepts numpy arrays indexed along axis 0 with any dtype,
+structured records included (redist.py:126-129, S8), and mutates ``position``
+in place (redist.py:68, S1).  Here:
+  * torch tensors already on the GPU are used in place (zero copies);
+  * numpy arrays / CPU tensors are staged to the GPU and the results (and
+    the in-place position write-back) are copied back, so a numpy caller of
+    the reference sees the same objects change.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_POS_CODES = {torch.float32: _lib.MGR_F32, torch.float64: _lib.MGR_F64}
+_ID_CODES = {torch.int32: _lib.MGR_I32, torch.int64: _lib.MGR_I64, torch.float32: _lib.MGR_F32,
+             torch.float64: _lib.MGR_F64}
+
+
+def device():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def is_device_tensor(x):
+    return isinstance(x, torch.Tensor) and x.is_cuda
+
+
+class Rows:
+    """A payload field: n rows of row_bytes opaque bytes on the device."""
+
+    def __init__(self, obj, dev):
+        self.obj = obj
+        if isinstance(obj, torch.Tensor):
+            if obj.dim() == 0:
+                raise ValueError("data must have at least one dimension (rows on axis 0)")
+            self.kind = "torch"
+            self.dtype, self.trailing = obj.dtype, tuple(obj.shape[1:])
+            t = obj if obj.is_cuda else obj.to(dev)
+            t = t.contiguous()
+            self.n = int(t.shape[0])
+            self.row_bytes = int(t.element_size() * int(np.prod(self.trailing, dtype=np.int64)))
+            self.flat = t.reshape(-1).view(torch.uint8) if t.numel() else torch.empty(
+                0, dtype=torch.uint8, device=dev)
+            self.out_device = obj.device
+        else:
+            a = np.asarray(obj)
+            if a.ndim == 0:
+                raise ValueError("data must have at least one dimension (rows on axis 0)")
+            if a.dtype.hasobject:
+                raise TypeError("object-dtype payloads are not supported (rows are moved as "
+                                "bytes); the reference pickles them")
+            self.kind = "numpy"
+            self.dtype, self.trailing = a.dtype, tuple(a.shape[1:])
+            self.host = a
+            self.contig = np.ascontiguousarray(a)
+            self.n = int(a.shape[0])
+            self.row_bytes = int(a.dtype.itemsize * int(np.prod(self.trailing, dtype=np.int64)))
+            flat = self.contig.reshape(-1).view(np.uint8) if a.size else np.zeros(0, np.uint8)
+            self.flat = torch.from_numpy(flat).to(dev)
+        if self.row_bytes == 0 and self.n:
+            raise ValueError("zero-byte rows")
+
+    def wrap(self, flat_out, m):
+        """Output of m rows in the caller's type (new array, redist.py:199)."""
+        if self.kind == "torch":
+            if m == 0:
+                return torch.empty((0,) + self.trailing, dtype=self.dtype, device=self.out_device)
+            t = flat_out.view(self.dtype).reshape((m,) + self.trailing)
+            return t if self.out_device.type == "cuda" else t.to(self.out_device)
+        host = flat_out.cpu().numpy() if m else np.zeros(0, np.uint8)
+        return host.view(self.dtype).reshape((m,) + self.trailing)
+
+    def write_back_host(self):
+        """numpy payload whose bytes were mutated on the device (position alias)."""
+        if self.kind == "numpy" and self.n:
+            dev_bytes = self.flat.cpu().numpy()
+            np.copyto(self.host, dev_bytes.view(self.dtype).reshape(self.host.shape))
+
+
+class Positions:
+    """(N, >=dim) float32/float64 positions as (device pointer, row stride).
+
+    ``finish()`` must run right after the binning kernel: it makes the
+    caller's array hold the wrapped values (S1) before anything reads it."""
+
+    def __init__(self, obj, dim, dev, data_rows: Rows | None = None):
+        self.obj = obj
+        self._copy_back = None
+        self._alias_rows = None
+        if isinstance(obj, torch.Tensor):
+            if obj.dim() != 2 or obj.shape[1] < dim:
+                raise ValueError(f"position must be (N, >= {dim}), got {tuple(obj.shape)}")
+            if obj.dtype not in _POS_CODES:
+                raise TypeError(f"position dtype {obj.dtype} not supported (float32/float64)")
+            t = obj
+            if not t.is_cuda or t.stride(1) != 1 or t.stride(0) < dim:
+                t = obj.to(dev).contiguous()
+                self._copy_back = ("torch", t)
+            self.t = t
+            self.n = int(t.shape[0])
+            self.stride = int(t.stride(0)) if self.n else dim
+            self.code = _POS_CODES[t.dtype]
+            self.addr = t.data_ptr()
+            return
+        a = obj
+        if not isinstance(a, np.ndarray):
+            raise TypeError("position must be a numpy array or a torch tensor")
+        if a.ndim != 2 or a.shape[1] < dim:
+            raise ValueError(f"position must be (N, >= {dim}), got {a.shape}")
+        if a.dtype not in (np.float32, np.float64):
+            raise TypeError(f"position dtype {a.dtype} not supported (float32/float64)")
+        self.n = int(a.shape[0])
+        self.code = _lib.MGR_F32 if a.dtype == np.float32 else _lib.MGR_F64
+        isz = a.dtype.itemsize
+        if (data_rows is not None and data_rows.kind == "numpy" and self.n
+                and np.shares_memory(a, data_rows.host)):
+            base = data_rows.host
+            off = a.__array_interface__["data"][0] - base.__array_interface__["data"][0]
+            ok = (base.flags.c_contiguous and off >= 0 and off % isz == 0
+                  and a.strides[1] == isz and a.strides[0] % isz == 0 and a.strides[0] > 0)
+            if not ok:
+                raise NotImplementedError("position overlaps data in a layout other than a "
+                                          "row-strided view of a C-contiguous data array")
+            # the kernels read/write the positions inside the device copy of data
+            self.addr = data_rows.flat.data_ptr() + off
+            self.stride = a.strides[0] // isz
+            self._alias_rows = data_rows
+            self.t = None
+            return
+        c = np.ascontiguousarray(a)
+        self.t = torch.from_numpy(c).to(dev)
+        self.stride = int(a.shape[1])
+        self.addr = self.t.data_ptr()
+        self._copy_back = ("numpy", a)
+
+    def finish(self):
+        if self._copy_back is None:
+            if self._alias_rows is not None:
+                self._alias_rows.write_back_host()
+            return
+        kind, target = self._copy_back
+        if kind == "torch":
+            if target is not self.obj:
+                self.obj.copy_(target)
+        else:
+            np.copyto(target, self.t.cpu().numpy())
+
+
+def id_array(obj, dev):
+    """rank_to_send as a device tensor of a kernel-supported dtype."""
+    t = obj if isinstance(obj, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(obj))
+    if t.dtype == torch.bool:
+        t = t.to(torch.int64)
+    elif t.dtype not in _ID_CODES:
+        t = t.to(torch.float64 if t.is_floating_point() else torch.int64)
+    t = t.to(dev).contiguous().reshape(-1)
+    return t, _ID_CODES[t.dtype]
+
+
+def box_dtype_code(box: np.ndarray):
+    """numpy dtype of box_length -> how numpy promotes the position math (S9, S11a)."""
+    if box.dtype in (np.float16, np.float32):
+        return _lib.MGR_F32
+    if np.issubdtype(box.dtype, np.floating):
+        return _lib.MGR_F64
+    return _lib.MGR_I64

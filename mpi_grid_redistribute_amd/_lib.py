@@ -1,0 +1,127 @@
+"""ctypes binding of libmgr.so (C ABI: include/mgr.h).
+
+The HIP library is the only compute path: if it is missing or cannot be
+loaded, every entry point raises -- there is no CPU or eager fallback.
+``torch`` is imported first on purpose: torch ships its own libamdhip64 /
+librccl, and loading it first makes libmgr.so bind to the same HIP runtime
+and RCCL instance (same SONAMEs) instead of a second copy.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmgr.so")
+
+MGR_OK = 0
+MGR_F32, MGR_F64, MGR_I32, MGR_I64 = 1, 2, 3, 4
+UNIQUE_ID_BYTES = 128
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+
+# name: (restype, argtypes) -- mirrors include/mgr.h one for one.
+SIGNATURES = {
+    "mgr_last_error": (ctypes.c_char_p, []),
+    "mgr_version": (ctypes.c_char_p, []),
+    "mgr_plan_create": (_I, [_I, _P, _P, _I, _I, ctypes.POINTER(_P)]),
+    "mgr_plan_destroy": (_I, [_P]),
+    "mgr_tile_rows": (_I, [_I64, _I]),
+    "mgr_workspace_bytes": (_I64, [_I64, _I, _I]),
+    "mgr_dest_bytes": (_I, [_I]),
+    "mgr_bin_count": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P]),
+    "mgr_cell_ids": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P]),
+    "mgr_bin_ids": (_I, [_P, _P, _I, _I64, _P, _I, _P, _P]),
+    "mgr_cell_number_from_indexes": (_I, [_P, _P, _I64, _I, _P, _P]),
+    "mgr_scan": (_I, [_I64, _I, _I, _P, _P, _P]),
+    "mgr_pack": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P]),
+    "mgr_partition_by_position": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I64, _P, _P, _P, _I,
+                                       _P, _P]),
+    "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
+    "mgr_comm_unique_id": (_I, [_P]),
+    "mgr_comm_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
+    "mgr_comm_destroy": (_I, [_P]),
+    "mgr_comm_rank": (_I, [_P]),
+    "mgr_comm_size": (_I, [_P]),
+    "mgr_exchange_counts": (_I, [_P, _P, _P, _P]),
+    "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "mgr_comm_allreduce_max_f64": (_I, [_P, _P, _P, _I64, _P]),
+    "mgr_synth_uniform": (_I, [ctypes.c_uint64, _I64, _I64, _I, _P, _P, _P, _P]),
+    "mgr_profile_enable": (_I, [_I]),
+    "mgr_profile_reset": (_I, []),
+    "mgr_profile_read": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _PI64]),
+}
+
+
+class MgrError(RuntimeError):
+    """A libmgr.so call returned a negative status."""
+
+
+_lib = None
+
+
+def load():
+    """Load libmgr.so (raises if it was not built -- run __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libmgr.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != MGR_OK:
+        msg = load().mgr_last_error().decode(errors="replace")
+        raise MgrError(f"{what} failed ({rc}): {msg}")
+    return rc
+
+
+def call(name, *args):
+    return check(getattr(load(), name)(*args), name)
+
+
+def require_gpu():
+    """The product path runs on the MI355X only; refuse loudly otherwise."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("mpi_grid_redistribute_amd needs a ROCm GPU (MI355X, gfx950); "
+                           "there is no CPU fallback")
+    load()
+
+
+def stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    """Device address of a torch tensor (None -> NULL)."""
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+# --------------------------------------------------------------- profiler
+def profile_enable(on=True):
+    call("mgr_profile_enable", int(bool(on)))
+
+
+def profile_reset():
+    call("mgr_profile_reset")
+
+
+def profile_read(kernel):
+    ms = ctypes.c_double(0.0)
+    cnt = ctypes.c_int64(0)
+    call("mgr_profile_read", kernel.encode(), ctypes.byref(ms), ctypes.byref(cnt))
+    return ms.value, cnt.value

@@ -1,0 +1,245 @@
+"""Communicators: the ``comm`` object ``MPIGridRedistributor`` is built on.
+
+The reference takes an mpi4py communicator and uses ``Get_rank`` /
+``Get_size`` (redist.py:41-42) and the pickle-based lowercase ``alltoall``
+(redist.py:199).  Here a communicator is a *transport* with two exchange
+steps of the redistribution:
+
+  exchange_counts(send_counts)   -> the count row all-to-all (host copies)
+  exchange_rows(...)             -> the packed segments, landing in the
+                                    output at source-ordered offsets (S7)
+
+Implementations
+  RcclComm       the product path: one process per GPU, a native RCCL
+                 communicator owned by libmgr.so (grouped ncclSend/ncclRecv
+                 over xGMI); created from torch.distributed or a unique id.
+  SelfComm       a single rank (size 1): no transport at all.
+  MpiHostComm    wraps any mpi4py-style comm (``alltoall(list)``): device
+                 segments are staged through host memory.  Lets a reference
+                 user keep mpi4py; slow, correctness only.
+  TorchDistComm  torch.distributed all_to_all_single (gloo on CPU tensors
+                 for the multi-process host-logic tests; works on nccl too).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def excl_cumsum(counts):
+    out = np.zeros(len(counts), dtype=np.int64)
+    if len(counts) > 1:
+        np.cumsum(counts[:-1], out=out[1:])
+    return out
+
+
+class Transport:
+    """Interface.  ``skips_self`` True means the transport never touches the
+    self segment, so the pack may write it straight into the output."""
+
+    rank = 0
+    size = 1
+    skips_self = True
+
+    def Get_rank(self):  # mpi4py duck type (redist.py:41)
+        return self.rank
+
+    def Get_size(self):  # redist.py:42
+        return self.size
+
+    def exchange_counts(self, send_counts):
+        """send_counts: int64 tensor [size] (device or host).
+        Returns (send_counts_host, recv_counts_host) as int64 numpy arrays."""
+        raise NotImplementedError
+
+    def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets):
+        """sends/outs: per-field uint8 tensors; counts/offsets in rows (host)."""
+        raise NotImplementedError
+
+    def barrier(self):
+        pass
+
+
+class SelfComm(Transport):
+    """One rank, one GPU (or N virtual destinations on one GPU)."""
+
+    def exchange_counts(self, send_counts):
+        s = send_counts.detach().to("cpu").numpy().astype(np.int64)
+        return s, s.copy()
+
+    def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets):
+        return  # the pack wrote the self segment into the output
+
+
+class RcclComm(Transport):
+    """Native RCCL communicator (libmgr.so ``mgr_comm_*``), one process per GPU.
+
+    ``RcclComm.from_torch_distributed()`` makes the unique id on rank 0 and
+    broadcasts it over the default torch.distributed group (any backend).
+    """
+
+    skips_self = True
+
+    def __init__(self, unique_id: bytes, size: int, rank: int, device=None):
+        _lib.require_gpu()
+        if device is not None:
+            torch.cuda.set_device(device)
+        assert len(unique_id) == _lib.UNIQUE_ID_BYTES
+        self.size, self.rank = int(size), int(rank)
+        buf = ctypes.create_string_buffer(unique_id, _lib.UNIQUE_ID_BYTES)
+        h = ctypes.c_void_p()
+        _lib.call("mgr_comm_create", buf, self.size, self.rank, ctypes.byref(h))
+        self._h = h
+        self._pinned = torch.empty(2 * self.size, dtype=torch.int64, pin_memory=True)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(_lib.UNIQUE_ID_BYTES)
+        _lib.call("mgr_comm_unique_id", buf)
+        return buf.raw
+
+    @classmethod
+    def from_torch_distributed(cls, group=None):
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls(obj[0], size, rank)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.call("mgr_comm_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def exchange_counts(self, send_counts):
+        stream = _lib.stream_handle()
+        recv = torch.empty_like(send_counts)
+        _lib.call("mgr_exchange_counts", self._h, _lib.ptr(send_counts), _lib.ptr(recv), stream)
+        P = self.size
+        self._pinned[:P].copy_(send_counts, non_blocking=True)
+        self._pinned[P:].copy_(recv, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        host = self._pinned.numpy().copy()
+        return host[:P], host[P:]
+
+    def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets):
+        nf = len(sends)
+        P = ctypes.c_void_p * nf
+        I64 = ctypes.c_int64
+        sp = P(*[s.data_ptr() for s in sends])
+        rp = P(*[o.data_ptr() for o in outs])
+        rb = (I64 * nf)(*row_bytes)
+        arr = lambda a: (I64 * self.size)(*[int(x) for x in a])  # noqa: E731
+        _lib.call("mgr_exchange_rows", self._h, nf, sp, rp, rb, arr(send_counts),
+                  arr(send_offsets), arr(recv_counts), arr(recv_offsets), 1, _lib.stream_handle())
+
+    def allreduce_max(self, values):
+        t = torch.as_tensor(values, dtype=torch.float64, device="cuda").reshape(-1)
+        out = torch.empty_like(t)
+        _lib.call("mgr_comm_allreduce_max_f64", self._h, _lib.ptr(t), _lib.ptr(out), t.numel(),
+                  _lib.stream_handle())
+        return out.cpu().numpy()
+
+    def barrier(self):
+        self.allreduce_max([0.0])
+
+
+class MpiHostComm(Transport):
+    """Any mpi4py-like communicator: counts and rows move with its lowercase
+    ``alltoall`` (list indexed by destination -> list indexed by source,
+    redist.py:199), staged through host memory."""
+
+    skips_self = True
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.rank, self.size = comm.Get_rank(), comm.Get_size()
+
+    def exchange_counts(self, send_counts):
+        s = send_counts.detach().to("cpu").numpy().astype(np.int64)
+        r = self.comm.alltoall([int(x) for x in s])
+        return s, np.asarray(r, dtype=np.int64)
+
+    def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets):
+        for f, (snd, out) in enumerate(zip(sends, outs)):
+            rb = row_bytes[f]
+            host = snd.detach().to("cpu").numpy() if snd.numel() else np.zeros(0, np.uint8)
+            lst = []
+            for p in range(self.size):
+                if p == self.rank:
+                    lst.append(np.zeros(0, np.uint8))
+                else:
+                    a = send_offsets[p] * rb
+                    lst.append(host[a:a + send_counts[p] * rb].copy())
+            got = self.comm.alltoall(lst)
+            for s in range(self.size):
+                if s == self.rank or recv_counts[s] == 0:
+                    continue
+                a = recv_offsets[s] * rb
+                out[a:a + recv_counts[s] * rb].copy_(torch.from_numpy(np.ascontiguousarray(got[s])),
+                                                     non_blocking=False)
+
+    def barrier(self):
+        self.comm.alltoall([0] * self.size)
+
+
+class TorchDistComm(Transport):
+    """torch.distributed all_to_all_single (gloo for CPU tests, nccl on GPUs).
+    The self segment travels with the collective, so the pack does not
+    redirect it (``skips_self`` False)."""
+
+    skips_self = False
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist, self.group = dist, group
+        self.rank, self.size = dist.get_rank(group), dist.get_world_size(group)
+
+    def exchange_counts(self, send_counts):
+        recv = torch.empty_like(send_counts)
+        self.dist.all_to_all_single(recv, send_counts.contiguous(), group=self.group)
+        return (send_counts.detach().cpu().numpy().astype(np.int64),
+                recv.detach().cpu().numpy().astype(np.int64))
+
+    def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets):
+        for f, (snd, out) in enumerate(zip(sends, outs)):
+            rb = row_bytes[f]
+            in_split = [int(c) * rb for c in send_counts]
+            out_split = [int(c) * rb for c in recv_counts]
+            # the packed send buffer is bin-major from row 0, so split sizes are enough
+            nsend = int(sum(in_split))
+            self.dist.all_to_all_single(out[: int(sum(out_split))], snd[:nsend].contiguous(),
+                                        output_split_sizes=out_split, input_split_sizes=in_split,
+                                        group=self.group)
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+
+def as_transport(comm):
+    """Accept our transports, any mpi4py-like comm, or None (single rank)."""
+    if comm is None:
+        return SelfComm()
+    if isinstance(comm, Transport):
+        return comm
+    if hasattr(comm, "alltoall") and hasattr(comm, "Get_rank") and hasattr(comm, "Get_size"):
+        if comm.Get_size() == 1:
+            return SelfComm()
+        return MpiHostComm(comm)
+    raise TypeError(f"unsupported communicator {type(comm)!r}: pass an RcclComm, SelfComm, "
+                    "TorchDistComm or an mpi4py-style comm")

@@ -1,0 +1,436 @@
+// C ABI of libmgr.so (include/mgr.h): argument validation, plans,
+// workspaces, the RCCL exchange, and the per-kernel HIP-event profiler.
+#include <math.h>
+#include <rccl/rccl.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mgr_internal.h"
+
+#define MGR_VERSION_STRING "mgr 0.1.0 (gfx950)"
+
+// ------------------------------------------------------------- errors
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_OK(expr)                                                                  \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(MGR_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                        __FILE__, __LINE__);                                          \
+    } while (0)
+
+#define NCCL_OK(expr)                                                                 \
+    do {                                                                              \
+        ncclResult_t r_ = (expr);                                                     \
+        if (r_ != ncclSuccess)                                                        \
+            return fail(MGR_ERCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_),   \
+                        __FILE__, __LINE__);                                          \
+    } while (0)
+
+struct mgr_plan {
+    mgr::Geom g;
+};
+
+struct mgr_comm {
+    ncclComm_t nccl;
+    int rank, size;
+};
+
+// ----------------------------------------------------------- profiler
+namespace mgr {
+namespace {
+struct ProfRec {
+    int kid;
+    hipEvent_t a, b;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_pending;
+std::vector<hipEvent_t> g_pool;
+double g_ms[K_NUM_KERNELS];
+int64_t g_cnt[K_NUM_KERNELS];
+thread_local hipEvent_t t_open = nullptr;
+
+hipEvent_t take_event() {
+    if (!g_pool.empty()) {
+        hipEvent_t e = g_pool.back();
+        g_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void collect_locked() {
+    for (auto& r : g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_ms[r.kid] += ms;
+            g_cnt[r.kid] += 1;
+        }
+        g_pool.push_back(r.a);
+        g_pool.push_back(r.b);
+    }
+    g_pending.clear();
+}
+}  // namespace
+
+const char* kernel_name(int k) {
+    static const char* names[K_NUM_KERNELS] = {"bin_count", "scan_reduce", "scan_apply",
+                                               "bin_totals", "pack", "cell_ids",
+                                               "bin_ids", "cellnum_idx", "synth"};
+    return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
+}
+
+void prof_begin(hipStream_t s, int) {
+    if (!g_prof_on) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    t_open = take_event();
+    if (t_open) (void)hipEventRecord(t_open, s);
+}
+
+void prof_end(hipStream_t s, int k) {
+    if (!g_prof_on || !t_open) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    hipEvent_t b = take_event();
+    if (!b) return;
+    (void)hipEventRecord(b, s);
+    g_pending.push_back({k, t_open, b});
+    t_open = nullptr;
+    if (g_pending.size() > 4096) collect_locked();
+}
+}  // namespace mgr
+
+// ============================================================== C ABI
+extern "C" {
+
+const char* mgr_last_error(void) { return g_err.c_str(); }
+const char* mgr_version(void) { return MGR_VERSION_STRING; }
+
+int mgr_plan_create(int dim, const int64_t* topo, const double* box, int box_dtype, int nbins,
+                    mgr_plan** out) {
+    if (!out || !topo || !box) return fail(MGR_EINVAL, "null argument");
+    if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d not in [1, %d]", dim, MGR_MAX_DIM);
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d not in [1, %d]", nbins, MGR_MAX_BINS);
+    if (box_dtype != MGR_F32 && box_dtype != MGR_F64 && box_dtype != MGR_I64 && box_dtype != MGR_I32)
+        return fail(MGR_EINVAL, "box_dtype %d", box_dtype);
+    mgr::Geom g;
+    memset(&g, 0, sizeof g);
+    g.dim = dim;
+    g.nbins = nbins;
+    g.nbits = mgr::nbits_for(nbins);
+    g.compute_f32 = box_dtype == MGR_F32;
+    int64_t prod = 1;
+    for (int d = dim - 1; d >= 0; --d) {
+        if (topo[d] < 1) return fail(MGR_EINVAL, "grid_topology[%d] = %lld < 1", d, (long long)topo[d]);
+        g.off[d] = prod;
+        prod *= topo[d];
+        if (prod > nbins)
+            return fail(MGR_EINVAL, "topology needs %lld ranks, have %d (redist.py:43-44)",
+                        (long long)prod, nbins);
+    }
+    for (int d = 0; d < dim; ++d) {
+        const double L = box[d];
+        g.L[d] = L;
+        g.twoL[d] = L + L;
+        g.fast[d] = (L > 0.0) && isfinite(L + L);
+        const float Lf = (float)L;
+        g.Lf[d] = Lf;
+        g.twoLf[d] = Lf + Lf;
+        g.fastf[d] = (Lf > 0.0f) && isfinite(Lf + Lf);
+        g.n[d] = topo[d];
+        g.nd[d] = (double)topo[d];
+    }
+    mgr_plan* p = new mgr_plan;
+    p->g = g;
+    *out = p;
+    return MGR_OK;
+}
+
+int mgr_plan_destroy(mgr_plan* plan) {
+    delete plan;
+    return MGR_OK;
+}
+
+int mgr_tile_rows(int64_t max_row_bytes, int nbins) {
+    if (max_row_bytes < 1) max_row_bytes = 1;
+    return mgr::pack_tile_rows(max_row_bytes, nbins);
+}
+
+int64_t mgr_workspace_bytes(int64_t n, int nbins, int tile_rows) {
+    if (n < 0 || nbins < 1 || tile_rows < mgr::kBlock) return -1;
+    return mgr::workspace_bytes(n, nbins, tile_rows);
+}
+
+int mgr_dest_bytes(int nbins) { return mgr::dest_bytes(nbins); }
+
+static int check_tile(int tile_rows) {
+    if (tile_rows < mgr::kBlock || tile_rows > mgr::kMaxTileRows || tile_rows % mgr::kBlock)
+        return fail(MGR_EINVAL, "tile_rows %d must be a multiple of %d in [%d, %d]", tile_rows,
+                    mgr::kBlock, mgr::kBlock, mgr::kMaxTileRows);
+    return MGR_OK;
+}
+
+static int check_pos(const mgr_plan* plan, const void* pos, int dtype, int64_t n, int64_t stride) {
+    if (!plan) return fail(MGR_EINVAL, "null plan");
+    if (dtype != MGR_F32 && dtype != MGR_F64)
+        return fail(MGR_EINVAL, "positions must be float32 or float64 (dtype %d)", dtype);
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    if (n > 0 && !pos) return fail(MGR_EINVAL, "null positions");
+    if (stride < plan->g.dim) return fail(MGR_EINVAL, "row_stride %lld < dim %d", (long long)stride, plan->g.dim);
+    return MGR_OK;
+}
+
+int mgr_bin_count(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
+                  int periodic, void* dest, int tile_rows, void* workspace, void* stream) {
+    int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
+    if (rc) return rc;
+    if ((rc = check_tile(tile_rows))) return rc;
+    if (n > 0 && (!dest || !workspace)) return fail(MGR_EINVAL, "null dest/workspace");
+    mgr::Geom g = plan->g;
+    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
+    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
+                                 tile_rows, ws, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
+                 int periodic, int64_t* cell_out, int64_t* idx_out, void* stream) {
+    int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
+    if (rc) return rc;
+    mgr::Geom g = plan->g;
+    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    HIP_OK(mgr::launch_cell_ids(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, cell_out,
+                                idx_out, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_bin_ids(const mgr_plan* plan, const void* ids, int ids_dtype, int64_t n, void* dest,
+                int tile_rows, void* workspace, void* stream) {
+    if (!plan) return fail(MGR_EINVAL, "null plan");
+    if (ids_dtype < MGR_F32 || ids_dtype > MGR_I64) return fail(MGR_EINVAL, "ids dtype %d", ids_dtype);
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (n > 0 && (!ids || !dest || !workspace)) return fail(MGR_EINVAL, "null argument");
+    if (plan->g.nbins + 1 > MGR_MAX_BINS) return fail(MGR_EINVAL, "too many bins");
+    const mgr::Workspace ws = mgr::carve(workspace, n, plan->g.nbins + 1, tile_rows);
+    HIP_OK(mgr::launch_bin_ids(ids, ids_dtype, n, plan->g.nbins, dest, tile_rows, ws,
+                               (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_cell_number_from_indexes(const mgr_plan* plan, const int64_t* idx, int64_t n,
+                                 int periodic, int64_t* cell_out, void* stream) {
+    if (!plan) return fail(MGR_EINVAL, "null plan");
+    if (n > 0 && (!idx || !cell_out)) return fail(MGR_EINVAL, "null argument");
+    HIP_OK(mgr::launch_cellnum_from_idx(plan->g, idx, n, periodic, cell_out, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_scan(int64_t n, int nbins, int tile_rows, void* workspace, int64_t* bin_counts,
+             void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (!workspace) return fail(MGR_EINVAL, "null workspace");
+    const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
+    HIP_OK(mgr::launch_scan(n, nbins, tile_rows, ws, bin_counts, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_bin_starts(int64_t n, int nbins, int tile_rows, const void* workspace,
+                   const int64_t** out) {
+    if (!workspace || !out) return fail(MGR_EINVAL, "null argument");
+    *out = mgr::carve((void*)workspace, n, nbins, tile_rows).bin_starts;
+    return MGR_OK;
+}
+
+int mgr_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
+             int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
+             void* redirect_dst, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (row_bytes < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes);
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (n > 0 && (!src || !dest || !workspace)) return fail(MGR_EINVAL, "null argument");
+    if (redirect_bin >= 0 && !redirect_dst) return fail(MGR_EINVAL, "redirect without buffer");
+    if (redirect_bin >= nbins) return fail(MGR_EINVAL, "redirect_bin out of range");
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
+    HIP_OK(mgr::launch_pack(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
+                            redirect_bin, redirect_dst, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n,
+                              int64_t row_stride, int periodic, const void* src,
+                              int64_t row_bytes, void* dst, void* dest, int64_t* bin_counts,
+                              int tile_rows, void* workspace, void* stream) {
+    int rc = mgr_bin_count(plan, pos, pos_dtype, n, row_stride, periodic, dest, tile_rows,
+                           workspace, stream);
+    if (rc) return rc;
+    rc = mgr_scan(n, plan->g.nbins, tile_rows, workspace, bin_counts, stream);
+    if (rc) return rc;
+    return mgr_pack(src, row_bytes, n, dest, plan->g.nbins, -1, tile_rows, workspace, dst, -1,
+                    nullptr, stream);
+}
+
+// ------------------------------------------------------------ exchange
+int mgr_comm_unique_id(void* out_id) {
+    if (!out_id) return fail(MGR_EINVAL, "null id");
+    ncclUniqueId id;
+    NCCL_OK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == MGR_UNIQUE_ID_BYTES, "unique id size");
+    memcpy(out_id, &id, sizeof id);
+    return MGR_OK;
+}
+
+int mgr_comm_create(const void* id, int nranks, int rank, mgr_comm** out) {
+    if (!id || !out) return fail(MGR_EINVAL, "null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(MGR_EINVAL, "rank %d of %d", rank, nranks);
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    ncclComm_t c;
+    NCCL_OK(ncclCommInitRank(&c, nranks, uid, rank));
+    mgr_comm* m = new mgr_comm;
+    m->nccl = c;
+    m->rank = rank;
+    m->size = nranks;
+    *out = m;
+    return MGR_OK;
+}
+
+int mgr_comm_destroy(mgr_comm* comm) {
+    if (!comm) return MGR_OK;
+    ncclResult_t r = ncclCommDestroy(comm->nccl);
+    delete comm;
+    if (r != ncclSuccess) return fail(MGR_ERCCL, "ncclCommDestroy: %s", ncclGetErrorString(r));
+    return MGR_OK;
+}
+
+int mgr_comm_rank(const mgr_comm* comm) { return comm ? comm->rank : -1; }
+int mgr_comm_size(const mgr_comm* comm) { return comm ? comm->size : -1; }
+
+int mgr_exchange_counts(mgr_comm* comm, const int64_t* send_counts, int64_t* recv_counts,
+                        void* stream) {
+    if (!comm || !send_counts || !recv_counts) return fail(MGR_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    NCCL_OK(ncclGroupStart());
+    for (int p = 0; p < comm->size; ++p) {
+        NCCL_OK(ncclSend(send_counts + p, 1, ncclInt64, p, comm->nccl, s));
+        NCCL_OK(ncclRecv(recv_counts + p, 1, ncclInt64, p, comm->nccl, s));
+    }
+    NCCL_OK(ncclGroupEnd());
+    return MGR_OK;
+}
+
+int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void* const* recv,
+                      const int64_t* row_bytes, const int64_t* send_counts,
+                      const int64_t* send_offsets, const int64_t* recv_counts,
+                      const int64_t* recv_offsets, int skip_self, void* stream) {
+    if (!comm || nfields < 1 || !send || !recv || !row_bytes || !send_counts || !send_offsets ||
+        !recv_counts || !recv_offsets)
+        return fail(MGR_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const int me = comm->rank;
+    bool any = false;
+    for (int p = 0; p < comm->size; ++p)
+        if (p != me && (send_counts[p] > 0 || recv_counts[p] > 0)) any = true;
+    if (any) {
+        NCCL_OK(ncclGroupStart());
+        // Peers in ring order starting after me spread the first wave of
+        // transfers over distinct xGMI links.
+        for (int j = 1; j < comm->size; ++j) {
+            const int to = (me + j) % comm->size;
+            const int from = (me - j + comm->size) % comm->size;
+            for (int f = 0; f < nfields; ++f) {
+                const int64_t rb = row_bytes[f];
+                if (send_counts[to] > 0)
+                    NCCL_OK(ncclSend((const char*)send[f] + send_offsets[to] * rb,
+                                     (size_t)(send_counts[to] * rb), ncclUint8, to, comm->nccl, s));
+                if (recv_counts[from] > 0)
+                    NCCL_OK(ncclRecv((char*)recv[f] + recv_offsets[from] * rb,
+                                     (size_t)(recv_counts[from] * rb), ncclUint8, from, comm->nccl, s));
+            }
+        }
+        NCCL_OK(ncclGroupEnd());
+    }
+    if (!skip_self && send_counts[me] > 0) {
+        for (int f = 0; f < nfields; ++f) {
+            const int64_t rb = row_bytes[f];
+            HIP_OK(hipMemcpyAsync((char*)recv[f] + recv_offsets[me] * rb,
+                                  (const char*)send[f] + send_offsets[me] * rb,
+                                  (size_t)(send_counts[me] * rb), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    return MGR_OK;
+}
+
+int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,
+                               void* stream) {
+    if (!comm || !in || !out || count < 0) return fail(MGR_EINVAL, "bad argument");
+    NCCL_OK(ncclAllReduce(in, out, (size_t)count, ncclFloat64, ncclMax, comm->nccl,
+                          (hipStream_t)stream));
+    return MGR_OK;
+}
+
+// ------------------------------------------------------ synthetic data
+int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const double* box,
+                      double* pos, void* rec32, void* stream) {
+    if (dim < 1 || dim > MGR_MAX_DIM || !box) return fail(MGR_EINVAL, "bad dim/box");
+    if (rec32 && dim != 3) return fail(MGR_EINVAL, "32-byte records need dim == 3");
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    HIP_OK(mgr::launch_synth_uniform(seed, gid0, n, dim, box, pos, rec32, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+// ------------------------------------------------------------ profiler
+int mgr_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(mgr::g_prof_mu);
+    if (!on) mgr::collect_locked();
+    mgr::g_prof_on = on != 0;
+    return MGR_OK;
+}
+
+int mgr_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(mgr::g_prof_mu);
+    mgr::collect_locked();
+    for (int k = 0; k < mgr::K_NUM_KERNELS; ++k) {
+        mgr::g_ms[k] = 0.0;
+        mgr::g_cnt[k] = 0;
+    }
+    return MGR_OK;
+}
+
+int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
+    if (!kernel) return fail(MGR_EINVAL, "null kernel name");
+    std::lock_guard<std::mutex> lk(mgr::g_prof_mu);
+    mgr::collect_locked();
+    for (int k = 0; k < mgr::K_NUM_KERNELS; ++k) {
+        if (strcmp(kernel, mgr::kernel_name(k)) == 0) {
+            if (total_ms) *total_ms = mgr::g_ms[k];
+            if (launches) *launches = mgr::g_cnt[k];
+            return MGR_OK;
+        }
+    }
+    return fail(MGR_EINVAL, "unknown kernel '%s'", kernel);
+}
+
+}  // extern "C"

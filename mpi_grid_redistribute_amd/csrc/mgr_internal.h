@@ -1,0 +1,74 @@
+// Internal declarations shared by mgr_kernels.hip and mgr_capi.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mgr.h"
+
+namespace mgr {
+
+constexpr int kBlock = 256;              // 4 waves of 64
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxTileRows = 4096;       // 16 rounds of 256 rows; spos fits uint16
+constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
+constexpr int kScanMaxBlocks = 1024;
+
+// Geometry of one plan, passed to kernels by value (kernarg segment).
+struct Geom {
+    int dim;
+    int compute_f32;                     // numpy f32 % f32 semantics (S9 note)
+    int nbins;
+    int nbits;                           // ceil(log2(nbins)) for the ballot match
+    int fast[MGR_MAX_DIM];               // L > 0 and 2L finite: [0,L) fast wrap is exact
+    int fastf[MGR_MAX_DIM];
+    double L[MGR_MAX_DIM];
+    double twoL[MGR_MAX_DIM];
+    float Lf[MGR_MAX_DIM];
+    float twoLf[MGR_MAX_DIM];
+    double nd[MGR_MAX_DIM];              // (double)n[d], the int64 multiplier promoted
+    int64_t n[MGR_MAX_DIM];
+    int64_t off[MGR_MAX_DIM];            // row-major offsets, last axis fastest (S4)
+};
+
+// Workspace carve for (n, nbins, tile_rows).
+struct Workspace {
+    int32_t* counts;     // [nbins][T] destination-major tile histogram
+    int64_t* offsets;    // [nbins][T] exclusive scan of counts
+    int64_t* bin_starts; // [nbins + 1]
+    int64_t* partials;   // [kScanMaxBlocks]
+    int64_t T;
+};
+int64_t num_tiles(int64_t n, int tile_rows);
+int64_t workspace_bytes(int64_t n, int nbins, int tile_rows);
+Workspace carve(void* base, int64_t n, int nbins, int tile_rows);
+int dest_bytes(int nbins);
+int nbits_for(int nbins);
+
+// Kernel ids for the profiler.
+enum KernelId { K_BIN_COUNT, K_SCAN_REDUCE, K_SCAN_APPLY, K_BIN_TOTALS, K_PACK, K_CELL_IDS,
+                K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_NUM_KERNELS };
+const char* kernel_name(int k);
+void prof_begin(hipStream_t s, int k);
+void prof_end(hipStream_t s, int k);
+
+// Launchers (return hipError_t of the launch; validate arguments before calling).
+hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+                            int periodic, void* dest, int tile_rows, const Workspace& ws,
+                            hipStream_t s);
+hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+                           int periodic, int64_t* cell, int64_t* idx, hipStream_t s);
+hipError_t launch_bin_ids(const void* ids, int ids_dtype, int64_t n, int nbins, void* dest,
+                          int tile_rows, const Workspace& ws, hipStream_t s);
+hipError_t launch_cellnum_from_idx(const Geom& g, const int64_t* idx, int64_t n, int periodic,
+                                   int64_t* cell, hipStream_t s);
+hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
+                       int64_t* bin_counts, hipStream_t s);
+hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                       int nbins, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                       int redirect_bin, void* redirect_dst, hipStream_t s);
+hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
+                                const double* box, double* pos, void* rec32, hipStream_t s);
+int pack_tile_rows(int64_t row_bytes, int nbins);
+
+}  // namespace mgr

@@ -1,0 +1,798 @@
+// HIP kernels for gfx950 (MI355X): wrap+bin+histogram, device-wide scan,
+// stable LDS-staged pack, id binning, synthetic input.
+//
+// Reference semantics (dkorytov/mpi_grid_redistribute, redist.py):
+//   wrap   ((x % L) + L) % L, numpy floor remainder, written back  :68, :328-329
+//   bin    trunc((t / L) * n) (x86 INT64_MIN on NaN/overflow)      :69-70
+//   cell   sum_d offset[d] * ((k % n) + n) % n, row-major           :53-58, :83-84
+//   split  data[rank_to_send == i], order kept                      :195-198
+// Every float operation below is IEEE-exact and ordered as in numpy (built
+// with -ffp-contract=off, no fast-math): the GPU results are bit-identical to
+// the reference (tests/test_gpu_parity.py).
+//
+// Work decomposition: a "tile" is tile_rows consecutive rows (a multiple of
+// 256), one 256-thread workgroup per tile.  Inside a tile, row i belongs to
+// round i / 256 and lane (i % 256): rounds, then waves, then lanes follow the
+// original row order, which is what makes the ballot ranks stable.
+
+#include "mgr_internal.h"
+
+#include <limits.h>
+
+#include <type_traits>
+
+namespace mgr {
+
+// ------------------------------------------------------------ scalar math
+__device__ __forceinline__ long long trunc_i64(double v) {
+    // numpy astype(int64) on x86 (cvttsd2si): NaN / out of range -> INT64_MIN (S10)
+    return (v >= -9223372036854775808.0 && v < 9223372036854775808.0) ? (long long)v : LLONG_MIN;
+}
+
+__device__ __forceinline__ double pymod(double a, double b) {
+    // numpy npy_remainder: floor remainder, sign of the divisor
+    double m = fmod(a, b);
+    if (b == 0.0) return m;
+    if (m != 0.0) {
+        if ((b < 0.0) != (m < 0.0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+
+__device__ __forceinline__ float pymodf(float a, float b) {
+    float m = fmodf(a, b);
+    if (b == 0.0f) return m;
+    if (m != 0.0f) {
+        if ((b < 0.0f) != (m < 0.0f)) m += b;
+    } else {
+        m = copysignf(0.0f, b);
+    }
+    return m;
+}
+
+// ((x % L) + L) % L.  Fast path for 0 <= x < L (every in-box particle):
+// x % L == x, y = x + L in [L, 2L], and fmod(y, L) == y - L exactly
+// (Sterbenz), 0 when y == 2L.  Bit-identical to the general path.
+__device__ __forceinline__ double wrap_f64(double x, double L, double twoL, int fast) {
+    if (fast && x >= 0.0 && x < L) {
+        const double y = x + L;
+        return (y == twoL) ? 0.0 : y - L;
+    }
+    return pymod(pymod(x, L) + L, L);
+}
+
+__device__ __forceinline__ float wrap_f32(float x, float L, float twoL, int fast) {
+    if (fast && x >= 0.0f && x < L) {
+        const float y = x + L;
+        return (y == twoL) ? 0.0f : y - L;
+    }
+    return pymodf(pymodf(x, L) + L, L);
+}
+
+__device__ __forceinline__ long long floormod_i64(long long a, long long n) {
+    if (n == 0 || n == -1) return 0;
+    long long r = a % n;
+    if (r != 0 && ((r < 0) != (n < 0))) r += n;
+    return r;
+}
+
+// One coordinate: wrap (+ write back), bin, index wrap.  Returns the wrapped
+// index; *raw gets trunc(t/L*n) before the index wrap (cell indexes API).
+template <typename PosT, bool kPeriodic>
+__device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw) {
+    long long k;
+    if (sizeof(PosT) == 4 && g.compute_f32) {
+        float x = (float)*p;
+        if (kPeriodic) {
+            x = wrap_f32(x, g.Lf[d], g.twoLf[d], g.fastf[d]);
+            *p = (PosT)x;
+        }
+        const float q = x / g.Lf[d];                 // f32 / f32 -> f32
+        k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
+    } else {
+        double x = (double)*p;
+        if (kPeriodic) {
+            const PosT w = (PosT)wrap_f64(x, g.L[d], g.twoL[d], g.fast[d]);  // f32: round (S9)
+            *p = w;
+            x = (double)w;                           // bin reads the written value (S2)
+        }
+        k = trunc_i64(x / g.L[d] * g.nd[d]);
+    }
+    if (raw) *raw = k;
+    const long long n = g.n[d];
+    if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
+    return k;
+}
+
+template <typename PosT, bool kPeriodic>
+__device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx) {
+    long long cell = 0;
+#pragma unroll
+    for (int d = 0; d < MGR_MAX_DIM; ++d) {
+        if (d < g.dim) cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr);
+    }
+    return cell;
+}
+
+// ------------------------------------------------------ wave primitives
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Lanes of this wave holding the same bin b (valid lanes only): nbits
+// ballots, one per bit of the bin id (gfx950 wave64 ballot + popc match).
+__device__ __forceinline__ unsigned long long match_bin(unsigned b, bool valid, int nbits) {
+    unsigned long long peers = __ballot(valid);
+    for (int i = 0; i < nbits; ++i) {
+        const bool bit = (b >> i) & 1u;
+        const unsigned long long m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return valid ? peers : 0ull;
+}
+
+__device__ __forceinline__ int rank_in(unsigned long long peers) {
+    const unsigned lo = (unsigned)peers, hi = (unsigned)(peers >> 32);
+    return __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+}
+
+// Block-wide exclusive scan of one int64 per thread (256 threads).
+__device__ __forceinline__ long long block_excl_scan(long long v, long long* total,
+                                                     long long* s_w /* [kWaves] */) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    long long pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) {
+        const long long t = s_w[i];
+        pre += (i < w) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
+// ----------------------------------------------------- bin + histogram
+// Kernel 1 of the hot path: reads positions, wraps + writes them back,
+// writes the destination of every row, and the tile's histogram
+// (destination-major counts[b * T + tile]).
+template <typename PosT, bool kPeriodic, typename DestT>
+__global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
+                                                           int64_t stride, Geom g,
+                                                           DestT* __restrict__ dest,
+                                                           int32_t* __restrict__ counts,
+                                                           int64_t T, int tile_rows) {
+    extern __shared__ __attribute__((aligned(16))) int32_t s_hist[];
+    const int64_t tile = blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    for (int b = threadIdx.x; b < g.nbins; b += kBlock) s_hist[b] = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < rows; i0 += kBlock) {
+        const int i = i0 + threadIdx.x;
+        const bool valid = i < rows;
+        unsigned b = 0;
+        if (valid) {
+            const int64_t r = row0 + i;
+            b = (unsigned)bin_row<PosT, kPeriodic>(pos + r * stride, g, nullptr);
+            dest[r] = (DestT)b;
+        }
+        const unsigned long long peers = match_bin(b, valid, g.nbits);
+        if (valid && rank_in(peers) == 0) atomicAdd(&s_hist[b], __popcll(peers));
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < g.nbins; b += kBlock) counts[(int64_t)b * T + tile] = s_hist[b];
+}
+
+// get_cell_number_from_position / get_cell_indexes_from_position (API helpers).
+template <typename PosT, bool kPeriodic>
+__global__ __launch_bounds__(kBlock) void cell_ids_kernel(PosT* __restrict__ pos, int64_t n,
+                                                          int64_t stride, Geom g,
+                                                          int64_t* __restrict__ cell,
+                                                          int64_t* __restrict__ idx) {
+    const int64_t step = (int64_t)gridDim.x * kBlock;
+    for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < n; r += step) {
+        long long* ip = idx ? (long long*)(idx + r * g.dim) : nullptr;
+        const long long c = bin_row<PosT, kPeriodic>(pos + r * stride, g, ip);
+        if (cell) cell[r] = c;
+    }
+}
+
+// redistribute_by_cell_number ids -> bin (out of range / non-integral -> drop bin).
+template <typename IdT, typename DestT>
+__global__ __launch_bounds__(kBlock) void bin_ids_kernel(const IdT* __restrict__ ids, int64_t n,
+                                                         int nbins, int nbits,
+                                                         DestT* __restrict__ dest,
+                                                         int32_t* __restrict__ counts, int64_t T,
+                                                         int tile_rows) {
+    extern __shared__ __attribute__((aligned(16))) int32_t s_hist[];
+    const int64_t tile = blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    const int nb = nbins + 1;
+    for (int b = threadIdx.x; b < nb; b += kBlock) s_hist[b] = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < rows; i0 += kBlock) {
+        const int i = i0 + threadIdx.x;
+        const bool valid = i < rows;
+        unsigned b = 0;
+        if (valid) {
+            const IdT v = ids[row0 + i];
+            bool ok;
+            if constexpr (std::is_floating_point<IdT>::value) {  // numpy float == int compare
+                ok = (v >= (IdT)0) && (v < (IdT)nbins) && (v == (IdT)(long long)v);
+            } else {
+                ok = (v >= 0) && ((long long)v < (long long)nbins);
+            }
+            b = ok ? (unsigned)(long long)v : (unsigned)nbins;
+            dest[row0 + i] = (DestT)b;
+        }
+        const unsigned long long peers = match_bin(b, valid, nbits);
+        if (valid && rank_in(peers) == 0) atomicAdd(&s_hist[b], __popcll(peers));
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kBlock) counts[(int64_t)b * T + tile] = s_hist[b];
+}
+
+__global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t* __restrict__ idx,
+                                                                  int64_t n, Geom g, int periodic,
+                                                                  int64_t* __restrict__ cell) {
+    const int64_t step = (int64_t)gridDim.x * kBlock;
+    for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < n; r += step) {
+        long long c = 0;
+        for (int d = 0; d < g.dim; ++d) {
+            long long k = idx[r * g.dim + d];
+            if (periodic) {
+                const long long nn = g.n[d];
+                k = floormod_i64(floormod_i64(k, nn) + nn, nn);
+            }
+            c += g.off[d] * k;   // non-periodic: '&' range check never fires (redist.py:80)
+        }
+        cell[r] = c;
+    }
+}
+
+// ------------------------------------------------------------------ scan
+__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const int32_t* __restrict__ counts,
+                                                             int64_t M, int64_t chunk,
+                                                             int64_t* __restrict__ partials) {
+    __shared__ long long s_w[kWaves];
+    const int64_t lo = blockIdx.x * chunk, hi = min(M, lo + chunk);
+    long long acc = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) acc += counts[i];
+    long long tot;
+    block_excl_scan(acc, &tot, s_w);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void scan_apply_kernel(const int32_t* __restrict__ counts,
+                                                            int64_t M, int64_t chunk,
+                                                            const int64_t* __restrict__ partials,
+                                                            int64_t* __restrict__ offsets, int64_t T,
+                                                            int64_t* __restrict__ bin_starts,
+                                                            int nbins) {
+    __shared__ long long s_w[kWaves];
+    long long carry = 0;
+    for (int j = threadIdx.x; j < (int)blockIdx.x; j += kBlock) carry += partials[j];
+    long long tot;
+    block_excl_scan(carry, &tot, s_w);
+    carry = tot;
+    const int64_t lo = blockIdx.x * chunk, hi = min(M, lo + chunk);
+    for (int64_t base = lo; base < hi; base += kBlock) {
+        const int64_t i = base + threadIdx.x;
+        const long long v = (i < hi) ? counts[i] : 0;
+        const long long ex = block_excl_scan(v, &tot, s_w) + carry;
+        if (i < hi) {
+            offsets[i] = ex;
+            if (i % T == 0) bin_starts[i / T] = ex;
+        }
+        carry += tot;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) bin_starts[nbins] = carry;
+}
+
+__global__ void bin_totals_kernel(const int64_t* __restrict__ bin_starts, int nbins,
+                                  int64_t* __restrict__ bin_counts) {
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x)
+        bin_counts[b] = bin_starts[b + 1] - bin_starts[b];
+}
+
+// ------------------------------------------------------------------ pack
+template <int W> struct Unit;
+template <> struct Unit<16> { using T = uint4; };
+template <> struct Unit<8> { using T = uint2; };
+template <> struct Unit<4> { using T = uint32_t; };
+template <> struct Unit<2> { using T = uint16_t; };
+template <> struct Unit<1> { using T = uint8_t; };
+
+// floor(u / d): multiply-high when every u of the tile satisfies u * d < 2^32
+// (m != 0), plain 64-bit division otherwise (very wide rows only).
+struct FastDiv {
+    uint64_t d;
+    uint32_t m;
+    __device__ __forceinline__ uint64_t div(uint64_t u) const {
+        if (d == 1) return u;
+        if (m) return __umulhi((uint32_t)u, m);
+        return u / d;
+    }
+};
+
+struct PackLayout {
+    // LDS carve of one pack workgroup (all offsets multiples of 16 bytes)
+    int sw;    // int64  [kWaves]  block-scan scratch
+    int cnt;   // uint16 [nb][RW]  counts, then scanned in place to sorted starts
+    int base;  // int32  [nb + 1]  first sorted slot of each bin in this tile
+    int goff;  // int64  [nb]      global row of the tile's segment per bin
+    int spos;  // uint16 [tile_rows] sorted slot of tile row i
+    int sbin;  // uint16 [tile_rows] bin of sorted slot s
+    int rows;  // bytes  [tile_rows * max(row_bytes, 4)] staged rows (aliased by the
+               //        uint32 bin|rank scratch of phase A-C)
+    int total;
+};
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+__host__ __device__ inline PackLayout pack_layout(int tile_rows, int64_t row_bytes, int nb,
+                                                  bool staged) {
+    PackLayout L;
+    const int RW = (tile_rows / kBlock) * kWaves;
+    int o = 0;
+    L.sw = o;   o += align16(kWaves * 8);
+    L.cnt = o;  o += align16(RW * nb * 2);
+    L.base = o; o += align16((nb + 1) * 4);
+    L.goff = o; o += align16(nb * 8);
+    L.spos = o; o += align16(tile_rows * 2);
+    L.sbin = o; o += align16(tile_rows * 2);
+    L.rows = o;
+    const int64_t rb = staged ? (row_bytes < 4 ? 4 : row_bytes) : 4;
+    o += align16((int)(tile_rows * rb));
+    L.total = o;
+    return L;
+}
+
+template <int W, typename DestT, bool kStaged>
+__global__ __launch_bounds__(kBlock) void pack_kernel(
+    const uint8_t* __restrict__ src, int64_t upr /* units per row */, FastDiv fd, int64_t n,
+    const DestT* __restrict__ dest, int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, PackLayout lay,
+    uint8_t* __restrict__ dst, int redirect_bin, uint8_t* __restrict__ redirect_dst) {
+    using U = typename Unit<W>::T;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint16_t* s_cnt = (uint16_t*)(smem + lay.cnt);
+    int32_t* s_base = (int32_t*)(smem + lay.base);
+    int64_t* s_goff = (int64_t*)(smem + lay.goff);
+    uint16_t* s_spos = (uint16_t*)(smem + lay.spos);
+    uint16_t* s_sbin = (uint16_t*)(smem + lay.sbin);
+    uint32_t* s_kr = (uint32_t*)(smem + lay.rows);   // phase A-C scratch
+    U* s_rows = (U*)(smem + lay.rows);               // phase D-E staging
+    long long* s_w = (long long*)(smem + lay.sw);
+
+    const int64_t tile = blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    const int R = (rows + kBlock - 1) / kBlock;
+    const int RW = (tile_rows / kBlock) * kWaves;
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+
+    for (int j = threadIdx.x; j < RW * nb; j += kBlock) s_cnt[j] = 0;
+    for (int b = threadIdx.x; b < nb; b += kBlock) {
+        int64_t g = offsets[(int64_t)b * T + tile];
+        if (b == redirect_bin) g -= bin_starts[b];
+        s_goff[b] = g;
+    }
+    __syncthreads();
+
+    // Phase A: per round, per wave: bin match -> stable rank inside the wave.
+    for (int r = 0; r < R; ++r) {
+        const int i = r * kBlock + threadIdx.x;
+        const bool valid = i < rows;
+        const unsigned b = valid ? (unsigned)dest[row0 + i] : 0u;
+        const unsigned long long peers = match_bin(b, valid, nbits);
+        const int rk = rank_in(peers);
+        if (valid) {
+            s_kr[i] = (b << 8) | (unsigned)rk;
+            if (rk == 0) s_cnt[b * RW + r * kWaves + w] = (uint16_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+
+    // Phase B: one exclusive scan over (bin, round, wave) in bin-major order
+    // gives each (round, wave, bin) group its first sorted slot in the tile.
+    {
+        const int M = RW * nb;
+        const int per = (M + kBlock - 1) / kBlock;
+        const int lo = threadIdx.x * per, hi = min(M, lo + per);
+        long long acc = 0;
+        for (int j = lo; j < hi; ++j) acc += s_cnt[j];
+        long long tot;
+        long long run = block_excl_scan(acc, &tot, s_w);
+        for (int j = lo; j < hi; ++j) {
+            const int c = s_cnt[j];
+            s_cnt[j] = (uint16_t)run;
+            run += c;
+        }
+        __syncthreads();
+        for (int b = threadIdx.x; b < nb; b += kBlock) s_base[b] = s_cnt[b * RW];
+        if (threadIdx.x == 0) s_base[nb] = rows;
+    }
+    __syncthreads();
+
+    // Phase C: sorted slot of every row.
+    for (int r = 0; r < R; ++r) {
+        const int i = r * kBlock + threadIdx.x;
+        if (i < rows) {
+            const uint32_t kr = s_kr[i];
+            const unsigned b = kr >> 8;
+            const int s = s_cnt[b * RW + r * kWaves + w] + (int)(kr & 0xffu);
+            s_spos[i] = (uint16_t)s;
+            s_sbin[s] = (uint16_t)b;
+        }
+    }
+    __syncthreads();
+    (void)lane;
+
+    const int64_t U_tile = (int64_t)rows * upr;
+    const U* __restrict__ src_tile = (const U*)(src + row0 * upr * W);
+    U* __restrict__ dst_u = (U*)dst;
+    U* __restrict__ red_u = (U*)redirect_dst;
+
+    if (kStaged) {
+        // Phase D: coalesced tile load, scattered into sorted order in LDS.
+        constexpr int kUnroll = 4;
+        for (int64_t u0 = threadIdx.x; u0 < U_tile; u0 += kBlock * kUnroll) {
+            U v[kUnroll];
+#pragma unroll
+            for (int j = 0; j < kUnroll; ++j) {
+                const int64_t u = u0 + j * kBlock;
+                if (u < U_tile) v[j] = src_tile[u];
+            }
+#pragma unroll
+            for (int j = 0; j < kUnroll; ++j) {
+                const int64_t u = u0 + j * kBlock;
+                if (u < U_tile) {
+                    const uint32_t row = (uint32_t)fd.div((uint64_t)u);
+                    const uint32_t k = (uint32_t)u - row * (uint32_t)upr;
+                    s_rows[(uint32_t)s_spos[row] * (uint32_t)upr + k] = v[j];
+                }
+            }
+        }
+        __syncthreads();
+        // Phase E: contiguous runs per bin -> coalesced stores.
+        for (int64_t su = threadIdx.x; su < U_tile; su += kBlock) {
+            const uint32_t srow = (uint32_t)fd.div((uint64_t)su);
+            const uint32_t k = (uint32_t)su - srow * (uint32_t)upr;
+            const int b = s_sbin[srow];
+            if (b == drop_bin) continue;
+            const int64_t grow = s_goff[b] + (int64_t)(srow - (uint32_t)s_base[b]);
+            U* o = (b == redirect_bin) ? red_u : dst_u;
+            o[grow * upr + k] = s_rows[su];
+        }
+    } else {
+        // Wide rows: copy straight from the source row to its slot.
+        for (int64_t u = threadIdx.x; u < U_tile; u += kBlock) {
+            const uint64_t row = fd.div((uint64_t)u);
+            const uint64_t k = (uint64_t)u - row * (uint64_t)upr;
+            const int s = s_spos[row];
+            const int b = s_sbin[s];
+            if (b == drop_bin) continue;
+            const int64_t grow = s_goff[b] + (int64_t)(s - s_base[b]);
+            U* o = (b == redirect_bin) ? red_u : dst_u;
+            o[grow * upr + k] = src_tile[u];
+        }
+    }
+}
+
+// --------------------------------------------------------- synthetic data
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+struct Box8 { double v[MGR_MAX_DIM]; };
+
+__global__ __launch_bounds__(kBlock) void synth_uniform_kernel(uint64_t seed, int64_t gid0,
+                                                               int64_t n, int dim, Box8 box,
+                                                               double* __restrict__ pos,
+                                                               double* __restrict__ rec) {
+    const int64_t step = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += step) {
+        const uint64_t gid = (uint64_t)(gid0 + i);
+        double c[MGR_MAX_DIM];
+#pragma unroll
+        for (int d = 0; d < MGR_MAX_DIM; ++d) {
+            if (d < dim) {
+                const uint64_t h = splitmix64(seed ^ (3ull * gid + (uint64_t)d));
+                c[d] = (double)(h >> 11) * 0x1.0p-53 * box.v[d];
+                if (pos) pos[i * dim + d] = c[d];
+            }
+        }
+        if (rec) {
+            double2* r2 = (double2*)(rec + i * 4);
+            r2[0] = make_double2(c[0], c[1]);
+            double2 t;
+            t.x = c[2];
+            long long id = (long long)gid;
+            t.y = __longlong_as_double(id);
+            r2[1] = t;
+        }
+    }
+}
+
+// ============================================================ launchers
+static int grid_for(int64_t n, int per_block_rows = kBlock) {
+    int64_t g = (n + per_block_rows - 1) / per_block_rows;
+    if (g > 256 * 16) g = 256 * 16;   // grid-stride beyond 16 blocks per CU
+    return (int)(g < 1 ? 1 : g);
+}
+
+int64_t num_tiles(int64_t n, int tile_rows) { return (n + tile_rows - 1) / tile_rows; }
+
+int dest_bytes(int nbins) { return nbins <= 256 ? 1 : (nbins <= 65536 ? 2 : 4); }
+
+int nbits_for(int nbins) {
+    int b = 0;
+    while ((1 << b) < nbins) ++b;
+    return b;
+}
+
+static int64_t a256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
+    const int64_t T = num_tiles(n, tile_rows);
+    const int64_t M = (int64_t)nbins * (T > 0 ? T : 1);
+    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) + a256(kScanMaxBlocks * 8);
+}
+
+Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
+    Workspace ws;
+    ws.T = num_tiles(n, tile_rows);
+    const int64_t M = (int64_t)nbins * (ws.T > 0 ? ws.T : 1);
+    char* p = (char*)base;
+    ws.counts = (int32_t*)p;     p += a256(M * 4);
+    ws.offsets = (int64_t*)p;    p += a256(M * 8);
+    ws.bin_starts = (int64_t*)p; p += a256((nbins + 1) * 8);
+    ws.partials = (int64_t*)p;
+    return ws;
+}
+
+template <typename K>
+static void ensure_lds(K kernel, int bytes) {
+    if (bytes > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+template <typename PosT, bool kP, typename DestT>
+static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
+                              int tile_rows, const Workspace& ws, hipStream_t s) {
+    auto k = bin_count_kernel<PosT, kP, DestT>;
+    const size_t lds = (size_t)g.nbins * 4;
+    ensure_lds(k, (int)lds);
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), lds, s, (PosT*)pos, n, stride, g,
+                       (DestT*)dest, ws.counts, ws.T, tile_rows);
+    return hipGetLastError();
+}
+
+template <typename PosT, typename DestT>
+static hipError_t bin_count_p(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
+                              void* dest, int tile_rows, const Workspace& ws, hipStream_t s) {
+    return periodic ? bin_count_t<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s)
+                    : bin_count_t<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s);
+}
+
+template <typename PosT>
+static hipError_t bin_count_d(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
+                              void* dest, int tile_rows, const Workspace& ws, hipStream_t s) {
+    switch (dest_bytes(g.nbins)) {
+        case 1: return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
+        case 2: return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
+        default: return bin_count_p<PosT, uint32_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
+    }
+}
+
+hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+                            int periodic, void* dest, int tile_rows, const Workspace& ws,
+                            hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_BIN_COUNT);
+    hipError_t e = pos_f32 ? bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s)
+                           : bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
+    prof_end(s, K_BIN_COUNT);
+    return e;
+}
+
+template <typename PosT>
+static hipError_t cell_ids_t(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
+                             int64_t* cell, int64_t* idx, hipStream_t s) {
+    const int grid = grid_for(n);
+    if (periodic)
+        hipLaunchKernelGGL((cell_ids_kernel<PosT, true>), dim3(grid), dim3(kBlock), 0, s,
+                           (PosT*)pos, n, stride, g, cell, idx);
+    else
+        hipLaunchKernelGGL((cell_ids_kernel<PosT, false>), dim3(grid), dim3(kBlock), 0, s,
+                           (PosT*)pos, n, stride, g, cell, idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+                           int periodic, int64_t* cell, int64_t* idx, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_CELL_IDS);
+    hipError_t e = pos_f32 ? cell_ids_t<float>(g, pos, n, stride, periodic, cell, idx, s)
+                           : cell_ids_t<double>(g, pos, n, stride, periodic, cell, idx, s);
+    prof_end(s, K_CELL_IDS);
+    return e;
+}
+
+template <typename IdT, typename DestT>
+static hipError_t bin_ids_t(const void* ids, int64_t n, int nbins, void* dest, int tile_rows,
+                            const Workspace& ws, hipStream_t s) {
+    auto k = bin_ids_kernel<IdT, DestT>;
+    const size_t lds = (size_t)(nbins + 1) * 4;
+    ensure_lds(k, (int)lds);
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), lds, s, (const IdT*)ids, n, nbins,
+                       nbits_for(nbins + 1), (DestT*)dest, ws.counts, ws.T, tile_rows);
+    return hipGetLastError();
+}
+
+template <typename IdT>
+static hipError_t bin_ids_d(const void* ids, int64_t n, int nbins, void* dest, int tile_rows,
+                            const Workspace& ws, hipStream_t s) {
+    switch (dest_bytes(nbins + 1)) {
+        case 1: return bin_ids_t<IdT, uint8_t>(ids, n, nbins, dest, tile_rows, ws, s);
+        case 2: return bin_ids_t<IdT, uint16_t>(ids, n, nbins, dest, tile_rows, ws, s);
+        default: return bin_ids_t<IdT, uint32_t>(ids, n, nbins, dest, tile_rows, ws, s);
+    }
+}
+
+hipError_t launch_bin_ids(const void* ids, int ids_dtype, int64_t n, int nbins, void* dest,
+                          int tile_rows, const Workspace& ws, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_BIN_IDS);
+    hipError_t e;
+    switch (ids_dtype) {
+        case MGR_I32: e = bin_ids_d<int32_t>(ids, n, nbins, dest, tile_rows, ws, s); break;
+        case MGR_I64: e = bin_ids_d<int64_t>(ids, n, nbins, dest, tile_rows, ws, s); break;
+        case MGR_F32: e = bin_ids_d<float>(ids, n, nbins, dest, tile_rows, ws, s); break;
+        default: e = bin_ids_d<double>(ids, n, nbins, dest, tile_rows, ws, s); break;
+    }
+    prof_end(s, K_BIN_IDS);
+    return e;
+}
+
+hipError_t launch_cellnum_from_idx(const Geom& g, const int64_t* idx, int64_t n, int periodic,
+                                   int64_t* cell, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_CELLNUM_IDX);
+    hipLaunchKernelGGL(cellnum_from_idx_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, idx, n, g,
+                       periodic, cell);
+    prof_end(s, K_CELLNUM_IDX);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
+                       int64_t* bin_counts, hipStream_t s) {
+    if (n <= 0 || ws.T == 0) {
+        hipError_t e = hipMemsetAsync(ws.bin_starts, 0, (size_t)(nbins + 1) * 8, s);
+        if (e == hipSuccess && bin_counts) e = hipMemsetAsync(bin_counts, 0, (size_t)nbins * 8, s);
+        return e;
+    }
+    const int64_t M = (int64_t)nbins * ws.T;
+    int64_t G = (M + 2047) / 2048;
+    if (G > kScanMaxBlocks) G = kScanMaxBlocks;
+    if (G < 1) G = 1;
+    int64_t chunk = (M + G - 1) / G;
+    G = (M + chunk - 1) / chunk;
+    prof_begin(s, K_SCAN_REDUCE);
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)G), dim3(kBlock), 0, s, ws.counts, M,
+                       chunk, ws.partials);
+    prof_end(s, K_SCAN_REDUCE);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    prof_begin(s, K_SCAN_APPLY);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)G), dim3(kBlock), 0, s, ws.counts, M,
+                       chunk, ws.partials, ws.offsets, ws.T, ws.bin_starts, nbins);
+    prof_end(s, K_SCAN_APPLY);
+    e = hipGetLastError();
+    if (e != hipSuccess || !bin_counts) return e;
+    prof_begin(s, K_BIN_TOTALS);
+    hipLaunchKernelGGL(bin_totals_kernel, dim3((nbins + 255) / 256), dim3(256), 0, s,
+                       ws.bin_starts, nbins, bin_counts);
+    prof_end(s, K_BIN_TOTALS);
+    return hipGetLastError();
+}
+
+int pack_tile_rows(int64_t row_bytes, int nbins) {
+    // Largest tile (multiple of 256, <= kMaxTileRows) whose staged LDS image
+    // fits kLdsBudget, so two pack workgroups share a CU; wide rows fall back
+    // to the unstaged copy with 2048-row tiles.
+    for (int tr = kMaxTileRows; tr >= kBlock; tr -= kBlock) {
+        if (pack_layout(tr, row_bytes, nbins, true).total <= kLdsBudget) return tr;
+    }
+    for (int tr = 2048; tr >= kBlock; tr -= kBlock) {
+        if (pack_layout(tr, row_bytes, nbins, false).total <= kLdsBudget) return tr;
+    }
+    return kBlock;
+}
+
+template <int W, typename DestT>
+static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
+                         int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                         int redirect_bin, void* redirect_dst, hipStream_t s) {
+    const int64_t upr = row_bytes / W;
+    FastDiv fd;
+    fd.d = (uint64_t)upr;
+    const unsigned __int128 umax = (unsigned __int128)tile_rows * (uint64_t)upr * (uint64_t)upr;
+    fd.m = (upr == 1 || umax >= ((unsigned __int128)1 << 32))
+               ? 0u : (uint32_t)((0x100000000ull + upr - 1) / upr);
+    const bool staged = pack_layout(tile_rows, row_bytes, nb, true).total <= 160 * 1024 - 64;
+    const PackLayout lay = pack_layout(tile_rows, row_bytes, nb, staged);
+    if (staged) {
+        auto k = pack_kernel<W, DestT, true>;
+        ensure_lds(k, lay.total);
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lay.total, s,
+                           (const uint8_t*)src, upr, fd, n, (const DestT*)dest, nb, nbits_for(nb),
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, lay,
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
+    } else {
+        auto k = pack_kernel<W, DestT, false>;
+        ensure_lds(k, lay.total);
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lay.total, s,
+                           (const uint8_t*)src, upr, fd, n, (const DestT*)dest, nb, nbits_for(nb),
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, lay,
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
+    }
+    return hipGetLastError();
+}
+
+template <int W>
+static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
+                         int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                         int redirect_bin, void* redirect_dst, hipStream_t s) {
+    switch (dest_bytes(nb)) {
+        case 1: return pack_t<W, uint8_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+        case 2: return pack_t<W, uint16_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+        default: return pack_t<W, uint32_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    }
+}
+
+hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                       int nbins, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                       int redirect_bin, void* redirect_dst, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    // Widest unit dividing the row and every base address.
+    uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
+    if (redirect_dst) a |= (uintptr_t)redirect_dst;
+    prof_begin(s, K_PACK);
+    hipError_t e;
+    if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    prof_end(s, K_PACK);
+    return e;
+}
+
+hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
+                                const double* box, double* pos, void* rec32, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    Box8 b;
+    for (int d = 0; d < MGR_MAX_DIM; ++d) b.v[d] = d < dim ? box[d] : 0.0;
+    prof_begin(s, K_SYNTH);
+    hipLaunchKernelGGL(synth_uniform_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, seed, gid0, n,
+                       dim, b, pos, (double*)rec32);
+    prof_end(s, K_SYNTH);
+    return hipGetLastError();
+}
+
+}  // namespace mgr

@@ -24,13 +24,14 @@ from __future__ import annotations
 import importlib.util
 import os
 import sys
-import threading
 import types
 
 import numpy as np
 
 REF_PATH = "/root/reference/redist.py"
 OUT_DIR = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(OUT_DIR))
+from fake_mpi import run_ranks  # noqa: E402  (threaded mpi4py stand-in)
 
 
 def load_reference():
@@ -47,57 +48,6 @@ def load_reference():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     return mod
-
-
-class FakeWorld:
-    def __init__(self, size):
-        self.size = size
-        self.barrier = threading.Barrier(size)
-        self.slots = [None] * size
-
-
-class FakeComm:
-    """mpi4py-comm duck type: Get_rank/Get_size/alltoall (redist.py:41-42, :199)."""
-
-    def __init__(self, world, rank):
-        self.world, self.rank = world, rank
-
-    def Get_rank(self):
-        return self.rank
-
-    def Get_size(self):
-        return self.world.size
-
-    def alltoall(self, sendobj):
-        w = self.world
-        assert len(sendobj) == w.size
-        w.slots[self.rank] = [np.array(x, copy=True) for x in sendobj]  # pickle == copy
-        w.barrier.wait()
-        out = [w.slots[s][self.rank] for s in range(w.size)]
-        w.barrier.wait()
-        return out
-
-
-def run_ranks(size, fn):
-    world = FakeWorld(size)
-    results = [None] * size
-    errors = []
-
-    def body(r):
-        try:
-            results[r] = fn(FakeComm(world, r), r)
-        except BaseException as e:  # pragma: no cover
-            errors.append((r, e))
-            world.barrier.abort()
-
-    th = [threading.Thread(target=body, args=(r,)) for r in range(size)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    if errors:
-        raise errors[0][1]
-    return results
 
 
 class SingleComm:

@@ -1,0 +1,87 @@
+"""CPU checks of the C ABI: libmgr.so loads and exports every symbol that
+include/mgr.h declares; host-only entry points behave (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mgr.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mgr_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from mpi_grid_redistribute_amd import _lib
+    return _lib.load()
+
+
+def test_header_declares_api():
+    fns = header_functions()
+    assert "mgr_bin_count" in fns and "mgr_pack" in fns and "mgr_exchange_rows" in fns
+    assert len(fns) >= 25
+
+
+def test_every_declared_symbol_exported(lib):
+    from mpi_grid_redistribute_amd import _lib
+    for name in header_functions():
+        assert hasattr(lib, name), name
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+    assert set(_lib.SIGNATURES) == set(header_functions())
+
+
+def test_library_is_gfx950():
+    so = os.path.join(ROOT, "mpi_grid_redistribute_amd", "libmgr.so")
+    blob = open(so, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_host_only_entry_points(lib):
+    assert lib.mgr_version().startswith(b"mgr ")
+    assert lib.mgr_dest_bytes(8) == 1 and lib.mgr_dest_bytes(300) == 2
+    tr = lib.mgr_tile_rows(32, 8)
+    assert tr % 256 == 0 and 256 <= tr <= 4096
+    assert lib.mgr_workspace_bytes(1 << 20, 8, tr) > 0
+    assert lib.mgr_workspace_bytes(-1, 8, tr) < 0
+
+
+def test_plan_validation(lib):
+    import numpy as np
+    topo = np.array([2, 2, 2], dtype=np.int64)
+    box = np.array([1.0, 1.0, 1.0])
+    h = ctypes.c_void_p()
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert lib.mgr_plan_create(3, vp(topo), vp(box), 2, 8, ctypes.byref(h)) == 0
+    assert lib.mgr_plan_destroy(h) == 0
+    # topology needs 8 ranks, only 7 (redist.py:43-44)
+    rc = lib.mgr_plan_create(3, vp(topo), vp(box), 2, 7, ctypes.byref(h))
+    assert rc < 0 and b"ranks" in lib.mgr_last_error()
+    rc = lib.mgr_plan_create(0, vp(topo), vp(box), 2, 8, ctypes.byref(h))
+    assert rc < 0
+
+
+def test_profiler_names(lib):
+    from mpi_grid_redistribute_amd import _lib
+    _lib.profile_reset()
+    for k in ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack", "synth"):
+        ms, cnt = _lib.profile_read(k)
+        assert cnt == 0 and ms == 0.0
+    with pytest.raises(_lib.MgrError):
+        _lib.profile_read("nope")
+
+
+def test_product_refuses_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import mpi_grid_redistribute_amd as m
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m.MPIGridRedistributor(None, [2], [1.0])
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m.GridPartitioner([2], [1.0])
