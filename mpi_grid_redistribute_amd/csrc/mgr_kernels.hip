@@ -29,10 +29,56 @@ __device__ __forceinline__ long long trunc_i64(double v) {
     return (v >= -9223372036854775808.0 && v < 9223372036854775808.0) ? (long long)v : LLONG_MIN;
 }
 
+// ---- x86/glibc NaN semantics (numpy runs on x86: SSE + glibc fmod) ----
+// An invalid operation (fmod(inf, L), fmod(x, 0), inf - inf) yields the x86
+// "default NaN" -- sign bit SET (0xFFF8... / 0xFFC00000); a NaN operand
+// propagates quieted, first operand first.  The GPU's own default NaN is
+// positive, so these cases are spelled out bit by bit.  They only occur on
+// the slow path (non-finite input or box), never for in-box particles.
+constexpr unsigned long long kDefaultNaN64 = 0xFFF8000000000000ull;
+constexpr unsigned kDefaultNaN32 = 0xFFC00000u;
+
+__device__ __forceinline__ double quiet64(double x) {
+    return __longlong_as_double(__double_as_longlong(x) | 0x0008000000000000ll);
+}
+__device__ __forceinline__ float quiet32(float x) {
+    return __uint_as_float(__float_as_uint(x) | 0x00400000u);
+}
+// cvtss2sd / cvtsd2ss on NaN: keep sign, quiet, shift the payload.
+__device__ __forceinline__ double f32_to_f64_x86(float x) {
+    if (!isnan(x)) return (double)x;
+    const unsigned u = __float_as_uint(x) | 0x00400000u;
+    const unsigned long long b = ((unsigned long long)(u >> 31) << 63) | 0x7FF0000000000000ull |
+                                 ((unsigned long long)(u & 0x007FFFFFu) << 29);
+    return __longlong_as_double((long long)b);
+}
+__device__ __forceinline__ float f64_to_f32_x86(double x) {
+    if (!isnan(x)) return (float)x;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x) | 0x0008000000000000ull;
+    const unsigned u = ((unsigned)(b >> 63) << 31) | 0x7F800000u | (unsigned)((b >> 29) & 0x007FFFFFu);
+    return __uint_as_float(u);
+}
+
+__device__ __forceinline__ double fmod_x86(double a, double b) {
+    if (isnan(a)) return quiet64(a);
+    if (isnan(b)) return quiet64(b);
+    if (isinf(a) || b == 0.0) return __longlong_as_double((long long)kDefaultNaN64);
+    if (isinf(b)) return a;
+    return fmod(a, b);  // finite / finite nonzero: exact
+}
+__device__ __forceinline__ float fmodf_x86(float a, float b) {
+    if (isnan(a)) return quiet32(a);
+    if (isnan(b)) return quiet32(b);
+    if (isinf(a) || b == 0.0f) return __uint_as_float(kDefaultNaN32);
+    if (isinf(b)) return a;
+    return fmodf(a, b);
+}
+
+// numpy npy_remainder: floor remainder, sign of the divisor.  A NaN result
+// is final: every later x86 operation propagates it unchanged.
 __device__ __forceinline__ double pymod(double a, double b) {
-    // numpy npy_remainder: floor remainder, sign of the divisor
-    double m = fmod(a, b);
-    if (b == 0.0) return m;
+    double m = fmod_x86(a, b);
+    if (b == 0.0 || isnan(m)) return m;
     if (m != 0.0) {
         if ((b < 0.0) != (m < 0.0)) m += b;
     } else {
@@ -42,8 +88,8 @@ __device__ __forceinline__ double pymod(double a, double b) {
 }
 
 __device__ __forceinline__ float pymodf(float a, float b) {
-    float m = fmodf(a, b);
-    if (b == 0.0f) return m;
+    float m = fmodf_x86(a, b);
+    if (b == 0.0f || isnan(m)) return m;
     if (m != 0.0f) {
         if ((b < 0.0f) != (m < 0.0f)) m += b;
     } else {
@@ -60,7 +106,9 @@ __device__ __forceinline__ double wrap_f64(double x, double L, double twoL, int 
         const double y = x + L;
         return (y == twoL) ? 0.0 : y - L;
     }
-    return pymod(pymod(x, L) + L, L);
+    const double m = pymod(x, L);
+    if (isnan(m)) return m;
+    return pymod(m + L, L);
 }
 
 __device__ __forceinline__ float wrap_f32(float x, float L, float twoL, int fast) {
@@ -68,7 +116,9 @@ __device__ __forceinline__ float wrap_f32(float x, float L, float twoL, int fast
         const float y = x + L;
         return (y == twoL) ? 0.0f : y - L;
     }
-    return pymodf(pymodf(x, L) + L, L);
+    const float m = pymodf(x, L);
+    if (isnan(m)) return m;
+    return pymodf(m + L, L);
 }
 
 __device__ __forceinline__ long long floormod_i64(long long a, long long n) {
@@ -92,11 +142,12 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
         const float q = x / g.Lf[d];                 // f32 / f32 -> f32
         k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
     } else {
-        double x = (double)*p;
+        double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)*p) : (double)*p;
         if (kPeriodic) {
-            const PosT w = (PosT)wrap_f64(x, g.L[d], g.twoL[d], g.fast[d]);  // f32: round (S9)
+            const double t = wrap_f64(x, g.L[d], g.twoL[d], g.fast[d]);
+            const PosT w = sizeof(PosT) == 4 ? (PosT)f64_to_f32_x86(t) : (PosT)t;  // round (S9)
             *p = w;
-            x = (double)w;                           // bin reads the written value (S2)
+            x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)w) : (double)w;  // bin reads it (S2)
         }
         k = trunc_i64(x / g.L[d] * g.nd[d]);
     }

@@ -30,3 +30,19 @@ def same_bytes(a, b):
     a = np.ascontiguousarray(a)
     b = np.ascontiguousarray(b)
     return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def diff_report(a, b, limit=8):
+    """First differing elements of two same-shape arrays, as hex bit patterns."""
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    if a.shape != b.shape or a.dtype != b.dtype:
+        return f"shape/dtype {a.shape} {a.dtype} vs {b.shape} {b.dtype}"
+    ua = a.view(np.uint8).reshape(len(a), -1) if a.ndim else a.view(np.uint8)
+    ub = b.view(np.uint8).reshape(len(b), -1) if b.ndim else b.view(np.uint8)
+    rows = np.nonzero((ua != ub).any(axis=1))[0]
+    out = [f"{len(rows)} differing rows"]
+    for r in rows[:limit]:
+        out.append(f"row {r}: {a[r]!r} [{ua[r].tobytes().hex()}] vs {b[r]!r} "
+                   f"[{ub[r].tobytes().hex()}]")
+    return "\n".join(out)

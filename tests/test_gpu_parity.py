@@ -47,8 +47,8 @@ def test_bin_edges_golden_numpy():
         p2 = pos.copy()
         idx = R.get_cell_indexes_from_position(p2, periodic=periodic)
         cell = R.get_cell_number_from_position(pos, periodic=periodic)
-        assert G.same_bytes(pos, f[key + "_pos_out"]), key
-        assert G.same_bytes(p2, f[key + "_pos_out"]), key
+        assert G.same_bytes(pos, f[key + "_pos_out"]), (key, G.diff_report(pos, f[key + "_pos_out"]))
+        assert G.same_bytes(p2, f[key + "_pos_out"]), (key, G.diff_report(p2, f[key + "_pos_out"]))
         assert np.array_equal(idx, f[key + "_idx"]), key
         assert np.array_equal(cell, f[key + "_cell"]), key
 
