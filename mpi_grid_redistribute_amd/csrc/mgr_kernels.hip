@@ -211,36 +211,89 @@ __device__ __forceinline__ long long block_excl_scan(long long v, long long* tot
     return pre + x - v;
 }
 
-// ----------------------------------------------------- bin + histogram
-// Kernel 1 of the hot path: reads positions, wraps + writes them back,
-// writes the destination of every row, and the tile's histogram
-// (destination-major counts[b * T + tile]).
-template <typename PosT, bool kPeriodic, typename DestT>
+// ------------------------------------------------------ wave-private tiles
+// A tile is tile_rows = 64 * R consecutive rows owned by ONE wavefront; a
+// workgroup of wpb waves runs tiles blockIdx.x * wpb + wave.  Row
+// (tile, round r, lane l) = tile * tile_rows + 64 r + l, so (round, lane)
+// order IS the original row order: a ballot rank inside a round plus a
+// running per-bin count across rounds is a stable rank.  Tiles never share
+// data, so the kernels have no workgroup barriers at all.
+__device__ __forceinline__ void wave_sync() {
+    // LDS traffic of one wave is performed in order; this only stops the
+    // compiler from moving LDS accesses across the point.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int W> struct Unit;
+template <> struct Unit<16> { using T = uint4; };
+template <> struct Unit<8> { using T = uint2; };
+template <> struct Unit<4> { using T = uint32_t; };
+template <> struct Unit<2> { using T = uint16_t; };
+template <> struct Unit<1> { using T = uint8_t; };
+
+// Copy nbytes (a multiple of 4) between 16-byte-aligned regions with one
+// wave: W-byte units, 4-byte tail.
+template <int W>
+__device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t* __restrict__ s,
+                                          int nbytes, int lane) {
+    using U = typename Unit<W>::T;
+    const int units = nbytes / W;
+    for (int u = lane; u < units; u += 64) ((U*)d)[u] = ((const U*)s)[u];
+    for (int q = units * (W / 4) + lane; q < nbytes / 4; q += 64)
+        ((uint32_t*)d)[q] = ((const uint32_t*)s)[q];
+}
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+// Kernel 1 of the hot path: wrap + write back positions, destination of
+// every row, per-tile histogram (destination-major counts[b * T + tile]).
+// kStaged: the tile's 64-row slabs of position rows (row_bytes <= 64) go
+// through wave-private LDS so every global access is a coalesced W-byte
+// vector; otherwise each lane reads its own row.
+template <typename PosT, bool kPeriodic, typename DestT, int W, bool kStaged>
 __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
                                                            int32_t* __restrict__ counts,
-                                                           int64_t T, int tile_rows) {
-    extern __shared__ __attribute__((aligned(16))) int32_t s_hist[];
-    const int64_t tile = blockIdx.x;
+                                                           int64_t T, int tile_rows,
+                                                           int per_wave_lds) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int wpb = blockDim.x >> 6;
+    const int64_t tile = (int64_t)blockIdx.x * wpb + w;
+    if (tile >= T) return;
+    int32_t* hist = (int32_t*)(smem + w * per_wave_lds);
+    uint8_t* stage = smem + w * per_wave_lds + align16(g.nbins * 4);
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
-    for (int b = threadIdx.x; b < g.nbins; b += kBlock) s_hist[b] = 0;
-    __syncthreads();
-    for (int i0 = 0; i0 < rows; i0 += kBlock) {
-        const int i = i0 + threadIdx.x;
-        const bool valid = i < rows;
+    const int rb = (int)(stride * (int64_t)sizeof(PosT));
+    for (int b = lane; b < g.nbins; b += 64) hist[b] = 0;
+    wave_sync();
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const int nr = min(64, rows - r0);
+        const int64_t grow0 = row0 + r0;
+        const bool valid = lane < nr;
         unsigned b = 0;
-        if (valid) {
-            const int64_t r = row0 + i;
-            b = (unsigned)bin_row<PosT, kPeriodic>(pos + r * stride, g, nullptr);
-            dest[r] = (DestT)b;
+        if (kStaged) {
+            uint8_t* gslab = (uint8_t*)pos + grow0 * rb;
+            wave_copy<W>(stage, gslab, nr * rb, lane);
+            wave_sync();
+            if (valid) b = (unsigned)bin_row<PosT, kPeriodic>((PosT*)(stage + lane * rb), g, nullptr);
+            if (kPeriodic) {
+                wave_sync();
+                wave_copy<W>(gslab, stage, nr * rb, lane);
+            }
+        } else {
+            if (valid) b = (unsigned)bin_row<PosT, kPeriodic>(pos + (grow0 + lane) * stride, g, nullptr);
         }
+        if (valid) dest[grow0 + lane] = (DestT)b;
         const unsigned long long peers = match_bin(b, valid, g.nbits);
-        if (valid && rank_in(peers) == 0) atomicAdd(&s_hist[b], __popcll(peers));
+        if (valid && rank_in(peers) == 0) hist[b] += __popcll(peers);  // leaders: distinct bins
+        wave_sync();
     }
-    __syncthreads();
-    for (int b = threadIdx.x; b < g.nbins; b += kBlock) counts[(int64_t)b * T + tile] = s_hist[b];
+    for (int b = lane; b < g.nbins; b += 64) counts[(int64_t)b * T + tile] = hist[b];
 }
 
 // get_cell_number_from_position / get_cell_indexes_from_position (API helpers).
@@ -263,20 +316,22 @@ __global__ __launch_bounds__(kBlock) void bin_ids_kernel(const IdT* __restrict__
                                                          int nbins, int nbits,
                                                          DestT* __restrict__ dest,
                                                          int32_t* __restrict__ counts, int64_t T,
-                                                         int tile_rows) {
-    extern __shared__ __attribute__((aligned(16))) int32_t s_hist[];
-    const int64_t tile = blockIdx.x;
+                                                         int tile_rows, int per_wave_lds) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    if (tile >= T) return;
+    int32_t* hist = (int32_t*)(smem + w * per_wave_lds);
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     const int nb = nbins + 1;
-    for (int b = threadIdx.x; b < nb; b += kBlock) s_hist[b] = 0;
-    __syncthreads();
-    for (int i0 = 0; i0 < rows; i0 += kBlock) {
-        const int i = i0 + threadIdx.x;
-        const bool valid = i < rows;
+    for (int b = lane; b < nb; b += 64) hist[b] = 0;
+    wave_sync();
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const bool valid = r0 + lane < rows;
         unsigned b = 0;
         if (valid) {
-            const IdT v = ids[row0 + i];
+            const IdT v = ids[row0 + r0 + lane];
             bool ok;
             if constexpr (std::is_floating_point<IdT>::value) {  // numpy float == int compare
                 ok = (v >= (IdT)0) && (v < (IdT)nbins) && (v == (IdT)(long long)v);
@@ -284,13 +339,13 @@ __global__ __launch_bounds__(kBlock) void bin_ids_kernel(const IdT* __restrict__
                 ok = (v >= 0) && ((long long)v < (long long)nbins);
             }
             b = ok ? (unsigned)(long long)v : (unsigned)nbins;
-            dest[row0 + i] = (DestT)b;
+            dest[row0 + r0 + lane] = (DestT)b;
         }
         const unsigned long long peers = match_bin(b, valid, nbits);
-        if (valid && rank_in(peers) == 0) atomicAdd(&s_hist[b], __popcll(peers));
+        if (valid && rank_in(peers) == 0) hist[b] += __popcll(peers);
+        wave_sync();
     }
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += kBlock) counts[(int64_t)b * T + tile] = s_hist[b];
+    for (int b = lane; b < nb; b += 64) counts[(int64_t)b * T + tile] = hist[b];
 }
 
 __global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t* __restrict__ idx,
@@ -357,187 +412,72 @@ __global__ void bin_totals_kernel(const int64_t* __restrict__ bin_starts, int nb
 }
 
 // ------------------------------------------------------------------ pack
-template <int W> struct Unit;
-template <> struct Unit<16> { using T = uint4; };
-template <> struct Unit<8> { using T = uint2; };
-template <> struct Unit<4> { using T = uint32_t; };
-template <> struct Unit<2> { using T = uint16_t; };
-template <> struct Unit<1> { using T = uint8_t; };
-
-// floor(u / d): multiply-high when every u of the tile satisfies u * d < 2^32
-// (m != 0), plain 64-bit division otherwise (very wide rows only).
-struct FastDiv {
-    uint64_t d;
-    uint32_t m;
-    __device__ __forceinline__ uint64_t div(uint64_t u) const {
-        if (d == 1) return u;
-        if (m) return __umulhi((uint32_t)u, m);
-        return u / d;
-    }
-};
-
-struct PackLayout {
-    // LDS carve of one pack workgroup (all offsets multiples of 16 bytes)
-    int sw;    // int64  [kWaves]  block-scan scratch
-    int cnt;   // uint16 [nb][RW]  counts, then scanned in place to sorted starts
-    int base;  // int32  [nb + 1]  first sorted slot of each bin in this tile
-    int goff;  // int64  [nb]      global row of the tile's segment per bin
-    int spos;  // uint16 [tile_rows] sorted slot of tile row i
-    int sbin;  // uint16 [tile_rows] bin of sorted slot s
-    int rows;  // bytes  [tile_rows * max(row_bytes, 4)] staged rows (aliased by the
-               //        uint32 bin|rank scratch of phase A-C)
-    int total;
-};
-
-__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
-
-__host__ __device__ inline PackLayout pack_layout(int tile_rows, int64_t row_bytes, int nb,
-                                                  bool staged) {
-    PackLayout L;
-    const int RW = (tile_rows / kBlock) * kWaves;
-    int o = 0;
-    L.sw = o;   o += align16(kWaves * 8);
-    L.cnt = o;  o += align16(RW * nb * 2);
-    L.base = o; o += align16((nb + 1) * 4);
-    L.goff = o; o += align16(nb * 8);
-    L.spos = o; o += align16(tile_rows * 2);
-    L.sbin = o; o += align16(tile_rows * 2);
-    L.rows = o;
-    const int64_t rb = staged ? (row_bytes < 4 ? 4 : row_bytes) : 4;
-    o += align16((int)(tile_rows * rb));
-    L.total = o;
-    return L;
-}
-
-template <int W, typename DestT, bool kStaged>
+// Kernel 3 of the hot path.  Per round: ballot match -> rank inside the
+// wave; slot = tile segment start of the bin + running count + rank; the
+// row is copied straight to its slot.  Same-bin lanes hold consecutive
+// slots, so each store instruction writes a few contiguous runs, and the
+// runs of consecutive rounds continue each other (merged in L2).
+// kWide (rows > 256 B): the wave copies one row at a time, 64 lanes wide.
+template <int W, typename DestT, bool kWide>
 __global__ __launch_bounds__(kBlock) void pack_kernel(
-    const uint8_t* __restrict__ src, int64_t upr /* units per row */, FastDiv fd, int64_t n,
-    const DestT* __restrict__ dest, int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, PackLayout lay,
-    uint8_t* __restrict__ dst, int redirect_bin, uint8_t* __restrict__ redirect_dst) {
+    const uint8_t* __restrict__ src, int64_t upr /* W-units per row */, int64_t n,
+    const DestT* __restrict__ dest, int nb, int nbits, int drop_bin,
+    const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts, int64_t T,
+    int tile_rows, int per_wave_lds, uint8_t* __restrict__ dst, int redirect_bin,
+    uint8_t* __restrict__ redirect_dst) {
     using U = typename Unit<W>::T;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint16_t* s_cnt = (uint16_t*)(smem + lay.cnt);
-    int32_t* s_base = (int32_t*)(smem + lay.base);
-    int64_t* s_goff = (int64_t*)(smem + lay.goff);
-    uint16_t* s_spos = (uint16_t*)(smem + lay.spos);
-    uint16_t* s_sbin = (uint16_t*)(smem + lay.sbin);
-    uint32_t* s_kr = (uint32_t*)(smem + lay.rows);   // phase A-C scratch
-    U* s_rows = (U*)(smem + lay.rows);               // phase D-E staging
-    long long* s_w = (long long*)(smem + lay.sw);
-
-    const int64_t tile = blockIdx.x;
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    if (tile >= T) return;
+    int64_t* goff = (int64_t*)(smem + w * per_wave_lds);
+    int32_t* run = (int32_t*)(smem + w * per_wave_lds + align16(nb * 8));
+    for (int b = lane; b < nb; b += 64) {
+        int64_t o = offsets[(int64_t)b * T + tile];
+        if (b == redirect_bin) o -= bin_starts[b];
+        goff[b] = o;
+        run[b] = 0;
+    }
+    wave_sync();
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
-    const int R = (rows + kBlock - 1) / kBlock;
-    const int RW = (tile_rows / kBlock) * kWaves;
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-
-    for (int j = threadIdx.x; j < RW * nb; j += kBlock) s_cnt[j] = 0;
-    for (int b = threadIdx.x; b < nb; b += kBlock) {
-        int64_t g = offsets[(int64_t)b * T + tile];
-        if (b == redirect_bin) g -= bin_starts[b];
-        s_goff[b] = g;
-    }
-    __syncthreads();
-
-    // Phase A: per round, per wave: bin match -> stable rank inside the wave.
-    for (int r = 0; r < R; ++r) {
-        const int i = r * kBlock + threadIdx.x;
-        const bool valid = i < rows;
-        const unsigned b = valid ? (unsigned)dest[row0 + i] : 0u;
+    const U* __restrict__ s_u = (const U*)src;
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const bool valid = r0 + lane < rows;
+        const int64_t row = row0 + r0 + lane;
+        const unsigned b = valid ? (unsigned)dest[row] : 0u;
         const unsigned long long peers = match_bin(b, valid, nbits);
         const int rk = rank_in(peers);
-        if (valid) {
-            s_kr[i] = (b << 8) | (unsigned)rk;
-            if (rk == 0) s_cnt[b * RW + r * kWaves + w] = (uint16_t)__popcll(peers);
-        }
-    }
-    __syncthreads();
-
-    // Phase B: one exclusive scan over (bin, round, wave) in bin-major order
-    // gives each (round, wave, bin) group its first sorted slot in the tile.
-    {
-        const int M = RW * nb;
-        const int per = (M + kBlock - 1) / kBlock;
-        const int lo = threadIdx.x * per, hi = min(M, lo + per);
-        long long acc = 0;
-        for (int j = lo; j < hi; ++j) acc += s_cnt[j];
-        long long tot;
-        long long run = block_excl_scan(acc, &tot, s_w);
-        for (int j = lo; j < hi; ++j) {
-            const int c = s_cnt[j];
-            s_cnt[j] = (uint16_t)run;
-            run += c;
-        }
-        __syncthreads();
-        for (int b = threadIdx.x; b < nb; b += kBlock) s_base[b] = s_cnt[b * RW];
-        if (threadIdx.x == 0) s_base[nb] = rows;
-    }
-    __syncthreads();
-
-    // Phase C: sorted slot of every row.
-    for (int r = 0; r < R; ++r) {
-        const int i = r * kBlock + threadIdx.x;
-        if (i < rows) {
-            const uint32_t kr = s_kr[i];
-            const unsigned b = kr >> 8;
-            const int s = s_cnt[b * RW + r * kWaves + w] + (int)(kr & 0xffu);
-            s_spos[i] = (uint16_t)s;
-            s_sbin[s] = (uint16_t)b;
-        }
-    }
-    __syncthreads();
-    (void)lane;
-
-    const int64_t U_tile = (int64_t)rows * upr;
-    const U* __restrict__ src_tile = (const U*)(src + row0 * upr * W);
-    U* __restrict__ dst_u = (U*)dst;
-    U* __restrict__ red_u = (U*)redirect_dst;
-
-    if (kStaged) {
-        // Phase D: coalesced tile load, scattered into sorted order in LDS.
-        constexpr int kUnroll = 4;
-        for (int64_t u0 = threadIdx.x; u0 < U_tile; u0 += kBlock * kUnroll) {
-            U v[kUnroll];
-#pragma unroll
-            for (int j = 0; j < kUnroll; ++j) {
-                const int64_t u = u0 + j * kBlock;
-                if (u < U_tile) v[j] = src_tile[u];
-            }
-#pragma unroll
-            for (int j = 0; j < kUnroll; ++j) {
-                const int64_t u = u0 + j * kBlock;
-                if (u < U_tile) {
-                    const uint32_t row = (uint32_t)fd.div((uint64_t)u);
-                    const uint32_t k = (uint32_t)u - row * (uint32_t)upr;
-                    s_rows[(uint32_t)s_spos[row] * (uint32_t)upr + k] = v[j];
+        int64_t slot = 0;
+        if (valid) slot = goff[b] + run[b] + rk;
+        wave_sync();
+        if (valid && rk == 0) run[b] += __popcll(peers);
+        const bool live = valid && (int)b != drop_bin;
+        if (!kWide) {
+            if (live) {
+                const U* sp = s_u + row * upr;
+                U* dp = ((int)b == redirect_bin ? r_u : d_u) + slot * upr;
+                int64_t k = 0;
+                for (; k + 4 <= upr; k += 4) {
+                    const U a0 = sp[k], a1 = sp[k + 1], a2 = sp[k + 2], a3 = sp[k + 3];
+                    dp[k] = a0; dp[k + 1] = a1; dp[k + 2] = a2; dp[k + 3] = a3;
                 }
+                for (; k < upr; ++k) dp[k] = sp[k];
+            }
+        } else {
+            const unsigned long long todo = __ballot(live);
+            for (int j = 0; j < 64; ++j) {
+                if (!((todo >> j) & 1ull)) continue;
+                const int bj = __shfl((int)b, j, 64);
+                const int64_t sj = __shfl((long long)slot, j, 64);
+                const U* sp = s_u + (row0 + r0 + j) * upr;
+                U* dp = (bj == redirect_bin ? r_u : d_u) + sj * upr;
+                for (int64_t k = lane; k < upr; k += 64) dp[k] = sp[k];
             }
         }
-        __syncthreads();
-        // Phase E: contiguous runs per bin -> coalesced stores.
-        for (int64_t su = threadIdx.x; su < U_tile; su += kBlock) {
-            const uint32_t srow = (uint32_t)fd.div((uint64_t)su);
-            const uint32_t k = (uint32_t)su - srow * (uint32_t)upr;
-            const int b = s_sbin[srow];
-            if (b == drop_bin) continue;
-            const int64_t grow = s_goff[b] + (int64_t)(srow - (uint32_t)s_base[b]);
-            U* o = (b == redirect_bin) ? red_u : dst_u;
-            o[grow * upr + k] = s_rows[su];
-        }
-    } else {
-        // Wide rows: copy straight from the source row to its slot.
-        for (int64_t u = threadIdx.x; u < U_tile; u += kBlock) {
-            const uint64_t row = fd.div((uint64_t)u);
-            const uint64_t k = (uint64_t)u - row * (uint64_t)upr;
-            const int s = s_spos[row];
-            const int b = s_sbin[s];
-            if (b == drop_bin) continue;
-            const int64_t grow = s_goff[b] + (int64_t)(s - s_base[b]);
-            U* o = (b == redirect_bin) ? red_u : dst_u;
-            o[grow * upr + k] = src_tile[u];
-        }
+        wave_sync();
     }
 }
 
@@ -622,32 +562,56 @@ static void ensure_lds(K kernel, int bytes) {
         (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-template <typename PosT, bool kP, typename DestT>
+// Waves per workgroup for a per-wave LDS footprint: 4 when a 4-wave
+// workgroup stays within 64 KiB, fewer otherwise (never above 160 KiB).
+static int waves_per_block(int per_wave_lds) {
+    if (per_wave_lds * kWaves <= 64 * 1024) return kWaves;
+    int w = (160 * 1024) / (per_wave_lds > 0 ? per_wave_lds : 1);
+    return w < 1 ? 1 : (w > kWaves ? kWaves : w);
+}
+
+constexpr int kStageMaxRowBytes = 64;   // bin kernel stages position rows up to 64 B
+
+template <typename PosT, bool kP, typename DestT, int W, bool kStaged>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto k = bin_count_kernel<PosT, kP, DestT>;
-    const size_t lds = (size_t)g.nbins * 4;
-    ensure_lds(k, (int)lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), lds, s, (PosT*)pos, n, stride, g,
-                       (DestT*)dest, ws.counts, ws.T, tile_rows);
+    auto k = bin_count_kernel<PosT, kP, DestT, W, kStaged>;
+    const int rb = (int)(stride * (int64_t)sizeof(PosT));
+    const int per_wave = align16(g.nbins * 4) + (kStaged ? align16(64 * rb) : 0);
+    const int wpb = waves_per_block(per_wave);
+    const int lds = per_wave * wpb;
+    ensure_lds(k, lds);
+    const int64_t grid = (ws.T + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s, (PosT*)pos, n,
+                       stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave);
     return hipGetLastError();
+}
+
+template <typename PosT, bool kP, typename DestT>
+static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
+                              int tile_rows, const Workspace& ws, hipStream_t s) {
+    const int64_t rb = stride * (int64_t)sizeof(PosT);
+    if (rb > kStageMaxRowBytes)
+        return bin_count_t<PosT, kP, DestT, 4, false>(g, pos, n, stride, dest, tile_rows, ws, s);
+    const uintptr_t a = (uintptr_t)pos;
+    if ((a & 15) == 0) return bin_count_t<PosT, kP, DestT, 16, true>(g, pos, n, stride, dest, tile_rows, ws, s);
+    if ((a & 7) == 0) return bin_count_t<PosT, kP, DestT, 8, true>(g, pos, n, stride, dest, tile_rows, ws, s);
+    return bin_count_t<PosT, kP, DestT, 4, true>(g, pos, n, stride, dest, tile_rows, ws, s);
 }
 
 template <typename PosT, typename DestT>
 static hipError_t bin_count_p(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
                               void* dest, int tile_rows, const Workspace& ws, hipStream_t s) {
-    return periodic ? bin_count_t<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s)
-                    : bin_count_t<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s);
+    return periodic ? bin_count_w<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s)
+                    : bin_count_w<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s);
 }
 
 template <typename PosT>
 static hipError_t bin_count_d(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
                               void* dest, int tile_rows, const Workspace& ws, hipStream_t s) {
-    switch (dest_bytes(g.nbins)) {
-        case 1: return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
-        case 2: return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
-        default: return bin_count_p<PosT, uint32_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
-    }
+    if (dest_bytes(g.nbins) == 1)
+        return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
+    return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
 }
 
 hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
@@ -688,21 +652,22 @@ template <typename IdT, typename DestT>
 static hipError_t bin_ids_t(const void* ids, int64_t n, int nbins, void* dest, int tile_rows,
                             const Workspace& ws, hipStream_t s) {
     auto k = bin_ids_kernel<IdT, DestT>;
-    const size_t lds = (size_t)(nbins + 1) * 4;
-    ensure_lds(k, (int)lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), lds, s, (const IdT*)ids, n, nbins,
-                       nbits_for(nbins + 1), (DestT*)dest, ws.counts, ws.T, tile_rows);
+    const int per_wave = align16((nbins + 1) * 4);
+    const int wpb = waves_per_block(per_wave);
+    const int lds = per_wave * wpb;
+    ensure_lds(k, lds);
+    const int64_t grid = (ws.T + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s, (const IdT*)ids,
+                       n, nbins, nbits_for(nbins + 1), (DestT*)dest, ws.counts, ws.T, tile_rows,
+                       per_wave);
     return hipGetLastError();
 }
 
 template <typename IdT>
 static hipError_t bin_ids_d(const void* ids, int64_t n, int nbins, void* dest, int tile_rows,
                             const Workspace& ws, hipStream_t s) {
-    switch (dest_bytes(nbins + 1)) {
-        case 1: return bin_ids_t<IdT, uint8_t>(ids, n, nbins, dest, tile_rows, ws, s);
-        case 2: return bin_ids_t<IdT, uint16_t>(ids, n, nbins, dest, tile_rows, ws, s);
-        default: return bin_ids_t<IdT, uint32_t>(ids, n, nbins, dest, tile_rows, ws, s);
-    }
+    if (dest_bytes(nbins + 1) == 1) return bin_ids_t<IdT, uint8_t>(ids, n, nbins, dest, tile_rows, ws, s);
+    return bin_ids_t<IdT, uint16_t>(ids, n, nbins, dest, tile_rows, ws, s);
 }
 
 hipError_t launch_bin_ids(const void* ids, int ids_dtype, int64_t n, int nbins, void* dest,
@@ -763,45 +728,28 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
 }
 
 int pack_tile_rows(int64_t row_bytes, int nbins) {
-    // Largest tile (multiple of 256, <= kMaxTileRows) whose staged LDS image
-    // fits kLdsBudget, so two pack workgroups share a CU; wide rows fall back
-    // to the unstaged copy with 2048-row tiles.
-    for (int tr = kMaxTileRows; tr >= kBlock; tr -= kBlock) {
-        if (pack_layout(tr, row_bytes, nbins, true).total <= kLdsBudget) return tr;
-    }
-    for (int tr = 2048; tr >= kBlock; tr -= kBlock) {
-        if (pack_layout(tr, row_bytes, nbins, false).total <= kLdsBudget) return tr;
-    }
-    return kBlock;
+    // 1024-row wave tiles (16 rounds); more rounds for many bins keep the
+    // [nbins][tiles] histogram small next to the payload.
+    (void)row_bytes;
+    int r = 16;
+    while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
+    return 64 * r;
 }
 
-template <int W, typename DestT>
+template <int W, typename DestT, bool kWide>
 static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                          int redirect_bin, void* redirect_dst, hipStream_t s) {
-    const int64_t upr = row_bytes / W;
-    FastDiv fd;
-    fd.d = (uint64_t)upr;
-    const unsigned __int128 umax = (unsigned __int128)tile_rows * (uint64_t)upr * (uint64_t)upr;
-    fd.m = (upr == 1 || umax >= ((unsigned __int128)1 << 32))
-               ? 0u : (uint32_t)((0x100000000ull + upr - 1) / upr);
-    const bool staged = pack_layout(tile_rows, row_bytes, nb, true).total <= 160 * 1024 - 64;
-    const PackLayout lay = pack_layout(tile_rows, row_bytes, nb, staged);
-    if (staged) {
-        auto k = pack_kernel<W, DestT, true>;
-        ensure_lds(k, lay.total);
-        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lay.total, s,
-                           (const uint8_t*)src, upr, fd, n, (const DestT*)dest, nb, nbits_for(nb),
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, lay,
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
-    } else {
-        auto k = pack_kernel<W, DestT, false>;
-        ensure_lds(k, lay.total);
-        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lay.total, s,
-                           (const uint8_t*)src, upr, fd, n, (const DestT*)dest, nb, nbits_for(nb),
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, lay,
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
-    }
+    auto k = pack_kernel<W, DestT, kWide>;
+    const int per_wave = align16(nb * 8) + align16(nb * 4);
+    const int wpb = waves_per_block(per_wave);
+    const int lds = per_wave * wpb;
+    ensure_lds(k, lds);
+    const int64_t grid = (ws.T + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s,
+                       (const uint8_t*)src, row_bytes / W, n, (const DestT*)dest, nb,
+                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,
+                       per_wave, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
     return hipGetLastError();
 }
 
@@ -809,11 +757,12 @@ template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                          int redirect_bin, void* redirect_dst, hipStream_t s) {
-    switch (dest_bytes(nb)) {
-        case 1: return pack_t<W, uint8_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-        case 2: return pack_t<W, uint16_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-        default: return pack_t<W, uint32_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    }
+    const bool wide = row_bytes > 256;
+    if (dest_bytes(nb) == 1)
+        return wide ? pack_t<W, uint8_t, true>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
+                    : pack_t<W, uint8_t, false>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    return wide ? pack_t<W, uint16_t, true>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
+                : pack_t<W, uint16_t, false>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
 }
 
 hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
