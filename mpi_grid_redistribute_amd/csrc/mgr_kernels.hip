@@ -101,14 +101,26 @@ __device__ __forceinline__ float pymodf(float a, float b) {
 // ((x % L) + L) % L.  Fast path for 0 <= x < L (every in-box particle):
 // x % L == x, y = x + L in [L, 2L], and fmod(y, L) == y - L exactly
 // (Sterbenz), 0 when y == 2L.  Bit-identical to the general path.
+// General path (outside the box, non-finite, odd boxes): out of line so its
+// registers do not weigh on the streaming fast path.
+__device__ __attribute__((noinline)) double wrap_f64_slow(double x, double L) {
+    const double m = pymod(x, L);
+    if (isnan(m)) return m;
+    return pymod(m + L, L);
+}
+
+__device__ __attribute__((noinline)) float wrap_f32_slow(float x, float L) {
+    const float m = pymodf(x, L);
+    if (isnan(m)) return m;
+    return pymodf(m + L, L);
+}
+
 __device__ __forceinline__ double wrap_f64(double x, double L, double twoL, int fast) {
     if (fast && x >= 0.0 && x < L) {
         const double y = x + L;
         return (y == twoL) ? 0.0 : y - L;
     }
-    const double m = pymod(x, L);
-    if (isnan(m)) return m;
-    return pymod(m + L, L);
+    return wrap_f64_slow(x, L);
 }
 
 __device__ __forceinline__ float wrap_f32(float x, float L, float twoL, int fast) {
@@ -116,9 +128,7 @@ __device__ __forceinline__ float wrap_f32(float x, float L, float twoL, int fast
         const float y = x + L;
         return (y == twoL) ? 0.0f : y - L;
     }
-    const float m = pymodf(x, L);
-    if (isnan(m)) return m;
-    return pymodf(m + L, L);
+    return wrap_f32_slow(x, L);
 }
 
 __device__ __forceinline__ long long floormod_i64(long long a, long long n) {
@@ -157,12 +167,17 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
     return k;
 }
 
-template <typename PosT, bool kPeriodic>
+// DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
+template <typename PosT, bool kPeriodic, int DIM = 0>
 __device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx) {
     long long cell = 0;
+    if (DIM > 0) {
 #pragma unroll
-    for (int d = 0; d < MGR_MAX_DIM; ++d) {
-        if (d < g.dim) cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr);
+        for (int d = 0; d < DIM; ++d)
+            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr);
+    } else {
+        for (int d = 0; d < g.dim; ++d)
+            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr);
     }
     return cell;
 }
@@ -249,11 +264,15 @@ __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
 // Kernel 1 of the hot path: wrap + write back positions, destination of
 // every row, per-tile histogram (destination-major counts[b * T + tile]).
-// kStaged: the tile's 64-row slabs of position rows (row_bytes <= 64) go
-// through wave-private LDS so every global access is a coalesced W-byte
-// vector; otherwise each lane reads its own row.
-template <typename PosT, bool kPeriodic, typename DestT, int W, bool kStaged>
-__global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
+// kStaged (16-byte aligned position rows of <= 64 B): each 64-row slab is
+// loaded with coalesced 16-byte vectors one round AHEAD into registers,
+// parked in wave-private LDS for the per-row math, and stored back the same
+// way; otherwise each lane reads its own row.
+constexpr int kStageMaxRowBytes = 64;
+constexpr int kSlabUnits = kStageMaxRowBytes * 64 / 16 / 64;   // uint4 per lane per slab (4)
+
+template <typename PosT, bool kPeriodic, typename DestT, bool kStaged, int DIM>
+__global__ __launch_bounds__(kBlock, 6) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
                                                            int32_t* __restrict__ counts,
@@ -270,6 +289,16 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     for (int b = lane; b < g.nbins; b += 64) hist[b] = 0;
+    // Slab of a round: nr * rb bytes at (row0 + r0) * rb, as 16-byte units
+    // u = lane + 64 k (k < kSlabUnits) plus a 4-byte tail on a partial slab.
+    uint4 nxt[kSlabUnits];
+    if (kStaged) {
+        const int units = min(64, rows) * rb / 16;
+        const uint4* gs = (const uint4*)((const uint8_t*)pos + row0 * rb);
+#pragma unroll
+        for (int k = 0; k < kSlabUnits; ++k)
+            if (lane + 64 * k < units) nxt[k] = gs[lane + 64 * k];
+    }
     wave_sync();
     for (int r0 = 0; r0 < rows; r0 += 64) {
         const int nr = min(64, rows - r0);
@@ -277,16 +306,35 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
         const bool valid = lane < nr;
         unsigned b = 0;
         if (kStaged) {
+            const int units = nr * rb / 16;
             uint8_t* gslab = (uint8_t*)pos + grow0 * rb;
-            wave_copy<W>(stage, gslab, nr * rb, lane);
+#pragma unroll
+            for (int k = 0; k < kSlabUnits; ++k)
+                if (lane + 64 * k < units) ((uint4*)stage)[lane + 64 * k] = nxt[k];
+            for (int q = units * 4 + lane; q < nr * rb / 4; q += 64)
+                ((uint32_t*)stage)[q] = ((const uint32_t*)gslab)[q];
+            if (r0 + 64 < rows) {  // next slab in flight while this one is binned
+                const int nu = min(64, rows - r0 - 64) * rb / 16;
+                const uint4* gs = (const uint4*)(gslab + 64 * rb);
+#pragma unroll
+                for (int k = 0; k < kSlabUnits; ++k)
+                    if (lane + 64 * k < nu) nxt[k] = gs[lane + 64 * k];
+            }
             wave_sync();
-            if (valid) b = (unsigned)bin_row<PosT, kPeriodic>((PosT*)(stage + lane * rb), g, nullptr);
+            if (valid)
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM>((PosT*)(stage + lane * rb), g, nullptr);
             if (kPeriodic) {
                 wave_sync();
-                wave_copy<W>(gslab, stage, nr * rb, lane);
+#pragma unroll
+                for (int k = 0; k < kSlabUnits; ++k)
+                    if (lane + 64 * k < units)
+                        ((uint4*)gslab)[lane + 64 * k] = ((const uint4*)stage)[lane + 64 * k];
+                for (int q = units * 4 + lane; q < nr * rb / 4; q += 64)
+                    ((uint32_t*)gslab)[q] = ((const uint32_t*)stage)[q];
             }
         } else {
-            if (valid) b = (unsigned)bin_row<PosT, kPeriodic>(pos + (grow0 + lane) * stride, g, nullptr);
+            if (valid)
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM>(pos + (grow0 + lane) * stride, g, nullptr);
         }
         if (valid) dest[grow0 + lane] = (DestT)b;
         const unsigned long long peers = match_bin(b, valid, g.nbits);
@@ -481,6 +529,72 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
     }
 }
 
+// Register-resident pack for <= 64 bins and rows of <= 64 bytes (the
+// common case, e.g. 8 grid cells x 32-byte records).  Lane l keeps the next
+// free slot of bin l in a register; a row finds its slot with one
+// cross-lane read (bpermute) of its bin's lane; per-bin round counts come
+// from the same nbits ballots as the rank, so there is no LDS traffic.  The
+// next round's destinations and rows are prefetched while the current
+// round is ranked and stored.
+template <int W, int UPR>
+__global__ __launch_bounds__(kBlock) void pack_small_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
+    int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst) {
+    using U = typename Unit<W>::T;
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    if (tile >= T) return;
+    long long next_slot = 0;  // lane l: next free slot of bin l
+    if (lane < nb) {
+        next_slot = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) next_slot -= bin_starts[lane];
+    }
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    const U* __restrict__ s_u = (const U*)src;
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+
+    unsigned nb_next = 0;
+    U nv[UPR];
+#define MGR_FETCH(R0)                                                   \
+    if ((R0) + lane < rows) {                                           \
+        const int64_t row_ = row0 + (R0) + lane;                        \
+        nb_next = dest[row_];                                           \
+        const U* sp_ = s_u + row_ * UPR;                                \
+        _Pragma("unroll") for (int k = 0; k < UPR; ++k) nv[k] = sp_[k]; \
+    }
+    MGR_FETCH(0)
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const bool valid = r0 + lane < rows;
+        const unsigned b = valid ? nb_next : 0u;
+        U v[UPR];
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) v[k] = nv[k];
+        if (r0 + 64 < rows) { MGR_FETCH(r0 + 64) }
+#undef MGR_FETCH
+        // nbits ballots: rank inside the wave + per-bin counts for lane == bin
+        unsigned long long peers = __ballot(valid);
+        unsigned long long mine = peers;  // lanes whose bin == this lane's index
+        for (int i = 0; i < nbits; ++i) {
+            const unsigned long long m = __ballot((b >> i) & 1u);
+            peers &= ((b >> i) & 1u) ? m : ~m;
+            mine &= ((lane >> i) & 1) ? m : ~m;
+        }
+        if (!valid) peers = 0;
+        const int rk = rank_in(peers);
+        const long long base = __shfl(next_slot, (int)b, 64);
+        next_slot += __popcll(mine);
+        if (valid && (int)b != drop_bin) {
+            U* dp = ((int)b == redirect_bin ? r_u : d_u) + (base + rk) * UPR;
+#pragma unroll
+            for (int k = 0; k < UPR; ++k) dp[k] = v[k];
+        }
+    }
+}
+
 // --------------------------------------------------------- synthetic data
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -570,12 +684,10 @@ static int waves_per_block(int per_wave_lds) {
     return w < 1 ? 1 : (w > kWaves ? kWaves : w);
 }
 
-constexpr int kStageMaxRowBytes = 64;   // bin kernel stages position rows up to 64 B
-
-template <typename PosT, bool kP, typename DestT, int W, bool kStaged>
+template <typename PosT, bool kP, typename DestT, bool kStaged, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto k = bin_count_kernel<PosT, kP, DestT, W, kStaged>;
+    auto k = bin_count_kernel<PosT, kP, DestT, kStaged, DIM>;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = align16(g.nbins * 4) + (kStaged ? align16(64 * rb) : 0);
     const int wpb = waves_per_block(per_wave);
@@ -587,16 +699,24 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     return hipGetLastError();
 }
 
+template <typename PosT, bool kP, typename DestT, bool kStaged>
+static hipError_t bin_count_dim(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
+                                int tile_rows, const Workspace& ws, hipStream_t s) {
+    switch (g.dim) {
+        case 1: return bin_count_t<PosT, kP, DestT, kStaged, 1>(g, pos, n, stride, dest, tile_rows, ws, s);
+        case 2: return bin_count_t<PosT, kP, DestT, kStaged, 2>(g, pos, n, stride, dest, tile_rows, ws, s);
+        case 3: return bin_count_t<PosT, kP, DestT, kStaged, 3>(g, pos, n, stride, dest, tile_rows, ws, s);
+        default: return bin_count_t<PosT, kP, DestT, kStaged, 0>(g, pos, n, stride, dest, tile_rows, ws, s);
+    }
+}
+
 template <typename PosT, bool kP, typename DestT>
 static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
     const int64_t rb = stride * (int64_t)sizeof(PosT);
-    if (rb > kStageMaxRowBytes)
-        return bin_count_t<PosT, kP, DestT, 4, false>(g, pos, n, stride, dest, tile_rows, ws, s);
-    const uintptr_t a = (uintptr_t)pos;
-    if ((a & 15) == 0) return bin_count_t<PosT, kP, DestT, 16, true>(g, pos, n, stride, dest, tile_rows, ws, s);
-    if ((a & 7) == 0) return bin_count_t<PosT, kP, DestT, 8, true>(g, pos, n, stride, dest, tile_rows, ws, s);
-    return bin_count_t<PosT, kP, DestT, 4, true>(g, pos, n, stride, dest, tile_rows, ws, s);
+    if (rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0)
+        return bin_count_dim<PosT, kP, DestT, true>(g, pos, n, stride, dest, tile_rows, ws, s);
+    return bin_count_dim<PosT, kP, DestT, false>(g, pos, n, stride, dest, tile_rows, ws, s);
 }
 
 template <typename PosT, typename DestT>
@@ -753,10 +873,56 @@ static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const vo
     return hipGetLastError();
 }
 
+template <int W, int UPR>
+static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
+                               void* redirect_dst, hipStream_t s) {
+    const int64_t grid = (ws.T + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL((pack_small_kernel<W, UPR>), dim3((unsigned)grid), dim3(kBlock), 0, s,
+                       (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
+                       ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
+                       (uint8_t*)redirect_dst);
+    return hipGetLastError();
+}
+
+// Compile-time units per row for rows of <= 64 bytes in 16/8/4-byte units
+// (registers, no scratch); returns hipErrorNotSupported for other shapes.
+template <int W>
+static hipError_t pack_small_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                               int nb, int drop_bin, int tile_rows, const Workspace& ws,
+                               void* dst, int redirect_bin, void* redirect_dst, hipStream_t s) {
+#define MGR_PS(U_) case U_: return pack_small_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    if (W >= 4) {
+        switch ((int)(row_bytes / W)) {
+            MGR_PS(1) MGR_PS(2) MGR_PS(3) MGR_PS(4)
+            default: break;
+        }
+        if (W <= 8) {
+            switch ((int)(row_bytes / W)) {
+                MGR_PS(5) MGR_PS(6) MGR_PS(7) MGR_PS(8)
+                default: break;
+            }
+        }
+        if (W == 4) {
+            switch ((int)(row_bytes / W)) {
+                MGR_PS(9) MGR_PS(10) MGR_PS(11) MGR_PS(12) MGR_PS(13) MGR_PS(14) MGR_PS(15) MGR_PS(16)
+                default: break;
+            }
+        }
+    }
+#undef MGR_PS
+    return hipErrorNotSupported;
+}
+
 template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                          int redirect_bin, void* redirect_dst, hipStream_t s) {
+    if (nb <= 64 && row_bytes <= 64 && W >= 4) {
+        const hipError_t e = pack_small_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
+                                             ws, dst, redirect_bin, redirect_dst, s);
+        if (e != hipErrorNotSupported) return e;
+    }
     const bool wide = row_bytes > 256;
     if (dest_bytes(nb) == 1)
         return wide ? pack_t<W, uint8_t, true>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
