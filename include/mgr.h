@@ -174,6 +174,12 @@ int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, in
 int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const double* box,
                       double* pos, void* rec32, void* stream);
 
+/* -------------------------------------------------------------- tuning --
+ * Kernel-variant knobs for A/B measurement ("bin_staged", "pack_small",
+ * "tile_rounds"); the defaults are the shipped configuration.  Process-wide,
+ * not thread-safe against concurrent launches.                           */
+int mgr_tune(const char* key, int64_t value);
+
 /* ----------------------------------------------------------- profiling --
  * Per-kernel HIP-event timing of every launch made while enabled, on the
  * launch's own stream.  mgr_profile_read synchronises those events and

@@ -52,6 +52,7 @@ SIGNATURES = {
     "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "mgr_comm_allreduce_max_f64": (_I, [_P, _P, _P, _I64, _P]),
     "mgr_synth_uniform": (_I, [ctypes.c_uint64, _I64, _I64, _I, _P, _P, _P, _P]),
+    "mgr_tune": (_I, [ctypes.c_char_p, _I64]),
     "mgr_profile_enable": (_I, [_I]),
     "mgr_profile_reset": (_I, []),
     "mgr_profile_read": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _PI64]),
@@ -109,6 +110,11 @@ def stream_handle(stream=None):
 def ptr(t):
     """Device address of a torch tensor (None -> NULL)."""
     return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+def tune(key, value):
+    """Kernel-variant knob (A/B measurement only; defaults are shipped)."""
+    call("mgr_tune", key.encode(), int(value))
 
 
 # --------------------------------------------------------------- profiler

@@ -157,6 +157,11 @@ int mgr_plan_create(int dim, const int64_t* topo, const double* box, int box_dty
         g.fastf[d] = (Lf > 0.0f) && isfinite(Lf + Lf);
         g.n[d] = topo[d];
         g.nd[d] = (double)topo[d];
+        int e;
+        g.pow2[d] = L > 0.0 && isfinite(L) && frexp(L, &e) == 0.5 && isnormal(1.0 / L);
+        g.invL[d] = g.pow2[d] ? 1.0 / L : 0.0;
+        g.pow2f[d] = Lf > 0.0f && isfinite(Lf) && frexpf(Lf, &e) == 0.5f && isnormal(1.0f / Lf);
+        g.invLf[d] = g.pow2f[d] ? 1.0f / Lf : 0.0f;
     }
     mgr_plan* p = new mgr_plan;
     p->g = g;
@@ -398,6 +403,19 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
     if (rec32 && dim != 3) return fail(MGR_EINVAL, "32-byte records need dim == 3");
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     HIP_OK(mgr::launch_synth_uniform(seed, gid0, n, dim, box, pos, rec32, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+// -------------------------------------------------------------- tuning
+int mgr_tune(const char* key, int64_t value) {
+    if (!key) return fail(MGR_EINVAL, "null key");
+    if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
+    else if (!strcmp(key, "pack_small")) mgr::g_tune.pack_small = (int)value;
+    else if (!strcmp(key, "tile_rounds")) {
+        if (value < 0 || value > mgr::kMaxTileRows / 64 || (value && (64 * value) % mgr::kBlock))
+            return fail(MGR_EINVAL, "tile_rounds %lld", (long long)value);
+        mgr::g_tune.tile_rounds = (int)value;
+    } else return fail(MGR_EINVAL, "unknown tuning key '%s'", key);
     return MGR_OK;
 }
 

@@ -26,6 +26,10 @@ struct Geom {
     double twoL[MGR_MAX_DIM];
     float Lf[MGR_MAX_DIM];
     float twoLf[MGR_MAX_DIM];
+    int pow2[MGR_MAX_DIM];               // L is a power of two: x / L == x * (1/L) exactly
+    int pow2f[MGR_MAX_DIM];
+    double invL[MGR_MAX_DIM];
+    float invLf[MGR_MAX_DIM];
     double nd[MGR_MAX_DIM];              // (double)n[d], the int64 multiplier promoted
     int64_t n[MGR_MAX_DIM];
     int64_t off[MGR_MAX_DIM];            // row-major offsets, last axis fastest (S4)
@@ -70,5 +74,13 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
+
+// Tuning knobs (mgr_tune); defaults are the shipped configuration.
+struct Tune {
+    int bin_staged = 1;    // stage 64-row position slabs through LDS
+    int pack_small = 1;    // register-resident pack for <= 64 bins, <= 64-byte rows
+    int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
+};
+extern Tune g_tune;
 
 }  // namespace mgr

@@ -23,9 +23,13 @@
 
 namespace mgr {
 
+Tune g_tune;
+
 // ------------------------------------------------------------ scalar math
 __device__ __forceinline__ long long trunc_i64(double v) {
-    // numpy astype(int64) on x86 (cvttsd2si): NaN / out of range -> INT64_MIN (S10)
+    // numpy astype(int64) on x86 (cvttsd2si): NaN / out of range -> INT64_MIN (S10).
+    // |v| < 2^31 (every in-box particle): one v_cvt_i32_f64.
+    if (v > -2147483648.0 && v < 2147483648.0) return (long long)(int)v;
     return (v >= -9223372036854775808.0 && v < 9223372036854775808.0) ? (long long)v : LLONG_MIN;
 }
 
@@ -149,7 +153,7 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
             x = wrap_f32(x, g.Lf[d], g.twoLf[d], g.fastf[d]);
             *p = (PosT)x;
         }
-        const float q = x / g.Lf[d];                 // f32 / f32 -> f32
+        const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];  // f32 / f32 -> f32
         k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
     } else {
         double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)*p) : (double)*p;
@@ -159,7 +163,7 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
             *p = w;
             x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)w) : (double)w;  // bin reads it (S2)
         }
-        k = trunc_i64(x / g.L[d] * g.nd[d]);
+        k = trunc_i64((g.pow2[d] ? x * g.invL[d] : x / g.L[d]) * g.nd[d]);
     }
     if (raw) *raw = k;
     const long long n = g.n[d];
@@ -714,7 +718,7 @@ template <typename PosT, bool kP, typename DestT>
 static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
     const int64_t rb = stride * (int64_t)sizeof(PosT);
-    if (rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0)
+    if (g_tune.bin_staged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0)
         return bin_count_dim<PosT, kP, DestT, true>(g, pos, n, stride, dest, tile_rows, ws, s);
     return bin_count_dim<PosT, kP, DestT, false>(g, pos, n, stride, dest, tile_rows, ws, s);
 }
@@ -851,6 +855,7 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // 1024-row wave tiles (16 rounds); more rounds for many bins keep the
     // [nbins][tiles] histogram small next to the payload.
     (void)row_bytes;
+    if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
     int r = 16;
     while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
@@ -918,7 +923,7 @@ template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                          int redirect_bin, void* redirect_dst, hipStream_t s) {
-    if (nb <= 64 && row_bytes <= 64 && W >= 4) {
+    if (g_tune.pack_small && nb <= 64 && row_bytes <= 64 && W >= 4) {
         const hipError_t e = pack_small_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
                                              ws, dst, redirect_bin, redirect_dst, s);
         if (e != hipErrorNotSupported) return e;

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Kernel A/B microbenchmark (GPU): per-kernel HIP-event times of the local
+stage (bin_count, scan, pack) on BASELINE config 2 for tuning-knob variants,
+next to torch's device copy of the same payload as a practical HBM ceiling."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import mpi_grid_redistribute_amd as mgr  # noqa: E402
+from mpi_grid_redistribute_amd import _lib  # noqa: E402
+
+N = int(os.environ.get("KB_N", 1 << 26))
+ITERS = int(os.environ.get("KB_ITERS", 10))
+
+
+def run(variant):
+    for k, v in variant.items():
+        _lib.tune(k, v)
+    part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
+    pos, rec = mgr.synth_uniform(N)
+    flat = rec.reshape(-1)
+    for _ in range(3):
+        part.partition_device(flat, 32, pos)
+    torch.cuda.synchronize()
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    for _ in range(ITERS):
+        part.partition_device(flat, 32, pos)
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    out = {}
+    for k in ("bin_count", "scan_reduce", "scan_apply", "pack"):
+        ms, cnt = _lib.profile_read(k)
+        out[k] = round(ms / max(cnt, 1), 4)
+    out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
+    out["pack_GBps"] = round(65 * N / (out["pack"] / 1e3) / 1e9, 1)
+    for k in ("bin_staged", "pack_small", "tile_rounds"):
+        _lib.tune(k, {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0}[k])
+    del part, pos, rec, flat
+    torch.cuda.empty_cache()
+    return out
+
+
+def copy_ceiling():
+    x = torch.empty(N * 32, dtype=torch.uint8, device="cuda")
+    y = torch.empty_like(x)
+    for _ in range(3):
+        y.copy_(x)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(ITERS):
+        y.copy_(x)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / ITERS
+    return {"copy_ms": round(ms, 4), "copy_GBps": round(2 * N * 32 / (ms / 1e3) / 1e9, 1)}
+
+
+if __name__ == "__main__":
+    variants = json.loads(os.environ.get("KB_VARIANTS", "[{}]"))
+    print(json.dumps({"n": N, **copy_ceiling()}), flush=True)
+    for v in variants:
+        print(json.dumps({"variant": v, **run(v)}), flush=True)
