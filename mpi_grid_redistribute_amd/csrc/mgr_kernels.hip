@@ -268,15 +268,15 @@ __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
 // Kernel 1 of the hot path: wrap + write back positions, destination of
 // every row, per-tile histogram (destination-major counts[b * T + tile]).
-// kStaged (16-byte aligned position rows of <= 64 B): each 64-row slab is
-// loaded with coalesced 16-byte vectors one round AHEAD into registers,
-// parked in wave-private LDS for the per-row math, and stored back the same
-// way; otherwise each lane reads its own row.
 constexpr int kStageMaxRowBytes = 64;
-constexpr int kSlabUnits = kStageMaxRowBytes * 64 / 16 / 64;   // uint4 per lane per slab (4)
 
-template <typename PosT, bool kPeriodic, typename DestT, bool kStaged, int DIM>
-__global__ __launch_bounds__(kBlock, 6) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
+// Kernel 1 body.  NU > 0: staged -- the 64-row slab of position rows
+// (64 * rb bytes, rb <= 64, 16-byte aligned) is read with fully coalesced
+// 16-byte loads into NU registers per lane ONE ROUND AHEAD, parked in
+// wave-private LDS for the per-row math, and written back the same way.
+// NU == 0: each lane reads and writes its own row.
+template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM>
+__global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
                                                            int32_t* __restrict__ counts,
@@ -293,15 +293,19 @@ __global__ __launch_bounds__(kBlock, 6) void bin_count_kernel(PosT* __restrict__
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     for (int b = lane; b < g.nbins; b += 64) hist[b] = 0;
-    // Slab of a round: nr * rb bytes at (row0 + r0) * rb, as 16-byte units
-    // u = lane + 64 k (k < kSlabUnits) plus a 4-byte tail on a partial slab.
-    uint4 nxt[kSlabUnits];
-    if (kStaged) {
+    // Prefetch registers: named scalars (an array here was demoted to scratch).
+    uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
+#define MGR_SLAB_LOAD(GS, UNITS)                                                   \
+    {                                                                              \
+        if (NU > 0 && lane < (UNITS)) n0 = (GS)[lane];                             \
+        if (NU > 1 && lane + 64 < (UNITS)) n1 = (GS)[lane + 64];                   \
+        if (NU > 2 && lane + 128 < (UNITS)) n2 = (GS)[lane + 128];                 \
+        if (NU > 3 && lane + 192 < (UNITS)) n3 = (GS)[lane + 192];                 \
+    }
+    if (NU > 0) {
         const int units = min(64, rows) * rb / 16;
         const uint4* gs = (const uint4*)((const uint8_t*)pos + row0 * rb);
-#pragma unroll
-        for (int k = 0; k < kSlabUnits; ++k)
-            if (lane + 64 * k < units) nxt[k] = gs[lane + 64 * k];
+        MGR_SLAB_LOAD(gs, units)
     }
     wave_sync();
     for (int r0 = 0; r0 < rows; r0 += 64) {
@@ -309,33 +313,35 @@ __global__ __launch_bounds__(kBlock, 6) void bin_count_kernel(PosT* __restrict__
         const int64_t grow0 = row0 + r0;
         const bool valid = lane < nr;
         unsigned b = 0;
-        if (kStaged) {
+        if (NU > 0) {
             const int units = nr * rb / 16;
             uint8_t* gslab = (uint8_t*)pos + grow0 * rb;
-#pragma unroll
-            for (int k = 0; k < kSlabUnits; ++k)
-                if (lane + 64 * k < units) ((uint4*)stage)[lane + 64 * k] = nxt[k];
-            for (int q = units * 4 + lane; q < nr * rb / 4; q += 64)
-                ((uint32_t*)stage)[q] = ((const uint32_t*)gslab)[q];
+            uint4* st = (uint4*)stage;
+            if (NU > 0 && lane < units) st[lane] = n0;
+            if (NU > 1 && lane + 64 < units) st[lane + 64] = n1;
+            if (NU > 2 && lane + 128 < units) st[lane + 128] = n2;
+            if (NU > 3 && lane + 192 < units) st[lane + 192] = n3;
+            if (nr * rb > units * 16 && lane < (nr * rb - units * 16) / 4)  // partial last slab
+                ((uint32_t*)stage)[units * 4 + lane] = ((const uint32_t*)gslab)[units * 4 + lane];
             if (r0 + 64 < rows) {  // next slab in flight while this one is binned
                 const int nu = min(64, rows - r0 - 64) * rb / 16;
                 const uint4* gs = (const uint4*)(gslab + 64 * rb);
-#pragma unroll
-                for (int k = 0; k < kSlabUnits; ++k)
-                    if (lane + 64 * k < nu) nxt[k] = gs[lane + 64 * k];
+                MGR_SLAB_LOAD(gs, nu)
             }
             wave_sync();
             if (valid)
                 b = (unsigned)bin_row<PosT, kPeriodic, DIM>((PosT*)(stage + lane * rb), g, nullptr);
             if (kPeriodic) {
                 wave_sync();
-#pragma unroll
-                for (int k = 0; k < kSlabUnits; ++k)
-                    if (lane + 64 * k < units)
-                        ((uint4*)gslab)[lane + 64 * k] = ((const uint4*)stage)[lane + 64 * k];
-                for (int q = units * 4 + lane; q < nr * rb / 4; q += 64)
-                    ((uint32_t*)gslab)[q] = ((const uint32_t*)stage)[q];
+                uint4* gd = (uint4*)gslab;
+                if (NU > 0 && lane < units) gd[lane] = st[lane];
+                if (NU > 1 && lane + 64 < units) gd[lane + 64] = st[lane + 64];
+                if (NU > 2 && lane + 128 < units) gd[lane + 128] = st[lane + 128];
+                if (NU > 3 && lane + 192 < units) gd[lane + 192] = st[lane + 192];
+                if (nr * rb > units * 16 && lane < (nr * rb - units * 16) / 4)
+                    ((uint32_t*)gslab)[units * 4 + lane] = ((const uint32_t*)stage)[units * 4 + lane];
             }
+#undef MGR_SLAB_LOAD
         } else {
             if (valid)
                 b = (unsigned)bin_row<PosT, kPeriodic, DIM>(pos + (grow0 + lane) * stride, g, nullptr);
@@ -557,28 +563,34 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
     }
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
-    const U* __restrict__ s_u = (const U*)src;
+    // Round = 64 rows = 64*UPR units of W bytes, contiguous in src.  Lane l
+    // moves units 64k + l (k < UPR): every load instruction reads 64*W
+    // contiguous bytes.  The unit's row (compile-time division by UPR) gets
+    // its slot from the lane that ranked it.
+    const U* __restrict__ s_u = (const U*)src + row0 * UPR;
     U* __restrict__ d_u = (U*)dst;
     U* __restrict__ r_u = (U*)redirect_dst;
-
     unsigned nb_next = 0;
     U nv[UPR];
-#define MGR_FETCH(R0)                                                   \
-    if ((R0) + lane < rows) {                                           \
-        const int64_t row_ = row0 + (R0) + lane;                        \
-        nb_next = dest[row_];                                           \
-        const U* sp_ = s_u + row_ * UPR;                                \
-        _Pragma("unroll") for (int k = 0; k < UPR; ++k) nv[k] = sp_[k]; \
-    }
-    MGR_FETCH(0)
+    if (lane < rows) nb_next = dest[row0 + lane];
+#pragma unroll
+    for (int k = 0; k < UPR; ++k)
+        if (64 * k + lane < rows * UPR) nv[k] = s_u[64 * k + lane];
     for (int r0 = 0; r0 < rows; r0 += 64) {
-        const bool valid = r0 + lane < rows;
+        const int nr = min(64, rows - r0);
+        const bool valid = lane < nr;
         const unsigned b = valid ? nb_next : 0u;
         U v[UPR];
 #pragma unroll
         for (int k = 0; k < UPR; ++k) v[k] = nv[k];
-        if (r0 + 64 < rows) { MGR_FETCH(r0 + 64) }
-#undef MGR_FETCH
+        if (r0 + 64 < rows) {  // next round in flight
+            const int nn = min(64, rows - r0 - 64);
+            if (lane < nn) nb_next = dest[row0 + r0 + 64 + lane];
+            const U* sp = s_u + (int64_t)(r0 + 64) * UPR;
+#pragma unroll
+            for (int k = 0; k < UPR; ++k)
+                if (64 * k + lane < nn * UPR) nv[k] = sp[64 * k + lane];
+        }
         // nbits ballots: rank inside the wave + per-bin counts for lane == bin
         unsigned long long peers = __ballot(valid);
         unsigned long long mine = peers;  // lanes whose bin == this lane's index
@@ -588,13 +600,21 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
             mine &= ((lane >> i) & 1) ? m : ~m;
         }
         if (!valid) peers = 0;
-        const int rk = rank_in(peers);
         const long long base = __shfl(next_slot, (int)b, 64);
         next_slot += __popcll(mine);
-        if (valid && (int)b != drop_bin) {
-            U* dp = ((int)b == redirect_bin ? r_u : d_u) + (base + rk) * UPR;
+        // per-row target: slot, or -1 (dropped / past the end); bit 62 = redirect
+        long long tgt = -1;
+        if (valid && (int)b != drop_bin)
+            tgt = (base + rank_in(peers)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
 #pragma unroll
-            for (int k = 0; k < UPR; ++k) dp[k] = v[k];
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane;
+            const int r = u / UPR, part = u - r * UPR;
+            const long long t = __shfl(tgt, r, 64);
+            if (u < nr * UPR && t >= 0) {
+                U* o = (t >> 62) ? r_u : d_u;
+                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[k];
+            }
         }
     }
 }
@@ -688,12 +708,12 @@ static int waves_per_block(int per_wave_lds) {
     return w < 1 ? 1 : (w > kWaves ? kWaves : w);
 }
 
-template <typename PosT, bool kP, typename DestT, bool kStaged, int DIM>
+template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto k = bin_count_kernel<PosT, kP, DestT, kStaged, DIM>;
+    auto k = bin_count_kernel<PosT, kP, DestT, NU, DIM>;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
-    const int per_wave = align16(g.nbins * 4) + (kStaged ? align16(64 * rb) : 0);
+    const int per_wave = align16(g.nbins * 4) + (NU > 0 ? align16(64 * rb) : 0);
     const int wpb = waves_per_block(per_wave);
     const int lds = per_wave * wpb;
     ensure_lds(k, lds);
@@ -703,14 +723,14 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     return hipGetLastError();
 }
 
-template <typename PosT, bool kP, typename DestT, bool kStaged>
+template <typename PosT, bool kP, typename DestT, int NU>
 static hipError_t bin_count_dim(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                                 int tile_rows, const Workspace& ws, hipStream_t s) {
     switch (g.dim) {
-        case 1: return bin_count_t<PosT, kP, DestT, kStaged, 1>(g, pos, n, stride, dest, tile_rows, ws, s);
-        case 2: return bin_count_t<PosT, kP, DestT, kStaged, 2>(g, pos, n, stride, dest, tile_rows, ws, s);
-        case 3: return bin_count_t<PosT, kP, DestT, kStaged, 3>(g, pos, n, stride, dest, tile_rows, ws, s);
-        default: return bin_count_t<PosT, kP, DestT, kStaged, 0>(g, pos, n, stride, dest, tile_rows, ws, s);
+        case 1: return bin_count_t<PosT, kP, DestT, NU, 1>(g, pos, n, stride, dest, tile_rows, ws, s);
+        case 2: return bin_count_t<PosT, kP, DestT, NU, 2>(g, pos, n, stride, dest, tile_rows, ws, s);
+        case 3: return bin_count_t<PosT, kP, DestT, NU, 3>(g, pos, n, stride, dest, tile_rows, ws, s);
+        default: return bin_count_t<PosT, kP, DestT, NU, 0>(g, pos, n, stride, dest, tile_rows, ws, s);
     }
 }
 
@@ -718,9 +738,15 @@ template <typename PosT, bool kP, typename DestT>
 static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
     const int64_t rb = stride * (int64_t)sizeof(PosT);
-    if (g_tune.bin_staged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0)
-        return bin_count_dim<PosT, kP, DestT, true>(g, pos, n, stride, dest, tile_rows, ws, s);
-    return bin_count_dim<PosT, kP, DestT, false>(g, pos, n, stride, dest, tile_rows, ws, s);
+    if (g_tune.bin_staged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0) {
+        switch ((int)((rb + 15) / 16)) {   // 16-byte units per lane per 64-row slab
+            case 1: return bin_count_dim<PosT, kP, DestT, 1>(g, pos, n, stride, dest, tile_rows, ws, s);
+            case 2: return bin_count_dim<PosT, kP, DestT, 2>(g, pos, n, stride, dest, tile_rows, ws, s);
+            case 3: return bin_count_dim<PosT, kP, DestT, 3>(g, pos, n, stride, dest, tile_rows, ws, s);
+            default: return bin_count_dim<PosT, kP, DestT, 4>(g, pos, n, stride, dest, tile_rows, ws, s);
+        }
+    }
+    return bin_count_dim<PosT, kP, DestT, 0>(g, pos, n, stride, dest, tile_rows, ws, s);
 }
 
 template <typename PosT, typename DestT>
