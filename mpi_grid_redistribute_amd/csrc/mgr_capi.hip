@@ -411,6 +411,8 @@ int mgr_tune(const char* key, int64_t value) {
     if (!key) return fail(MGR_EINVAL, "null key");
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_small")) mgr::g_tune.pack_small = (int)value;
+    else if (!strcmp(key, "bin_nt")) mgr::g_tune.bin_nt = (int)value;
+    else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
     else if (!strcmp(key, "tile_rounds")) {
         if (value < 0 || value > mgr::kMaxTileRows / 64 || (value && (64 * value) % mgr::kBlock))
             return fail(MGR_EINVAL, "tile_rounds %lld", (long long)value);

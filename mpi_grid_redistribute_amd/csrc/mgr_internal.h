@@ -80,6 +80,8 @@ struct Tune {
     int bin_staged = 1;    // stage 64-row position slabs through LDS
     int pack_small = 1;    // register-resident pack for <= 64 bins, <= 64-byte rows
     int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
+    int bin_nt = 0;        // nontemporal loads/stores of position slabs
+    int pack_nt = 0;       // nontemporal loads/stores of payload rows
 };
 extern Tune g_tune;
 

@@ -266,6 +266,45 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
+// Streaming accesses: NT selects the nontemporal (nt) cache policy for data
+// that is read or written exactly once.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (!NT) {
+        return *p;
+    } else if constexpr (sizeof(T) == 16) {
+        const u32x4_t x = __builtin_nontemporal_load((const u32x4_t*)p);
+        T r;
+        __builtin_memcpy(&r, &x, 16);
+        return r;
+    } else if constexpr (sizeof(T) == 8) {
+        const u32x2_t x = __builtin_nontemporal_load((const u32x2_t*)p);
+        T r;
+        __builtin_memcpy(&r, &x, 8);
+        return r;
+    } else {
+        return __builtin_nontemporal_load(p);
+    }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T* p, const T& v) {
+    if constexpr (!NT) {
+        *p = v;
+    } else if constexpr (sizeof(T) == 16) {
+        u32x4_t x;
+        __builtin_memcpy(&x, &v, 16);
+        __builtin_nontemporal_store(x, (u32x4_t*)p);
+    } else if constexpr (sizeof(T) == 8) {
+        u32x2_t x;
+        __builtin_memcpy(&x, &v, 8);
+        __builtin_nontemporal_store(x, (u32x2_t*)p);
+    } else {
+        __builtin_nontemporal_store(v, p);
+    }
+}
+
 // Kernel 1 of the hot path: wrap + write back positions, destination of
 // every row, per-tile histogram (destination-major counts[b * T + tile]).
 constexpr int kStageMaxRowBytes = 64;
@@ -275,7 +314,7 @@ constexpr int kStageMaxRowBytes = 64;
 // 16-byte loads into NU registers per lane ONE ROUND AHEAD, parked in
 // wave-private LDS for the per-row math, and written back the same way.
 // NU == 0: each lane reads and writes its own row.
-template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM>
+template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT>
 __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
@@ -297,10 +336,10 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
     uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
 #define MGR_SLAB_LOAD(GS, UNITS)                                                   \
     {                                                                              \
-        if (NU > 0 && lane < (UNITS)) n0 = (GS)[lane];                             \
-        if (NU > 1 && lane + 64 < (UNITS)) n1 = (GS)[lane + 64];                   \
-        if (NU > 2 && lane + 128 < (UNITS)) n2 = (GS)[lane + 128];                 \
-        if (NU > 3 && lane + 192 < (UNITS)) n3 = (GS)[lane + 192];                 \
+        if (NU > 0 && lane < (UNITS)) n0 = ld<NT>((GS) + lane);                    \
+        if (NU > 1 && lane + 64 < (UNITS)) n1 = ld<NT>((GS) + lane + 64);          \
+        if (NU > 2 && lane + 128 < (UNITS)) n2 = ld<NT>((GS) + lane + 128);        \
+        if (NU > 3 && lane + 192 < (UNITS)) n3 = ld<NT>((GS) + lane + 192);        \
     }
     if (NU > 0) {
         const int units = min(64, rows) * rb / 16;
@@ -316,11 +355,11 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
         if (NU > 0) {
             const int units = nr * rb / 16;
             uint8_t* gslab = (uint8_t*)pos + grow0 * rb;
-            uint4* st = (uint4*)stage;
-            if (NU > 0 && lane < units) st[lane] = n0;
-            if (NU > 1 && lane + 64 < units) st[lane + 64] = n1;
-            if (NU > 2 && lane + 128 < units) st[lane + 128] = n2;
-            if (NU > 3 && lane + 192 < units) st[lane + 192] = n3;
+            uint4* sg = (uint4*)stage;
+            if (NU > 0 && lane < units) sg[lane] = n0;
+            if (NU > 1 && lane + 64 < units) sg[lane + 64] = n1;
+            if (NU > 2 && lane + 128 < units) sg[lane + 128] = n2;
+            if (NU > 3 && lane + 192 < units) sg[lane + 192] = n3;
             if (nr * rb > units * 16 && lane < (nr * rb - units * 16) / 4)  // partial last slab
                 ((uint32_t*)stage)[units * 4 + lane] = ((const uint32_t*)gslab)[units * 4 + lane];
             if (r0 + 64 < rows) {  // next slab in flight while this one is binned
@@ -334,10 +373,10 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
             if (kPeriodic) {
                 wave_sync();
                 uint4* gd = (uint4*)gslab;
-                if (NU > 0 && lane < units) gd[lane] = st[lane];
-                if (NU > 1 && lane + 64 < units) gd[lane + 64] = st[lane + 64];
-                if (NU > 2 && lane + 128 < units) gd[lane + 128] = st[lane + 128];
-                if (NU > 3 && lane + 192 < units) gd[lane + 192] = st[lane + 192];
+                if (NU > 0 && lane < units) st<NT>(gd + lane, sg[lane]);
+                if (NU > 1 && lane + 64 < units) st<NT>(gd + lane + 64, sg[lane + 64]);
+                if (NU > 2 && lane + 128 < units) st<NT>(gd + lane + 128, sg[lane + 128]);
+                if (NU > 3 && lane + 192 < units) st<NT>(gd + lane + 192, sg[lane + 192]);
                 if (nr * rb > units * 16 && lane < (nr * rb - units * 16) / 4)
                     ((uint32_t*)gslab)[units * 4 + lane] = ((const uint32_t*)stage)[units * 4 + lane];
             }
@@ -546,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
 // from the same nbits ballots as the rank, so there is no LDS traffic.  The
 // next round's destinations and rows are prefetched while the current
 // round is ranked and stored.
-template <int W, int UPR>
+template <int W, int UPR, bool NT>
 __global__ __launch_bounds__(kBlock) void pack_small_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
     int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
@@ -575,7 +614,7 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
     if (lane < rows) nb_next = dest[row0 + lane];
 #pragma unroll
     for (int k = 0; k < UPR; ++k)
-        if (64 * k + lane < rows * UPR) nv[k] = s_u[64 * k + lane];
+        if (64 * k + lane < rows * UPR) nv[k] = ld<NT>(s_u + 64 * k + lane);
     for (int r0 = 0; r0 < rows; r0 += 64) {
         const int nr = min(64, rows - r0);
         const bool valid = lane < nr;
@@ -589,7 +628,7 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
             const U* sp = s_u + (int64_t)(r0 + 64) * UPR;
 #pragma unroll
             for (int k = 0; k < UPR; ++k)
-                if (64 * k + lane < nn * UPR) nv[k] = sp[64 * k + lane];
+                if (64 * k + lane < nn * UPR) nv[k] = ld<NT>(sp + 64 * k + lane);
         }
         // nbits ballots: rank inside the wave + per-bin counts for lane == bin
         unsigned long long peers = __ballot(valid);
@@ -613,7 +652,7 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
             const long long t = __shfl(tgt, r, 64);
             if (u < nr * UPR && t >= 0) {
                 U* o = (t >> 62) ? r_u : d_u;
-                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[k];
+                st<NT>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[k]);
             }
         }
     }
@@ -711,7 +750,8 @@ static int waves_per_block(int per_wave_lds) {
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto k = bin_count_kernel<PosT, kP, DestT, NU, DIM>;
+    auto k = g_tune.bin_nt ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true>
+                           : bin_count_kernel<PosT, kP, DestT, NU, DIM, false>;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = align16(g.nbins * 4) + (NU > 0 ? align16(64 * rb) : 0);
     const int wpb = waves_per_block(per_wave);
@@ -909,10 +949,16 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
                                int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                                void* redirect_dst, hipStream_t s) {
     const int64_t grid = (ws.T + kWaves - 1) / kWaves;
-    hipLaunchKernelGGL((pack_small_kernel<W, UPR>), dim3((unsigned)grid), dim3(kBlock), 0, s,
-                       (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
-                       ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
-                       (uint8_t*)redirect_dst);
+    if (g_tune.pack_nt)
+        hipLaunchKernelGGL((pack_small_kernel<W, UPR, true>), dim3((unsigned)grid), dim3(kBlock), 0,
+                           s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,
+                           redirect_bin, (uint8_t*)redirect_dst);
+    else
+        hipLaunchKernelGGL((pack_small_kernel<W, UPR, false>), dim3((unsigned)grid), dim3(kBlock), 0,
+                           s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,
+                           redirect_bin, (uint8_t*)redirect_dst);
     return hipGetLastError();
 }
 

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Run tools/hbm_probe.hip variants on 2 GiB (+2 GiB) and print GB/s (read+write)."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_hbm_probe.so")
+if not os.path.exists(SO):
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
+                    "-o", SO, os.path.join(HERE, "hbm_probe.hip")], check=True)
+lib = ctypes.CDLL(SO)
+lib.probe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+nbytes = int(os.environ.get("PROBE_BYTES", 2 << 30))
+x = torch.ones(nbytes, dtype=torch.uint8, device="cuda")
+y = torch.empty_like(x)
+names = ["copy_u1", "copy_u4", "copy_u8", "copy_u1_nt", "copy_u4_nt", "copy_u8_nt", "scatter8_u4"]
+res = {}
+for w, name in enumerate(names):
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        assert lib.probe(w, x.data_ptr(), y.data_ptr(), nbytes // 16, s) == 0
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        lib.probe(w, x.data_ptr(), y.data_ptr(), nbytes // 16, s)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / 10
+    res[name] = round(2 * nbytes / (ms / 1e3) / 1e9, 1)
+print(json.dumps(res))

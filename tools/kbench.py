@@ -37,8 +37,9 @@ def run(variant):
         out[k] = round(ms / max(cnt, 1), 4)
     out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
     out["pack_GBps"] = round(65 * N / (out["pack"] / 1e3) / 1e9, 1)
-    for k in ("bin_staged", "pack_small", "tile_rounds"):
-        _lib.tune(k, {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0}[k])
+    for k, v in {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0, "bin_nt": 0,
+                 "pack_nt": 0}.items():
+        _lib.tune(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
     return out
@@ -60,7 +61,8 @@ def copy_ceiling():
 
 
 if __name__ == "__main__":
-    variants = json.loads(os.environ.get("KB_VARIANTS", "[{}]"))
+    vf = os.environ.get("KB_VARIANTS_FILE")
+    variants = json.load(open(vf)) if vf else json.loads(os.environ.get("KB_VARIANTS", "[{}]"))
     print(json.dumps({"n": N, **copy_ceiling()}), flush=True)
     for v in variants:
         print(json.dumps({"variant": v, **run(v)}), flush=True)
