@@ -69,7 +69,7 @@ int mgr_plan_create(int dim, const int64_t* grid_topology, const double* box_len
 int mgr_plan_destroy(mgr_plan* plan);
 
 /* Rows per tile used by the histogram / pack kernels for rows of at most
- * max_row_bytes bytes and nbins destinations (multiple of 256).            */
+ * max_row_bytes bytes and nbins destinations (a multiple of 64 rows).      */
 int mgr_tile_rows(int64_t max_row_bytes, int nbins);
 /* Device workspace for n rows, nbins bins (incl. a drop bin if any).       */
 int64_t mgr_workspace_bytes(int64_t n, int nbins, int tile_rows);

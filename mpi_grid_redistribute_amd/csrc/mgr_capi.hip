@@ -180,16 +180,16 @@ int mgr_tile_rows(int64_t max_row_bytes, int nbins) {
 }
 
 int64_t mgr_workspace_bytes(int64_t n, int nbins, int tile_rows) {
-    if (n < 0 || nbins < 1 || tile_rows < mgr::kBlock) return -1;
+    if (n < 0 || nbins < 1 || tile_rows < 64) return -1;
     return mgr::workspace_bytes(n, nbins, tile_rows);
 }
 
 int mgr_dest_bytes(int nbins) { return mgr::dest_bytes(nbins); }
 
 static int check_tile(int tile_rows) {
-    if (tile_rows < mgr::kBlock || tile_rows > mgr::kMaxTileRows || tile_rows % mgr::kBlock)
-        return fail(MGR_EINVAL, "tile_rows %d must be a multiple of %d in [%d, %d]", tile_rows,
-                    mgr::kBlock, mgr::kBlock, mgr::kMaxTileRows);
+    if (tile_rows < 64 || tile_rows > mgr::kMaxTileRows || tile_rows % 64)
+        return fail(MGR_EINVAL, "tile_rows %d must be a multiple of 64 in [64, %d]", tile_rows,
+                    mgr::kMaxTileRows);
     return MGR_OK;
 }
 
@@ -414,7 +414,7 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "bin_nt")) mgr::g_tune.bin_nt = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
     else if (!strcmp(key, "tile_rounds")) {
-        if (value < 0 || value > mgr::kMaxTileRows / 64 || (value && (64 * value) % mgr::kBlock))
+        if (value < 0 || value > mgr::kMaxTileRows / 64)
             return fail(MGR_EINVAL, "tile_rounds %lld", (long long)value);
         mgr::g_tune.tile_rounds = (int)value;
     } else return fail(MGR_EINVAL, "unknown tuning key '%s'", key);

@@ -81,7 +81,7 @@ struct Tune {
     int pack_small = 1;    // register-resident pack for <= 64 bins, <= 64-byte rows
     int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
     int bin_nt = 0;        // nontemporal loads/stores of position slabs
-    int pack_nt = 0;       // nontemporal loads/stores of payload rows
+    int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores
 };
 extern Tune g_tune;
 

@@ -585,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
 // from the same nbits ballots as the rank, so there is no LDS traffic.  The
 // next round's destinations and rows are prefetched while the current
 // round is ranked and stored.
-template <int W, int UPR, bool NT>
+template <int W, int UPR, bool NT, bool NTS>
 __global__ __launch_bounds__(kBlock) void pack_small_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
     int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
             const long long t = __shfl(tgt, r, 64);
             if (u < nr * UPR && t >= 0) {
                 U* o = (t >> 62) ? r_u : d_u;
-                st<NT>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[k]);
+                st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[k]);
             }
         }
     }
@@ -949,16 +949,15 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
                                int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                                void* redirect_dst, hipStream_t s) {
     const int64_t grid = (ws.T + kWaves - 1) / kWaves;
-    if (g_tune.pack_nt)
-        hipLaunchKernelGGL((pack_small_kernel<W, UPR, true>), dim3((unsigned)grid), dim3(kBlock), 0,
-                           s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,
-                           redirect_bin, (uint8_t*)redirect_dst);
-    else
-        hipLaunchKernelGGL((pack_small_kernel<W, UPR, false>), dim3((unsigned)grid), dim3(kBlock), 0,
-                           s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,
-                           redirect_bin, (uint8_t*)redirect_dst);
+#define MGR_PSK(NT_, NTS_)                                                                  \
+    hipLaunchKernelGGL((pack_small_kernel<W, UPR, NT_, NTS_>), dim3((unsigned)grid), dim3(kBlock), \
+                       0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),    \
+                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,     \
+                       redirect_bin, (uint8_t*)redirect_dst)
+    if (g_tune.pack_nt >= 2) MGR_PSK(true, true);
+    else if (g_tune.pack_nt == 1) MGR_PSK(true, false);
+    else MGR_PSK(false, false);
+#undef MGR_PSK
     return hipGetLastError();
 }
 

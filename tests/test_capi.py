@@ -46,7 +46,7 @@ def test_host_only_entry_points(lib):
     assert lib.mgr_version().startswith(b"mgr ")
     assert lib.mgr_dest_bytes(8) == 1 and lib.mgr_dest_bytes(300) == 2
     tr = lib.mgr_tile_rows(32, 8)
-    assert tr % 256 == 0 and 256 <= tr <= 4096
+    assert tr % 64 == 0 and 64 <= tr <= 4096
     assert lib.mgr_workspace_bytes(1 << 20, 8, tr) > 0
     assert lib.mgr_workspace_bytes(-1, 8, tr) < 0
 
