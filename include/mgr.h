@@ -175,7 +175,7 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
                       double* pos, void* rec32, void* stream);
 
 /* -------------------------------------------------------------- tuning --
- * Kernel-variant knobs for A/B measurement ("bin_staged", "pack_small", "bin_nt", "pack_nt",
+ * Kernel-variant knobs for A/B measurement ("bin_staged", "pack_small", "bin_nt", "pack_nt", "pack_coop",
  * "tile_rounds"); the defaults are the shipped configuration.  Process-wide,
  * not thread-safe against concurrent launches.                           */
 int mgr_tune(const char* key, int64_t value);

@@ -412,9 +412,10 @@ int mgr_tune(const char* key, int64_t value) {
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_small")) mgr::g_tune.pack_small = (int)value;
     else if (!strcmp(key, "bin_nt")) mgr::g_tune.bin_nt = (int)value;
+    else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
     else if (!strcmp(key, "tile_rounds")) {
-        if (value < 0 || value > mgr::kMaxTileRows / 64)
+        if (value < 0 || value > 16)
             return fail(MGR_EINVAL, "tile_rounds %lld", (long long)value);
         mgr::g_tune.tile_rounds = (int)value;
     } else return fail(MGR_EINVAL, "unknown tuning key '%s'", key);

@@ -80,7 +80,8 @@ struct Tune {
     int bin_staged = 1;    // stage 64-row position slabs through LDS
     int pack_small = 1;    // register-resident pack for <= 64 bins, <= 64-byte rows
     int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
-    int bin_nt = 0;        // nontemporal loads/stores of position slabs
+    int bin_nt = 1;        // nontemporal loads/stores of position slabs
+    int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
     int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores
 };
 extern Tune g_tune;

@@ -658,6 +658,68 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
     }
 }
 
+// Block-cooperative pack for <= 64 bins and rows of <= 64 bytes: one
+// workgroup per tile of R rounds, wave w ranks and moves round w (64 rows)
+// in one shot -- the short-lived, fully parallel shape that streams best.
+// The waves exchange their per-bin counts through a [R][64] LDS table (one
+// barrier) to get each bin's base inside the tile.  Unit-transposed moves:
+// lane l moves W-byte units 64k + l of the round, so each load instruction
+// reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
+template <int W, int UPR, bool NT>
+__global__ __launch_bounds__(1024) void pack_coop_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst) {
+    using U = typename Unit<W>::T;
+    __shared__ int s_cnt[kMaxTileRows / 64][64];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * w;
+    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
+    const bool valid = lane < nr;
+    // issue every load of the round first
+    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
+    long long tbase = 0;
+    if (lane < nb) {
+        tbase = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) tbase -= bin_starts[lane];
+    }
+    const U* __restrict__ sp = (const U*)src + row0 * UPR;
+    U v[UPR];
+#pragma unroll
+    for (int k = 0; k < UPR; ++k)
+        if (64 * k + lane < nr * UPR) v[k] = ld<NT>(sp + 64 * k + lane);
+    // rank inside the wave; lane l counts bin l
+    unsigned long long peers = __ballot(valid);
+    unsigned long long mine = peers;
+    for (int i = 0; i < nbits; ++i) {
+        const unsigned long long m = __ballot((b >> i) & 1u);
+        peers &= ((b >> i) & 1u) ? m : ~m;
+        mine &= ((lane >> i) & 1) ? m : ~m;
+    }
+    if (!valid) peers = 0;
+    s_cnt[w][lane] = __popcll(mine);
+    __syncthreads();
+    for (int j = 0; j < w; ++j) tbase += s_cnt[j][lane];
+    const long long base = __shfl(tbase, (int)b, 64);
+    long long tgt = -1;
+    if (valid && (int)b != drop_bin)
+        tgt = (base + rank_in(peers)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+#pragma unroll
+    for (int k = 0; k < UPR; ++k) {
+        const int u = 64 * k + lane;
+        const int r = u / UPR, part = u - r * UPR;
+        const long long t = __shfl(tgt, r, 64);
+        if (u < nr * UPR && t >= 0) {
+            U* o = (t >> 62) ? r_u : d_u;
+            o[(t & ((1ll << 62) - 1)) * UPR + part] = v[k];
+        }
+    }
+}
+
 // --------------------------------------------------------- synthetic data
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -922,6 +984,10 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // [nbins][tiles] histogram small next to the payload.
     (void)row_bytes;
     if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
+    // <= 64 bins: 256-row tiles (one bin wave of 4 rounds, one 4-wave pack
+    // workgroup); more bins: longer tiles keep the [nbins][tiles] histogram
+    // small next to the payload.
+    if (nbins <= 64) return 256;
     int r = 16;
     while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
@@ -948,6 +1014,18 @@ template <int W, int UPR>
 static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                                int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                                void* redirect_dst, hipStream_t s) {
+    if (g_tune.pack_coop) {
+        const int threads = tile_rows;   // one wave per 64-row round of the tile
+#define MGR_PCK(NT_)                                                                          \
+        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_>), dim3((unsigned)ws.T), dim3(threads), \
+                           0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), \
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,  \
+                           redirect_bin, (uint8_t*)redirect_dst)
+        if (g_tune.pack_nt) MGR_PCK(true);
+        else MGR_PCK(false);
+#undef MGR_PCK
+        return hipGetLastError();
+    }
     const int64_t grid = (ws.T + kWaves - 1) / kWaves;
 #define MGR_PSK(NT_, NTS_)                                                                  \
     hipLaunchKernelGGL((pack_small_kernel<W, UPR, NT_, NTS_>), dim3((unsigned)grid), dim3(kBlock), \
