@@ -314,6 +314,9 @@ constexpr int kStageMaxRowBytes = 64;
 // 16-byte loads into NU registers per lane ONE ROUND AHEAD, parked in
 // wave-private LDS for the per-row math, and written back the same way.
 // NU == 0: each lane reads and writes its own row.
+// One workgroup per tile: its waves split the tile's 64-row rounds into
+// contiguous runs (wave w: rows [w*rows_per_wave, ...)), bin them, and add
+// their wave-aggregated counts into one LDS histogram for the tile.
 template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT>
 __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
@@ -323,15 +326,17 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
                                                            int per_wave_lds) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int wpb = blockDim.x >> 6;
-    const int64_t tile = (int64_t)blockIdx.x * wpb + w;
-    if (tile >= T) return;
-    int32_t* hist = (int32_t*)(smem + w * per_wave_lds);
-    uint8_t* stage = smem + w * per_wave_lds + align16(g.nbins * 4);
-    const int64_t row0 = tile * (int64_t)tile_rows;
-    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    const int nwaves = blockDim.x >> 6;
+    const int64_t tile = blockIdx.x;
+    int32_t* hist = (int32_t*)smem;
+    uint8_t* stage = smem + align16(g.nbins * 4) + w * per_wave_lds;
+    const int rows_per_wave = tile_rows / nwaves;
+    const int64_t tile0 = tile * (int64_t)tile_rows;
+    const int64_t row0 = tile0 + (int64_t)w * rows_per_wave;
+    const int rows = (int)max((int64_t)0, min((int64_t)rows_per_wave, n - row0));
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
-    for (int b = lane; b < g.nbins; b += 64) hist[b] = 0;
+    for (int b = threadIdx.x; b < g.nbins; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
     // Prefetch registers: named scalars (an array here was demoted to scratch).
     uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
 #define MGR_SLAB_LOAD(GS, UNITS)                                                   \
@@ -387,10 +392,11 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
         }
         if (valid) dest[grow0 + lane] = (DestT)b;
         const unsigned long long peers = match_bin(b, valid, g.nbits);
-        if (valid && rank_in(peers) == 0) hist[b] += __popcll(peers);  // leaders: distinct bins
+        if (valid && rank_in(peers) == 0) atomicAdd(&hist[b], __popcll(peers));
         wave_sync();
     }
-    for (int b = lane; b < g.nbins; b += 64) counts[(int64_t)b * T + tile] = hist[b];
+    __syncthreads();
+    for (int b = threadIdx.x; b < g.nbins; b += blockDim.x) counts[(int64_t)b * T + tile] = hist[b];
 }
 
 // get_cell_number_from_position / get_cell_indexes_from_position (API helpers).
@@ -815,12 +821,12 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     auto k = g_tune.bin_nt ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true>
                            : bin_count_kernel<PosT, kP, DestT, NU, DIM, false>;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
-    const int per_wave = align16(g.nbins * 4) + (NU > 0 ? align16(64 * rb) : 0);
-    const int wpb = waves_per_block(per_wave);
-    const int lds = per_wave * wpb;
+    const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
+    int nwaves = tile_rows / 64;                             // <= kWaves waves, whole rounds each
+    while (nwaves > kWaves || (tile_rows / 64) % nwaves) --nwaves;
+    const int lds = align16(g.nbins * 4) + per_wave * nwaves;
     ensure_lds(k, lds);
-    const int64_t grid = (ws.T + wpb - 1) / wpb;
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s, (PosT*)pos, n,
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nwaves), (size_t)lds, s, (PosT*)pos, n,
                        stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave);
     return hipGetLastError();
 }
@@ -984,10 +990,10 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // [nbins][tiles] histogram small next to the payload.
     (void)row_bytes;
     if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
-    // <= 64 bins: 256-row tiles (one bin wave of 4 rounds, one 4-wave pack
-    // workgroup); more bins: longer tiles keep the [nbins][tiles] histogram
+    // <= 64 bins: 1024-row tiles (bin: 4 waves x 4 rounds; pack: 16 waves x
+    // 1 round); more bins: longer tiles keep the [nbins][tiles] histogram
     // small next to the payload.
-    if (nbins <= 64) return 256;
+    if (nbins <= 64) return 1024;
     int r = 16;
     while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
