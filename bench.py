@@ -163,10 +163,21 @@ def main():
         elapsed = float(t.item())
 
     kernels = {}
-    for k in ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack"):
+    for k in ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack", "exchange"):
         ms, cnt = _lib.profile_read(k)
         if cnt:
             kernels[k] = {"avg_ms": ms / cnt, "launches": cnt}
+    xgmi = None
+    if world > 1 and "exchange" in kernels:
+        # bytes this rank moved over xGMI per exchange: its off-rank sends +
+        # receives (uniform input: (P-1)/P of the rows each way)
+        moved = 2 * n * 32 * (world - 1) / world
+        gbps = moved / (kernels["exchange"]["avg_ms"] / 1e3) / 1e9
+        xgmi = {"achieved": gbps, "peak": XGMI_PEAK_GBS, "unit": "GB/s",
+                "frac": gbps / XGMI_PEAK_GBS,
+                "note": "rank 0: bytes sent + received per grouped ncclSend/ncclRecv over its "
+                        "avg duration; peak = 7 links x 153 GB/s (link rate taken as "
+                        "bidirectional)"}
     dom = max(("bin_count", "pack"), key=lambda k: kernels.get(k, {"avg_ms": 0})["avg_ms"])
     avg_s = kernels[dom]["avg_ms"] / 1e3
     alg_bytes = BYTES_PER_PARTICLE[dom] * n
@@ -198,11 +209,13 @@ def main():
                          "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes},
             "kernels": kernels,
+            "xgmi": xgmi,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
+        comm.close()
         dist.destroy_process_group()
 
 

@@ -185,7 +185,8 @@ int mgr_tune(const char* key, int64_t value);
  * launch's own stream.  mgr_profile_read synchronises those events and
  * returns the accumulated device time (ms) and launch count of the named
  * kernel ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack",
- * "cell_ids", "bin_ids", "synth").                                         */
+ * "cell_ids", "bin_ids", "cellnum_idx", "synth") or of the RCCL grouped
+ * row exchange ("exchange").                                               */
 int mgr_profile_enable(int on);
 int mgr_profile_reset(void);
 int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);

@@ -95,7 +95,8 @@ void collect_locked() {
 const char* kernel_name(int k) {
     static const char* names[K_NUM_KERNELS] = {"bin_count", "scan_reduce", "scan_apply",
                                                "bin_totals", "pack", "cell_ids",
-                                               "bin_ids", "cellnum_idx", "synth"};
+                                               "bin_ids", "cellnum_idx", "synth",
+                                               "exchange"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -359,6 +360,7 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
     for (int p = 0; p < comm->size; ++p)
         if (p != me && (send_counts[p] > 0 || recv_counts[p] > 0)) any = true;
     if (any) {
+        mgr::prof_begin(s, mgr::K_EXCHANGE);
         NCCL_OK(ncclGroupStart());
         // Peers in ring order starting after me spread the first wave of
         // transfers over distinct xGMI links.
@@ -376,6 +378,7 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
             }
         }
         NCCL_OK(ncclGroupEnd());
+        mgr::prof_end(s, mgr::K_EXCHANGE);
     }
     if (!skip_self && send_counts[me] > 0) {
         for (int f = 0; f < nfields; ++f) {

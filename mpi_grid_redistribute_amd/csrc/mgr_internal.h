@@ -51,7 +51,7 @@ int nbits_for(int nbins);
 
 // Kernel ids for the profiler.
 enum KernelId { K_BIN_COUNT, K_SCAN_REDUCE, K_SCAN_APPLY, K_BIN_TOTALS, K_PACK, K_CELL_IDS,
-                K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_NUM_KERNELS };
+                K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_EXCHANGE, K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);
