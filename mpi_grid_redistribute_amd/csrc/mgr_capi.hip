@@ -417,6 +417,17 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "bin_nt")) mgr::g_tune.bin_nt = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
+    else if (!strcmp(key, "bin_skip_clean")) mgr::g_tune.bin_skip_clean = (int)value;
+    else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
+    else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
+    else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
+    else if (!strcmp(key, "bin_depth")) {
+        if (value < 1 || value > 2) return fail(MGR_EINVAL, "bin_depth %lld", (long long)value);
+        mgr::g_tune.bin_depth = (int)value;
+    } else if (!strcmp(key, "bin_waves")) {
+        if (value < 1 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);
+        mgr::g_tune.bin_waves = (int)value;
+    }
     else if (!strcmp(key, "tile_rounds")) {
         if (value < 0 || value > 16)
             return fail(MGR_EINVAL, "tile_rounds %lld", (long long)value);

@@ -83,6 +83,12 @@ struct Tune {
     int bin_nt = 1;        // nontemporal loads/stores of position slabs
     int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
     int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores
+    int bin_skip_clean = 1;  // write a position slab back only if a row changed
+    int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
+    int xcd_pack = 0;      // ... in the pack kernels
+    int pack_sorted = 0;   // pack through an LDS image sorted by destination
+    int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
+    int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
 };
 extern Tune g_tune;
 

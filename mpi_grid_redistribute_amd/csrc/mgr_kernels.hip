@@ -142,25 +142,36 @@ __device__ __forceinline__ long long floormod_i64(long long a, long long n) {
     return r;
 }
 
+template <typename PosT>
+__device__ __forceinline__ bool same_bits(PosT a, PosT b) {
+    if constexpr (sizeof(PosT) == 8) return __double_as_longlong((double)a) == __double_as_longlong((double)b);
+    else return __float_as_uint((float)a) == __float_as_uint((float)b);
+}
+
 // One coordinate: wrap (+ write back), bin, index wrap.  Returns the wrapped
 // index; *raw gets trunc(t/L*n) before the index wrap (cell indexes API).
+// The wrapped value is stored only when its bits differ from the input
+// (the in-place mutation of redist.py:68 / :328-329 is then complete: an
+// in-box coordinate wraps to itself) and *dirty records that a store happened.
 template <typename PosT, bool kPeriodic>
-__device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw) {
+__device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw,
+                                               bool* dirty) {
     long long k;
+    const PosT in = *p;
     if (sizeof(PosT) == 4 && g.compute_f32) {
-        float x = (float)*p;
+        float x = (float)in;
         if (kPeriodic) {
             x = wrap_f32(x, g.Lf[d], g.twoLf[d], g.fastf[d]);
-            *p = (PosT)x;
+            if (!same_bits((PosT)x, in)) { *p = (PosT)x; *dirty = true; }
         }
         const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];  // f32 / f32 -> f32
         k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
     } else {
-        double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)*p) : (double)*p;
+        double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)in) : (double)in;
         if (kPeriodic) {
             const double t = wrap_f64(x, g.L[d], g.twoL[d], g.fast[d]);
             const PosT w = sizeof(PosT) == 4 ? (PosT)f64_to_f32_x86(t) : (PosT)t;  // round (S9)
-            *p = w;
+            if (!same_bits(w, in)) { *p = w; *dirty = true; }
             x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)w) : (double)w;  // bin reads it (S2)
         }
         k = trunc_i64((g.pow2[d] ? x * g.invL[d] : x / g.L[d]) * g.nd[d]);
@@ -173,15 +184,16 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
 
 // DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
 template <typename PosT, bool kPeriodic, int DIM = 0>
-__device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx) {
+__device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx,
+                                             bool* dirty) {
     long long cell = 0;
     if (DIM > 0) {
 #pragma unroll
         for (int d = 0; d < DIM; ++d)
-            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr);
+            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr, dirty);
     } else {
         for (int d = 0; d < g.dim; ++d)
-            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr);
+            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr, dirty);
     }
     return cell;
 }
@@ -266,6 +278,18 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
+// XCD-contiguous tile order.  Workgroups are dealt to the 8 XCDs round-robin
+// (blockIdx % 8 labels the XCD, MI355X_MICROARCH.md "Workgroup dispatch"), so
+// tile = blockIdx would put neighbouring tiles on different L2s.  This
+// bijection gives each XCD label one contiguous run of T/8 tiles: the cache
+// lines that two neighbouring tiles' output segments share are then written
+// through ONE L2 and leave it as whole lines.  Speed only, never correctness.
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t T) {
+    const int64_t per = T >> 3;
+    if (bid < per * 8) return (bid & 7) * per + (bid >> 3);
+    return bid;
+}
+
 // Streaming accesses: NT selects the nontemporal (nt) cache policy for data
 // that is read or written exactly once.
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
@@ -311,23 +335,25 @@ constexpr int kStageMaxRowBytes = 64;
 
 // Kernel 1 body.  NU > 0: staged -- the 64-row slab of position rows
 // (64 * rb bytes, rb <= 64, 16-byte aligned) is read with fully coalesced
-// 16-byte loads into NU registers per lane ONE ROUND AHEAD, parked in
-// wave-private LDS for the per-row math, and written back the same way.
+// 16-byte loads into NU registers per lane DEPTH rounds ahead (two register
+// sets when DEPTH == 2), parked in wave-private LDS for the per-row math, and
+// written back the same way when a row of it changed.
 // NU == 0: each lane reads and writes its own row.
 // One workgroup per tile: its waves split the tile's 64-row rounds into
 // contiguous runs (wave w: rows [w*rows_per_wave, ...)), bin them, and add
 // their wave-aggregated counts into one LDS histogram for the tile.
-template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT>
-__global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
+template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT, int DEPTH>
+__global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
                                                            int32_t* __restrict__ counts,
                                                            int64_t T, int tile_rows,
-                                                           int per_wave_lds) {
+                                                           int per_wave_lds, int skip_clean,
+                                                           int xcd) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int nwaves = blockDim.x >> 6;
-    const int64_t tile = blockIdx.x;
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
     int32_t* hist = (int32_t*)smem;
     uint8_t* stage = smem + align16(g.nbins * 4) + w * per_wave_lds;
     const int rows_per_wave = tile_rows / nwaves;
@@ -337,45 +363,52 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     for (int b = threadIdx.x; b < g.nbins; b += blockDim.x) hist[b] = 0;
     __syncthreads();
-    // Prefetch registers: named scalars (an array here was demoted to scratch).
-    uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0, n2 = n0, n3 = n0;
-#define MGR_SLAB_LOAD(GS, UNITS)                                                   \
-    {                                                                              \
-        if (NU > 0 && lane < (UNITS)) n0 = ld<NT>((GS) + lane);                    \
-        if (NU > 1 && lane + 64 < (UNITS)) n1 = ld<NT>((GS) + lane + 64);          \
-        if (NU > 2 && lane + 128 < (UNITS)) n2 = ld<NT>((GS) + lane + 128);        \
-        if (NU > 3 && lane + 192 < (UNITS)) n3 = ld<NT>((GS) + lane + 192);        \
-    }
-    if (NU > 0) {
-        const int units = min(64, rows) * rb / 16;
-        const uint4* gs = (const uint4*)((const uint8_t*)pos + row0 * rb);
-        MGR_SLAB_LOAD(gs, units)
-    }
-    wave_sync();
-    for (int r0 = 0; r0 < rows; r0 += 64) {
-        const int nr = min(64, rows - r0);
-        const int64_t grow0 = row0 + r0;
-        const bool valid = lane < nr;
-        unsigned b = 0;
-        if (NU > 0) {
+
+    // destination byte + wave-aggregated histogram add of one round
+    auto account = [&](unsigned b, bool valid, int r0) {
+        if (valid) dest[row0 + r0 + lane] = (DestT)b;
+        const unsigned long long peers = match_bin(b, valid, g.nbits);
+        if (valid && rank_in(peers) == 0) atomicAdd(&hist[b], __popcll(peers));
+    };
+
+    if constexpr (NU > 0) {
+        // Prefetch registers: named scalars (an array here was demoted to scratch).
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        uint4 a0 = z, a1 = z, a2 = z, a3 = z, b0 = z, b1 = z, b2 = z, b3 = z;
+        // Every lane issues every load, without branches (index clamped into
+        // the slab; a slab past the wave's rows re-reads its first one), so the
+        // compiler's wait for the oldest slab is a counted vmcnt that leaves
+        // the younger one in flight.  A slab's last 16-byte unit may extend
+        // past its last row: an aligned 16-byte read that starts inside the
+        // buffer stays inside its page, and those bytes are never stored.
+        auto load = [&](uint4& x0, uint4& x1, uint4& x2, uint4& x3, int r) {
+            const int rr = r < rows ? r : 0;
+            const int cu = (min(64, rows - rr) * rb + 15) / 16;
+            const uint4* gs = (const uint4*)((const uint8_t*)pos + (row0 + rr) * rb);
+            if (NU > 0) x0 = ld<NT>(gs + min(lane, cu - 1));
+            if (NU > 1) x1 = ld<NT>(gs + min(lane + 64, cu - 1));
+            if (NU > 2) x2 = ld<NT>(gs + min(lane + 128, cu - 1));
+            if (NU > 3) x3 = ld<NT>(gs + min(lane + 192, cu - 1));
+        };
+        auto round = [&](uint4& x0, uint4& x1, uint4& x2, uint4& x3, int r0) {
+            const int nr = min(64, rows - r0);
+            const bool valid = lane < nr;
             const int units = nr * rb / 16;
-            uint8_t* gslab = (uint8_t*)pos + grow0 * rb;
+            const int cu = (nr * rb + 15) / 16;
+            uint8_t* gslab = (uint8_t*)pos + (row0 + r0) * rb;
             uint4* sg = (uint4*)stage;
-            if (NU > 0 && lane < units) sg[lane] = n0;
-            if (NU > 1 && lane + 64 < units) sg[lane + 64] = n1;
-            if (NU > 2 && lane + 128 < units) sg[lane + 128] = n2;
-            if (NU > 3 && lane + 192 < units) sg[lane + 192] = n3;
-            if (nr * rb > units * 16 && lane < (nr * rb - units * 16) / 4)  // partial last slab
-                ((uint32_t*)stage)[units * 4 + lane] = ((const uint32_t*)gslab)[units * 4 + lane];
-            if (r0 + 64 < rows) {  // next slab in flight while this one is binned
-                const int nu = min(64, rows - r0 - 64) * rb / 16;
-                const uint4* gs = (const uint4*)(gslab + 64 * rb);
-                MGR_SLAB_LOAD(gs, nu)
-            }
+            if (NU > 0 && lane < cu) sg[lane] = x0;
+            if (NU > 1 && lane + 64 < cu) sg[lane + 64] = x1;
+            if (NU > 2 && lane + 128 < cu) sg[lane + 128] = x2;
+            if (NU > 3 && lane + 192 < cu) sg[lane + 192] = x3;
+            load(x0, x1, x2, x3, r0 + 64 * DEPTH);  // DEPTH slabs in flight while this one is binned
             wave_sync();
+            unsigned b = 0;
+            bool dirty = false;
             if (valid)
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM>((PosT*)(stage + lane * rb), g, nullptr);
-            if (kPeriodic) {
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM>((PosT*)(stage + lane * rb), g, nullptr, &dirty);
+            // write the slab back only if a row of it changed (skip_clean)
+            if (kPeriodic && (!skip_clean || __ballot(dirty) != 0ull)) {
                 wave_sync();
                 uint4* gd = (uint4*)gslab;
                 if (NU > 0 && lane < units) st<NT>(gd + lane, sg[lane]);
@@ -385,16 +418,38 @@ __global__ __launch_bounds__(kBlock) void bin_count_kernel(PosT* __restrict__ po
                 if (nr * rb > units * 16 && lane < (nr * rb - units * 16) / 4)
                     ((uint32_t*)gslab)[units * 4 + lane] = ((const uint32_t*)stage)[units * 4 + lane];
             }
-#undef MGR_SLAB_LOAD
-        } else {
-            if (valid)
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM>(pos + (grow0 + lane) * stride, g, nullptr);
-        }
-        if (valid) dest[grow0 + lane] = (DestT)b;
-        const unsigned long long peers = match_bin(b, valid, g.nbits);
-        if (valid && rank_in(peers) == 0) atomicAdd(&hist[b], __popcll(peers));
+            account(b, valid, r0);
+            wave_sync();
+        };
+        if (rows <= 0) goto done;   // a trailing wave of the last tile
+        load(a0, a1, a2, a3, 0);
+        if (DEPTH == 2) load(b0, b1, b2, b3, 64);
         wave_sync();
+        if (DEPTH == 2) {
+            // both rounds on every trip: the loop-carried wait for set A then
+            // leaves set B's slab in flight (counted vmcnt)
+            int r0 = 0;
+            for (; r0 + 64 < rows; r0 += 128) {
+                round(a0, a1, a2, a3, r0);
+                round(b0, b1, b2, b3, r0 + 64);
+            }
+            if (r0 < rows) round(a0, a1, a2, a3, r0);
+        } else {
+            for (int r0 = 0; r0 < rows; r0 += 64) round(a0, a1, a2, a3, r0);
+        }
+    } else {
+        for (int r0 = 0; r0 < rows; r0 += 64) {
+            const bool valid = r0 + lane < rows;
+            unsigned b = 0;
+            bool dirty = false;
+            if (valid)
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM>(pos + (row0 + r0 + lane) * stride, g,
+                                                             nullptr, &dirty);
+            account(b, valid, r0);
+            wave_sync();
+        }
     }
+done:
     __syncthreads();
     for (int b = threadIdx.x; b < g.nbins; b += blockDim.x) counts[(int64_t)b * T + tile] = hist[b];
 }
@@ -408,7 +463,8 @@ __global__ __launch_bounds__(kBlock) void cell_ids_kernel(PosT* __restrict__ pos
     const int64_t step = (int64_t)gridDim.x * kBlock;
     for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < n; r += step) {
         long long* ip = idx ? (long long*)(idx + r * g.dim) : nullptr;
-        const long long c = bin_row<PosT, kPeriodic>(pos + r * stride, g, ip);
+        bool dirty = false;
+        const long long c = bin_row<PosT, kPeriodic>(pos + r * stride, g, ip, &dirty);
         if (cell) cell[r] = c;
     }
 }
@@ -676,11 +732,11 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kMaxTileRows / 64][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = blockIdx.x;
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
     const int64_t row0 = tile * (int64_t)tile_rows + 64 * w;
     const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
     const bool valid = lane < nr;
@@ -722,6 +778,96 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
         if (u < nr * UPR && t >= 0) {
             U* o = (t >> 62) ? r_u : d_u;
             o[(t & ((1ll << 62) - 1)) * UPR + part] = v[k];
+        }
+    }
+}
+
+// Destination-sorted pack for <= 64 bins and rows of <= 64 bytes.  As
+// pack_coop_kernel, one workgroup per tile and wave w ranks round w; but the
+// rows are first written into an LDS image of the tile SORTED by destination
+// (bin, then original order), and the image is then streamed out in order:
+// each store instruction writes 64*W contiguous bytes of one or two
+// destination runs instead of ~nbins short runs.  LDS: the image
+// (tile_rows * row bytes), the [rounds][64] count table and one bin byte per
+// sorted row.
+template <int W, int UPR, bool NT>
+__global__ __launch_bounds__(1024) void pack_sorted_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    using U = typename Unit<W>::T;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int R = tile_rows >> 6;
+    U* img = (U*)smem;
+    int* s_cnt = (int*)(smem + (size_t)tile_rows * UPR * W);
+    uint8_t* s_bin = (uint8_t*)(s_cnt + R * 64);
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t trow0 = tile * (int64_t)tile_rows;
+    const int64_t row0 = trow0 + 64 * w;
+    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
+    const int trows = (int)min((int64_t)tile_rows, n - trow0);
+    const bool valid = lane < nr;
+    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
+    long long tbase = 0;
+    if (lane < nb) {
+        tbase = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) tbase -= bin_starts[lane];
+    }
+    const U* __restrict__ sp = (const U*)src + row0 * UPR;
+    U v[UPR];
+#pragma unroll
+    for (int k = 0; k < UPR; ++k)
+        if (64 * k + lane < nr * UPR) v[k] = ld<NT>(sp + 64 * k + lane);
+    unsigned long long peers = __ballot(valid);
+    unsigned long long mine = peers;
+    for (int i = 0; i < nbits; ++i) {
+        const unsigned long long m = __ballot((b >> i) & 1u);
+        peers &= ((b >> i) & 1u) ? m : ~m;
+        mine &= ((lane >> i) & 1) ? m : ~m;
+    }
+    if (!valid) peers = 0;
+    s_cnt[w * 64 + lane] = __popcll(mine);
+    __syncthreads();
+    // lane = bin: rows of this bin in earlier rounds, and in the whole tile
+    int before = 0, tot = 0;
+    for (int j = 0; j < R; ++j) {
+        const int c = s_cnt[j * 64 + lane];
+        before += (j < w) ? c : 0;
+        tot += c;
+    }
+    // exclusive scan of the per-bin tile totals over the lanes: local bin start
+    int lstart = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(lstart, o, 64);
+        if (lane >= o) lstart += y;
+    }
+    lstart -= tot;
+    const int lpos = __shfl(lstart + before, (int)b, 64) + rank_in(peers);
+#pragma unroll
+    for (int k = 0; k < UPR; ++k) {
+        const int u = 64 * k + lane;
+        const int r = u / UPR, part = u - r * UPR;
+        const int t = __shfl(lpos, r, 64);
+        if (u < nr * UPR) img[t * UPR + part] = v[k];
+    }
+    if (valid) s_bin[lpos] = (uint8_t)b;
+    __syncthreads();
+    // stream the sorted image out: wave w writes sorted units [w*64*UPR, ...)
+    const long long delta = tbase - lstart;   // lane = bin: global slot - local position
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+#pragma unroll
+    for (int k = 0; k < UPR; ++k) {
+        const int u = w * 64 * UPR + 64 * k + lane;
+        const int p = u / UPR, part = u - p * UPR;
+        const int bb = p < trows ? (int)s_bin[p] : 0;
+        const long long dl = __shfl(delta, bb, 64);
+        if (p < trows && bb != drop_bin) {
+            U* o = bb == redirect_bin ? r_u : d_u;
+            o[(p + dl) * UPR + part] = img[u];
         }
     }
 }
@@ -818,16 +964,19 @@ static int waves_per_block(int per_wave_lds) {
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto k = g_tune.bin_nt ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true>
-                           : bin_count_kernel<PosT, kP, DestT, NU, DIM, false>;
+    auto k = g_tune.bin_nt ? (g_tune.bin_depth == 2 ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 2>
+                                                    : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>)
+                           : (g_tune.bin_depth == 2 ? bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 2>
+                                                    : bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 1>);
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
-    int nwaves = tile_rows / 64;                             // <= kWaves waves, whole rounds each
-    while (nwaves > kWaves || (tile_rows / 64) % nwaves) --nwaves;
+    int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each
+    while (nwaves > g_tune.bin_waves || (tile_rows / 64) % nwaves) --nwaves;
     const int lds = align16(g.nbins * 4) + per_wave * nwaves;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nwaves), (size_t)lds, s, (PosT*)pos, n,
-                       stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave);
+                       stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave,
+                       g_tune.bin_skip_clean, g_tune.xcd_bin);
     return hipGetLastError();
 }
 
@@ -1020,13 +1169,28 @@ template <int W, int UPR>
 static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                                int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                                void* redirect_dst, hipStream_t s) {
+    if (g_tune.pack_sorted && tile_rows <= 1024) {
+        const int threads = tile_rows;   // one wave per 64-row round of the tile
+        const int lds = tile_rows * UPR * W + (tile_rows / 64) * 64 * 4 + tile_rows;
+#define MGR_PSS(NT_)                                                                          \
+        {                                                                                     \
+        ensure_lds(pack_sorted_kernel<W, UPR, NT_>, lds);                                      \
+        hipLaunchKernelGGL((pack_sorted_kernel<W, UPR, NT_>), dim3((unsigned)ws.T), dim3(threads), \
+                           (size_t)lds, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb,   \
+                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack); }
+        if (g_tune.pack_nt) MGR_PSS(true)
+        else MGR_PSS(false)
+#undef MGR_PSS
+        return hipGetLastError();
+    }
     if (g_tune.pack_coop) {
         const int threads = tile_rows;   // one wave per 64-row round of the tile
 #define MGR_PCK(NT_)                                                                          \
         hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_>), dim3((unsigned)ws.T), dim3(threads), \
                            0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), \
                            drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,  \
-                           redirect_bin, (uint8_t*)redirect_dst)
+                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
         if (g_tune.pack_nt) MGR_PCK(true);
         else MGR_PCK(false);
 #undef MGR_PCK

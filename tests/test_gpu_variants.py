@@ -1,0 +1,108 @@
+"""GPU parity of every kernel variant the tuning knobs select (mgr_tune).
+
+The shipped defaults are covered by test_gpu_parity.py; here each non-default
+variant (destination-sorted LDS pack, XCD-contiguous tile order, unconditional
+position write-back) must give the same bytes on the same inputs: the C
+oracle on seeded inputs, and the reference's own golden fixtures.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import c_oracle
+from tests import golden_io as G
+from tests.fake_mpi import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+mgr = pytest.importorskip("mpi_grid_redistribute_amd")
+from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
+
+DEFAULTS = {"pack_sorted": 0, "xcd_pack": 0, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
+            "pack_small": 1, "pack_nt": 0, "bin_nt": 1, "bin_staged": 1, "tile_rounds": 0}
+VARIANTS = [
+    {"pack_sorted": 1},
+    {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
+    {"xcd_pack": 1, "xcd_bin": 1},
+    {"bin_skip_clean": 0},
+    {"pack_sorted": 1, "tile_rounds": 8},
+    {"pack_sorted": 1, "pack_nt": 1},
+    {"bin_waves": 16, "xcd_pack": 1},
+    {"bin_waves": 8, "bin_skip_clean": 0},
+    {"bin_depth": 2, "bin_waves": 2},
+    {"bin_depth": 2, "bin_skip_clean": 0, "bin_staged": 0},
+    {"bin_depth": 2, "bin_waves": 1, "xcd_bin": 1},
+]
+
+
+@pytest.fixture(params=VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
+def variant(request):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    for k, v in request.param.items():
+        _lib.tune(k, v)
+    yield request.param
+    for k, v in DEFAULTS.items():
+        _lib.tune(k, v)
+
+
+@pytest.mark.parametrize("topo,row_bytes", [([2, 2, 2], 32), ([2, 2, 2], 36), ([7], 8),
+                                            ([4, 4, 4], 12), ([3, 3, 3], 64), ([2], 4)])
+def test_partition_variant_vs_c_oracle(variant, topo, row_bytes):
+    rng = np.random.default_rng(row_bytes * 7 + len(topo))
+    n = 70_001 + row_bytes
+    dim = len(topo)
+    box = [1.0] * dim
+    pos = rng.uniform(0.0, 1.0, (n, dim))
+    # a few out-of-box rows: some 64-row slabs are dirty, most are clean
+    k = rng.integers(0, n, 300)
+    pos[k] = rng.uniform(-1.0, 2.0, (300, dim))
+    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
+    exp_pos = pos.copy()
+    cell = c_oracle.bin_positions(exp_pos, topo, box)
+    nb = int(np.prod(topo))
+    exp, exp_off = c_oracle.partition(data, cell, nb)
+    P = GridPartitioner(topo, box)
+    tpos = torch.from_numpy(pos).cuda()
+    out, off = P.partition_by_position(torch.from_numpy(data).cuda(), tpos)
+    assert G.same_bytes(tpos.cpu().numpy(), exp_pos)
+    assert np.array_equal(off.cpu().numpy(), exp_off)
+    assert np.array_equal(out.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("case", ["redist_p8_f64_rec32.npz", "redist_p8_rec36_view.npz",
+                                  "redist_p27_333_ids.npz", "redist_p2_f32_rec36.npz"])
+def test_golden_variant(variant, case):
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, periodic = f["topology"], f["box"], bool(f["periodic"])
+    pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
+    if bool(f["alias"]):
+        data = pos
+    elif "view" in case:
+        data = [d.copy() for d in G.per_rank(f, "data", size)]
+        pos = [d["pos"] for d in data]
+    else:
+        data = [d.copy() for d in G.per_rank(f, "data", size)]
+
+    def fn(comm, r):
+        return MPIGridRedistributor(comm, topo, box).redistribute_by_position(
+            data[r], pos[r], periodic=periodic)
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), (case, r)
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
+
+
+def test_cellnum_drop_variant(variant):
+    f = G.load("cellnum_p5_f32mat.npz")
+    size = int(f["size"])
+
+    def fn(comm, r):
+        return MPIGridRedistributor(comm, [size], [1.0]).redistribute_by_cell_number(
+            f[f"r{r}_data"], f[f"r{r}_ids"])
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), r

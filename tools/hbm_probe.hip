@@ -45,6 +45,24 @@ __global__ __launch_bounds__(256) void scatter8_k(const v4u* __restrict__ s, v4u
     }
 }
 
+// Read-only stream: each thread reads U units and folds them; the store
+// never fires (magic never matches) but keeps the loads alive.
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_k(const v4u* __restrict__ s, v4u* __restrict__ d,
+                                              int64_t n, unsigned magic) {
+    const int64_t base = ((int64_t)blockIdx.x * U) * 256 + threadIdx.x;
+    unsigned acc = 0;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int64_t i = base + k * 256;
+        if (i < n) {
+            const v4u v = NT ? __builtin_nontemporal_load(s + i) : s[i];
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == magic) d[base] = v4u{acc, 0, 0, 0};
+}
+
 extern "C" int probe(int which, const void* s, void* d, int64_t n16, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const v4u* S = (const v4u*)s;
@@ -58,6 +76,11 @@ extern "C" int probe(int which, const void* s, void* d, int64_t n16, void* strea
         case 4: hipLaunchKernelGGL((copy_k<4, true>), grid(4), dim3(256), 0, st, S, D, n16); break;
         case 5: hipLaunchKernelGGL((copy_k<8, true>), grid(8), dim3(256), 0, st, S, D, n16); break;
         case 6: hipLaunchKernelGGL((scatter8_k<4>), grid(4), dim3(256), 0, st, S, D, n16); break;
+        case 7: hipLaunchKernelGGL((read_k<1, false>), grid(1), dim3(256), 0, st, S, D, n16, 0xDEADBEEFu); break;
+        case 8: hipLaunchKernelGGL((read_k<1, true>), grid(1), dim3(256), 0, st, S, D, n16, 0xDEADBEEFu); break;
+        case 9: hipLaunchKernelGGL((read_k<4, false>), grid(4), dim3(256), 0, st, S, D, n16, 0xDEADBEEFu); break;
+        case 10: hipLaunchKernelGGL((read_k<4, true>), grid(4), dim3(256), 0, st, S, D, n16, 0xDEADBEEFu); break;
+        case 11: hipLaunchKernelGGL((read_k<16, true>), grid(16), dim3(256), 0, st, S, D, n16, 0xDEADBEEFu); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -10,7 +10,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SO = os.path.join(HERE, "_hbm_probe.so")
-if not os.path.exists(SO):
+if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(os.path.join(HERE, "hbm_probe.hip")):
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
                     "-o", SO, os.path.join(HERE, "hbm_probe.hip")], check=True)
 lib = ctypes.CDLL(SO)
@@ -18,7 +18,8 @@ lib.probe.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_i
 nbytes = int(os.environ.get("PROBE_BYTES", 2 << 30))
 x = torch.ones(nbytes, dtype=torch.uint8, device="cuda")
 y = torch.empty_like(x)
-names = ["copy_u1", "copy_u4", "copy_u8", "copy_u1_nt", "copy_u4_nt", "copy_u8_nt", "scatter8_u4"]
+names = ["copy_u1", "copy_u4", "copy_u8", "copy_u1_nt", "copy_u4_nt", "copy_u8_nt", "scatter8_u4",
+         "read_u1", "read_u1_nt", "read_u4", "read_u4_nt", "read_u16_nt"]
 res = {}
 for w, name in enumerate(names):
     s = torch.cuda.current_stream().cuda_stream
@@ -31,5 +32,6 @@ for w, name in enumerate(names):
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / 10
-    res[name] = round(2 * nbytes / (ms / 1e3) / 1e9, 1)
+    moved = nbytes if name.startswith("read") else 2 * nbytes
+    res[name] = round(moved / (ms / 1e3) / 1e9, 1)
 print(json.dumps(res))
