@@ -139,6 +139,27 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
 int mgr_bin_starts(int64_t n, int nbins, int tile_rows, const void* workspace,
                    const int64_t** out);
 
+/* ---------------------------------------------------------- halo (f1) --
+ * exchange_overload_by_position (redist.py:202-309), the overload/halo
+ * exchange that redistribute_by_position runs when overload_lengths is set
+ * (:161-166).  Per dimension d the reference selects the rows to send right
+ * with position[:, d] > rank_cell_limits[d,1] - overload_lengths[d] (:271,
+ * :274) and left with position[:, d] < rank_cell_limits[d,0] +
+ * overload_lengths[d] (:272, :275), compared in float64 (numpy promotion of
+ * the float32/float64 column against a float64 scalar; NaN selects none).
+ *
+ * mgr_halo_flags  : one pass over n position rows; flags[r] (uint16) bit 2d =
+ *                   coordinate d > hi[d], bit 2d+1 = coordinate d < lo[d].
+ *                   hi/lo: host arrays of dim doubles.
+ * mgr_select_count: selection (flags & mask) != 0 as a 2-bin partition for
+ *                   mgr_scan / mgr_pack (bin 0 = selected, in order; bin 1 =
+ *                   not selected, pass drop_bin = 1 to mgr_pack).  Workspace
+ *                   sized by mgr_workspace_bytes(n, 2, tile_rows).           */
+int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
+                   const double* hi, const double* lo, uint16_t* flags, void* stream);
+int mgr_select_count(const uint16_t* flags, int64_t n, int mask, void* dest, int tile_rows,
+                     void* workspace, void* stream);
+
 /* ------------------------------------------------------------ exchange --
  * Replaces comm.alltoall(send_buff) + np.concatenate (redist.py:199):
  * RCCL over xGMI, one process per GPU.  The unique id is made on one rank
@@ -163,6 +184,12 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
                       const int64_t* row_bytes, const int64_t* send_counts,
                       const int64_t* send_offsets, const int64_t* recv_counts,
                       const int64_t* recv_offsets, int skip_self, void* stream);
+/* One isend/irecv pair of the halo exchange (redist.py:289-303): send
+ * send_bytes to rank dest and receive recv_bytes from rank source, grouped
+ * (ncclSend + ncclRecv); dest == source == me is a device copy.  Sizes must
+ * match the peers' (exchange them first, e.g. as 8-byte messages).         */
+int mgr_sendrecv(mgr_comm* comm, const void* send, int64_t send_bytes, int dest, void* recv,
+                 int64_t recv_bytes, int source, void* stream);
 /* Element-wise max all-reduce of count doubles (bench timing, barriers).   */
 int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,
                                void* stream);
@@ -185,8 +212,8 @@ int mgr_tune(const char* key, int64_t value);
  * launch's own stream.  mgr_profile_read synchronises those events and
  * returns the accumulated device time (ms) and launch count of the named
  * kernel ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack",
- * "cell_ids", "bin_ids", "cellnum_idx", "synth") or of the RCCL grouped
- * row exchange ("exchange").                                               */
+ * "cell_ids", "bin_ids", "cellnum_idx", "synth", "halo") or of the RCCL
+ * grouped row exchange ("exchange").                                               */
 int mgr_profile_enable(int on);
 int mgr_profile_reset(void);
 int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);

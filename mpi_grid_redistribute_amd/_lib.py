@@ -43,6 +43,8 @@ SIGNATURES = {
     "mgr_partition_by_position": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I64, _P, _P, _P, _I,
                                        _P, _P]),
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
+    "mgr_halo_flags": (_I, [_P, _I, _I64, _I64, _I, _P, _P, _P, _P]),
+    "mgr_select_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
     "mgr_comm_unique_id": (_I, [_P]),
     "mgr_comm_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
     "mgr_comm_destroy": (_I, [_P]),
@@ -50,6 +52,7 @@ SIGNATURES = {
     "mgr_comm_size": (_I, [_P]),
     "mgr_exchange_counts": (_I, [_P, _P, _P, _P]),
     "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "mgr_sendrecv": (_I, [_P, _P, _I64, _I, _P, _I64, _I, _P]),
     "mgr_comm_allreduce_max_f64": (_I, [_P, _P, _P, _I64, _P]),
     "mgr_synth_uniform": (_I, [ctypes.c_uint64, _I64, _I64, _I, _P, _P, _P, _P]),
     "mgr_tune": (_I, [ctypes.c_char_p, _I64]),

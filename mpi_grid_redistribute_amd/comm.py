@@ -30,6 +30,9 @@ import torch
 from . import _lib
 
 
+_HALO_TAG = 0  # redist.py:290-299 uses tag 0 for every halo message
+
+
 def excl_cumsum(counts):
     out = np.zeros(len(counts), dtype=np.int64)
     if len(counts) > 1:
@@ -61,12 +64,23 @@ class Transport:
         """sends/outs: per-field uint8 tensors; counts/offsets in rows (host)."""
         raise NotImplementedError
 
+    def sendrecv(self, send, dest, recv, source):
+        """One isend/irecv pair of the halo exchange (redist.py:289-303):
+        send the flat uint8 tensor ``send`` to rank ``dest`` and fill ``recv``
+        (pre-sized by the caller) from rank ``source``."""
+        raise NotImplementedError
+
     def barrier(self):
         pass
 
 
 class SelfComm(Transport):
     """One rank, one GPU (or N virtual destinations on one GPU)."""
+
+    def sendrecv(self, send, dest, recv, source):
+        assert dest == 0 and source == 0 and send.numel() == recv.numel()
+        if recv.numel():
+            recv.copy_(send)
 
     def exchange_counts(self, send_counts):
         s = send_counts.detach().to("cpu").numpy().astype(np.int64)
@@ -146,6 +160,10 @@ class RcclComm(Transport):
         _lib.call("mgr_exchange_rows", self._h, nf, sp, rp, rb, arr(send_counts),
                   arr(send_offsets), arr(recv_counts), arr(recv_offsets), 1, _lib.stream_handle())
 
+    def sendrecv(self, send, dest, recv, source):
+        _lib.call("mgr_sendrecv", self._h, _lib.ptr(send), send.numel(), int(dest),
+                  _lib.ptr(recv), recv.numel(), int(source), _lib.stream_handle())
+
     def allreduce_max(self, values):
         t = torch.as_tensor(values, dtype=torch.float64, device="cuda").reshape(-1)
         out = torch.empty_like(t)
@@ -193,6 +211,18 @@ class MpiHostComm(Transport):
                 out[a:a + recv_counts[s] * rb].copy_(torch.from_numpy(np.ascontiguousarray(got[s])),
                                                      non_blocking=False)
 
+    def sendrecv(self, send, dest, recv, source):
+        host = send.detach().cpu().numpy() if send.numel() else np.zeros(0, np.uint8)
+        req = self.comm.isend(host, dest=int(dest), tag=_HALO_TAG)
+        got = self.comm.irecv(source=int(source), tag=_HALO_TAG).wait()
+        req.wait()
+        got = np.ascontiguousarray(got, dtype=np.uint8).reshape(-1)
+        if got.size != recv.numel():
+            raise RuntimeError(f"halo message from rank {source}: {got.size} bytes, "
+                               f"expected {recv.numel()}")
+        if got.size:
+            recv.copy_(torch.from_numpy(got))
+
     def barrier(self):
         self.comm.alltoall([0] * self.size)
 
@@ -226,6 +256,22 @@ class TorchDistComm(Transport):
             self.dist.all_to_all_single(out[: int(sum(out_split))], snd[:nsend].contiguous(),
                                         output_split_sizes=out_split, input_split_sizes=in_split,
                                         group=self.group)
+
+    def sendrecv(self, send, dest, recv, source):
+        if dest == self.rank and source == self.rank:
+            if recv.numel():
+                recv.copy_(send)
+            return
+        reqs = []
+        if send.numel():
+            reqs.append(self.dist.isend(send.contiguous(), self._global(dest), group=self.group))
+        if recv.numel():
+            reqs.append(self.dist.irecv(recv, self._global(source), group=self.group))
+        for r in reqs:
+            r.wait()
+
+    def _global(self, r):
+        return r if self.group is None else self.dist.get_global_rank(self.group, r)
 
     def barrier(self):
         self.dist.barrier(group=self.group)

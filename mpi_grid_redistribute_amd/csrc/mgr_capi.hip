@@ -96,7 +96,7 @@ const char* kernel_name(int k) {
     static const char* names[K_NUM_KERNELS] = {"bin_count", "scan_reduce", "scan_apply",
                                                "bin_totals", "pack", "cell_ids",
                                                "bin_ids", "cellnum_idx", "synth",
-                                               "exchange"};
+                                               "exchange", "halo"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -298,6 +298,33 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
                     nullptr, stream);
 }
 
+// ------------------------------------------------------ halo (f1)
+int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
+                   const double* hi, const double* lo, uint16_t* flags, void* stream) {
+    if (pos_dtype != MGR_F32 && pos_dtype != MGR_F64)
+        return fail(MGR_EINVAL, "positions must be float32 or float64 (dtype %d)", pos_dtype);
+    if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d", dim);
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    if (row_stride < dim) return fail(MGR_EINVAL, "row_stride %lld < dim %d", (long long)row_stride, dim);
+    if (!hi || !lo) return fail(MGR_EINVAL, "null thresholds");
+    if (n > 0 && (!pos || !flags)) return fail(MGR_EINVAL, "null argument");
+    HIP_OK(mgr::launch_halo_flags(pos, pos_dtype == MGR_F32, n, row_stride, dim, hi, lo, flags,
+                                  (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_select_count(const uint16_t* flags, int64_t n, int mask, void* dest, int tile_rows,
+                     void* workspace, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    if (n > 0 && (!flags || !dest || !workspace)) return fail(MGR_EINVAL, "null argument");
+    const mgr::Workspace ws = mgr::carve(workspace, n, 2, tile_rows);
+    HIP_OK(mgr::launch_select_count(flags, n, (unsigned)mask, (uint8_t*)dest, tile_rows, ws,
+                                    (hipStream_t)stream));
+    return MGR_OK;
+}
+
 // ------------------------------------------------------------ exchange
 int mgr_comm_unique_id(void* out_id) {
     if (!out_id) return fail(MGR_EINVAL, "null id");
@@ -391,6 +418,27 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
     return MGR_OK;
 }
 
+int mgr_sendrecv(mgr_comm* comm, const void* send, int64_t send_bytes, int dest, void* recv,
+                 int64_t recv_bytes, int source, void* stream) {
+    if (!comm) return fail(MGR_EINVAL, "null comm");
+    if (dest < 0 || dest >= comm->size || source < 0 || source >= comm->size)
+        return fail(MGR_EINVAL, "peer out of range (dest %d, source %d, size %d)", dest, source,
+                    comm->size);
+    if (send_bytes < 0 || recv_bytes < 0) return fail(MGR_EINVAL, "negative size");
+    if ((send_bytes > 0 && !send) || (recv_bytes > 0 && !recv)) return fail(MGR_EINVAL, "null buffer");
+    hipStream_t s = (hipStream_t)stream;
+    if (dest == comm->rank && source == comm->rank) {   // self exchange: a device copy
+        if (send_bytes != recv_bytes) return fail(MGR_EINVAL, "self sendrecv size mismatch");
+        if (send_bytes > 0) HIP_OK(hipMemcpyAsync(recv, send, (size_t)send_bytes, hipMemcpyDeviceToDevice, s));
+        return MGR_OK;
+    }
+    NCCL_OK(ncclGroupStart());
+    if (send_bytes > 0) NCCL_OK(ncclSend(send, (size_t)send_bytes, ncclUint8, dest, comm->nccl, s));
+    if (recv_bytes > 0) NCCL_OK(ncclRecv(recv, (size_t)recv_bytes, ncclUint8, source, comm->nccl, s));
+    NCCL_OK(ncclGroupEnd());
+    return MGR_OK;
+}
+
 int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,
                                void* stream) {
     if (!comm || !in || !out || count < 0) return fail(MGR_EINVAL, "bad argument");
@@ -421,8 +469,11 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
-    else if (!strcmp(key, "bin_depth")) {
-        if (value < 1 || value > 2) return fail(MGR_EINVAL, "bin_depth %lld", (long long)value);
+    else if (!strcmp(key, "pack_rpw")) {
+        if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
+        mgr::g_tune.pack_rpw = (int)value;
+    } else if (!strcmp(key, "bin_depth")) {
+        if (value < 1 || value > 4) return fail(MGR_EINVAL, "bin_depth %lld", (long long)value);
         mgr::g_tune.bin_depth = (int)value;
     } else if (!strcmp(key, "bin_waves")) {
         if (value < 1 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);

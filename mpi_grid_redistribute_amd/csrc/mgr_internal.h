@@ -51,7 +51,7 @@ int nbits_for(int nbins);
 
 // Kernel ids for the profiler.
 enum KernelId { K_BIN_COUNT, K_SCAN_REDUCE, K_SCAN_APPLY, K_BIN_TOTALS, K_PACK, K_CELL_IDS,
-                K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_EXCHANGE, K_NUM_KERNELS };
+                K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_EXCHANGE, K_HALO, K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);
@@ -74,6 +74,10 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
+hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
+                             const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
+hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,
+                               int tile_rows, const Workspace& ws, hipStream_t s);
 
 // Tuning knobs (mgr_tune); defaults are the shipped configuration.
 struct Tune {
@@ -85,10 +89,11 @@ struct Tune {
     int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores
     int bin_skip_clean = 1;  // write a position slab back only if a row changed
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
-    int xcd_pack = 0;      // ... in the pack kernels
+    int xcd_pack = 1;      // ... in the pack kernels
     int pack_sorted = 0;   // pack through an LDS image sorted by destination
-    int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
-    int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
+    int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
+    int bin_depth = 2;     // position slabs in flight per bin wave (1..4)
+    int bin_waves = 1;     // waves per bin workgroup (1..16; a tile's rounds split over them)
 };
 extern Tune g_tune;
 

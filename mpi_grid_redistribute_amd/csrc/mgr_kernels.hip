@@ -375,6 +375,7 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
         // Prefetch registers: named scalars (an array here was demoted to scratch).
         const uint4 z = make_uint4(0, 0, 0, 0);
         uint4 a0 = z, a1 = z, a2 = z, a3 = z, b0 = z, b1 = z, b2 = z, b3 = z;
+        uint4 c0 = z, c1 = z, c2 = z, c3 = z, e0 = z, e1 = z, e2 = z, e3 = z;
         // Every lane issues every load, without branches (index clamped into
         // the slab; a slab past the wave's rows re-reads its first one), so the
         // compiler's wait for the oldest slab is a counted vmcnt that leaves
@@ -423,19 +424,24 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
         };
         if (rows <= 0) goto done;   // a trailing wave of the last tile
         load(a0, a1, a2, a3, 0);
-        if (DEPTH == 2) load(b0, b1, b2, b3, 64);
+        if (DEPTH > 1) load(b0, b1, b2, b3, 64);
+        if (DEPTH > 2) load(c0, c1, c2, c3, 128);
+        if (DEPTH > 3) load(e0, e1, e2, e3, 192);
         wave_sync();
-        if (DEPTH == 2) {
-            // both rounds on every trip: the loop-carried wait for set A then
-            // leaves set B's slab in flight (counted vmcnt)
+        {
+            // DEPTH rounds on every trip, one register set each: the
+            // loop-carried wait for the oldest set is then a counted vmcnt
+            // that leaves the younger sets' slabs in flight
             int r0 = 0;
-            for (; r0 + 64 < rows; r0 += 128) {
+            for (; r0 + 64 * (DEPTH - 1) < rows; r0 += 64 * DEPTH) {
                 round(a0, a1, a2, a3, r0);
-                round(b0, b1, b2, b3, r0 + 64);
+                if (DEPTH > 1) round(b0, b1, b2, b3, r0 + 64);
+                if (DEPTH > 2) round(c0, c1, c2, c3, r0 + 128);
+                if (DEPTH > 3) round(e0, e1, e2, e3, r0 + 192);
             }
             if (r0 < rows) round(a0, a1, a2, a3, r0);
-        } else {
-            for (int r0 = 0; r0 < rows; r0 += 64) round(a0, a1, a2, a3, r0);
+            if (DEPTH > 2 && r0 + 64 < rows) round(b0, b1, b2, b3, r0 + 64);
+            if (DEPTH > 3 && r0 + 128 < rows) round(c0, c1, c2, c3, r0 + 128);
         }
     } else {
         for (int r0 = 0; r0 < rows; r0 += 64) {
@@ -727,7 +733,7 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
 // barrier) to get each bin's base inside the tile.  Unit-transposed moves:
 // lane l moves W-byte units 64k + l of the round, so each load instruction
 // reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
-template <int W, int UPR, bool NT>
+template <int W, int UPR, bool NT, int RPW>
 __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
@@ -737,47 +743,66 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     __shared__ int s_cnt[kMaxTileRows / 64][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
-    const int64_t row0 = tile * (int64_t)tile_rows + 64 * w;
-    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
-    const bool valid = lane < nr;
-    // issue every load of the round first
-    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
+    // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
+    // issue every load of the wave's rounds first
+    int nr[RPW];
+    unsigned b[RPW];
+    U v[RPW][UPR];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
+        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+    }
     long long tbase = 0;
     if (lane < nb) {
         tbase = offsets[(int64_t)lane * T + tile];
         if (lane == redirect_bin) tbase -= bin_starts[lane];
     }
-    const U* __restrict__ sp = (const U*)src + row0 * UPR;
-    U v[UPR];
 #pragma unroll
-    for (int k = 0; k < UPR; ++k)
-        if (64 * k + lane < nr * UPR) v[k] = ld<NT>(sp + 64 * k + lane);
-    // rank inside the wave; lane l counts bin l
-    unsigned long long peers = __ballot(valid);
-    unsigned long long mine = peers;
-    for (int i = 0; i < nbits; ++i) {
-        const unsigned long long m = __ballot((b >> i) & 1u);
-        peers &= ((b >> i) & 1u) ? m : ~m;
-        mine &= ((lane >> i) & 1) ? m : ~m;
+    for (int q = 0; q < RPW; ++q) {
+        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+#pragma unroll
+        for (int k = 0; k < UPR; ++k)
+            if (64 * k + lane < nr[q] * UPR) v[q][k] = ld<NT>(sp + 64 * k + lane);
     }
-    if (!valid) peers = 0;
-    s_cnt[w][lane] = __popcll(mine);
+    // rank inside each round; lane l counts bin l
+    unsigned long long peers[RPW];
+    int cnt[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const bool valid = lane < nr[q];
+        unsigned long long pe = __ballot(valid);
+        unsigned long long mine = pe;
+        for (int i = 0; i < nbits; ++i) {
+            const unsigned long long m = __ballot((b[q] >> i) & 1u);
+            pe &= ((b[q] >> i) & 1u) ? m : ~m;
+            mine &= ((lane >> i) & 1) ? m : ~m;
+        }
+        peers[q] = valid ? pe : 0ull;
+        cnt[q] = __popcll(mine);
+        s_cnt[w * RPW + q][lane] = cnt[q];
+    }
     __syncthreads();
-    for (int j = 0; j < w; ++j) tbase += s_cnt[j][lane];
-    const long long base = __shfl(tbase, (int)b, 64);
-    long long tgt = -1;
-    if (valid && (int)b != drop_bin)
-        tgt = (base + rank_in(peers)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
+    for (int j = 0; j < w * RPW; ++j) tbase += s_cnt[j][lane];
     U* __restrict__ d_u = (U*)dst;
     U* __restrict__ r_u = (U*)redirect_dst;
 #pragma unroll
-    for (int k = 0; k < UPR; ++k) {
-        const int u = 64 * k + lane;
-        const int r = u / UPR, part = u - r * UPR;
-        const long long t = __shfl(tgt, r, 64);
-        if (u < nr * UPR && t >= 0) {
-            U* o = (t >> 62) ? r_u : d_u;
-            o[(t & ((1ll << 62) - 1)) * UPR + part] = v[k];
+    for (int q = 0; q < RPW; ++q) {
+        const long long base = __shfl(tbase, (int)b[q], 64);
+        long long tgt = -1;
+        if (lane < nr[q] && (int)b[q] != drop_bin)
+            tgt = (base + rank_in(peers[q])) | ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
+        tbase += cnt[q];
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane;
+            const int r = u / UPR, part = u - r * UPR;
+            const long long t = __shfl(tgt, r, 64);
+            if (u < nr[q] * UPR && t >= 0) {
+                U* o = (t >> 62) ? r_u : d_u;
+                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
+            }
         }
     }
 }
@@ -869,6 +894,63 @@ __global__ __launch_bounds__(1024) void pack_sorted_kernel(
             U* o = bb == redirect_bin ? r_u : d_u;
             o[(p + dl) * UPR + part] = img[u];
         }
+    }
+}
+
+// ---------------------------------------------------------- halo (f1)
+// exchange_overload_by_position (redist.py:202-309) selects, per dimension
+// d, the rows with position[:, d] > limits[d,1] - ol[d] (sent to the right
+// neighbour, :271/:274) and position[:, d] < limits[d,0] + ol[d] (to the
+// left, :272/:275).  numpy compares the float32/float64 column against the
+// float64 threshold in float64 (exact), NaN selects nothing.
+struct HaloThr { double hi[MGR_MAX_DIM]; double lo[MGR_MAX_DIM]; };
+
+// flags[r] bit 2d: coordinate d > hi[d]; bit 2d+1: coordinate d < lo[d].
+template <typename PosT>
+__global__ __launch_bounds__(kBlock) void halo_flags_kernel(const PosT* __restrict__ pos,
+                                                            int64_t n, int64_t stride, int dim,
+                                                            HaloThr t,
+                                                            uint16_t* __restrict__ flags) {
+    const int64_t step = (int64_t)gridDim.x * kBlock;
+    for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < n; r += step) {
+        unsigned f = 0;
+        for (int d = 0; d < dim; ++d) {
+            const double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)pos[r * stride + d])
+                                               : (double)pos[r * stride + d];
+            f |= (x > t.hi[d] ? 1u : 0u) << (2 * d);
+            f |= (x < t.lo[d] ? 1u : 0u) << (2 * d + 1);
+        }
+        flags[r] = (uint16_t)f;
+    }
+}
+
+// Selection as a 2-bin partition for mgr_scan / mgr_pack: bin 0 = selected
+// ((flags & mask) != 0), bin 1 = not (the drop bin).  Wave-private tiles of
+// tile_rows rows; counts[b * T + tile].
+__global__ __launch_bounds__(kBlock) void select_count_kernel(const uint16_t* __restrict__ flags,
+                                                              int64_t n, unsigned mask,
+                                                              uint8_t* __restrict__ dest,
+                                                              int32_t* __restrict__ counts,
+                                                              int64_t T, int tile_rows) {
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * kWaves + w;
+    if (tile >= T) return;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    int sel = 0, all = 0;
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const bool valid = r0 + lane < rows;
+        bool on = false;
+        if (valid) {
+            on = (flags[row0 + r0 + lane] & mask) != 0;
+            dest[row0 + r0 + lane] = on ? 0 : 1;
+        }
+        sel += __popcll(__ballot(on));
+        all += __popcll(__ballot(valid));
+    }
+    if (lane == 0) {
+        counts[tile] = sel;
+        counts[T + tile] = all - sel;
     }
 }
 
@@ -964,10 +1046,18 @@ static int waves_per_block(int per_wave_lds) {
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto k = g_tune.bin_nt ? (g_tune.bin_depth == 2 ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 2>
-                                                    : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>)
-                           : (g_tune.bin_depth == 2 ? bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 2>
-                                                    : bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 1>);
+    auto pick = [](int depth, auto k1, auto k2, auto k3, auto k4) {
+        return depth >= 4 ? k4 : depth == 3 ? k3 : depth == 2 ? k2 : k1;
+    };
+    auto k = g_tune.bin_nt
+                 ? pick(g_tune.bin_depth, bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>,
+                        bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 2>,
+                        bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 3>,
+                        bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 4>)
+                 : pick(g_tune.bin_depth, bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 1>,
+                        bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 2>,
+                        bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 3>,
+                        bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 4>);
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
     int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each
@@ -1142,7 +1232,7 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // <= 64 bins: 1024-row tiles (bin: 4 waves x 4 rounds; pack: 16 waves x
     // 1 round); more bins: longer tiles keep the [nbins][tiles] histogram
     // small next to the payload.
-    if (nbins <= 64) return 1024;
+    if (nbins <= 64) return 1024 * g_tune.pack_rpw;
     int r = 16;
     while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
@@ -1185,14 +1275,19 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
         return hipGetLastError();
     }
     if (g_tune.pack_coop) {
-        const int threads = tile_rows;   // one wave per 64-row round of the tile
-#define MGR_PCK(NT_)                                                                          \
-        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_>), dim3((unsigned)ws.T), dim3(threads), \
-                           0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), \
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,  \
-                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
-        if (g_tune.pack_nt) MGR_PCK(true);
-        else MGR_PCK(false);
+        // one wave per RPW 64-row rounds of the tile (<= 16 waves)
+        const int rpw = tile_rows > 1024 ? 2 : 1;
+        const int threads = tile_rows / rpw;
+#define MGR_PCK(NT_, RPW_)                                                                    \
+        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_>), dim3((unsigned)ws.T),       \
+                           dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
+                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
+        if (g_tune.pack_nt) {
+            if (rpw == 2) MGR_PCK(true, 2); else MGR_PCK(true, 1);
+        } else {
+            if (rpw == 2) MGR_PCK(false, 2); else MGR_PCK(false, 1);
+        }
 #undef MGR_PCK
         return hipGetLastError();
     }
@@ -1271,6 +1366,36 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
     else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
     prof_end(s, K_PACK);
     return e;
+}
+
+hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
+                             const double* hi, const double* lo, uint16_t* flags, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    HaloThr t;
+    for (int d = 0; d < MGR_MAX_DIM; ++d) {
+        t.hi[d] = d < dim ? hi[d] : 0.0;
+        t.lo[d] = d < dim ? lo[d] : 0.0;
+    }
+    prof_begin(s, K_HALO);
+    if (pos_f32)
+        hipLaunchKernelGGL(halo_flags_kernel<float>, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                           (const float*)pos, n, stride, dim, t, flags);
+    else
+        hipLaunchKernelGGL(halo_flags_kernel<double>, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                           (const double*)pos, n, stride, dim, t, flags);
+    prof_end(s, K_HALO);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,
+                               int tile_rows, const Workspace& ws, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t grid = (ws.T + kWaves - 1) / kWaves;
+    prof_begin(s, K_HALO);
+    hipLaunchKernelGGL(select_count_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, flags, n,
+                       mask, dest, ws.counts, ws.T, tile_rows);
+    prof_end(s, K_HALO);
+    return hipGetLastError();
 }
 
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,

@@ -24,8 +24,8 @@ Documented divergences from the reference:
     method, redist.py:13, S13);
   * ``return_positions=True`` returns ``(data, positions)`` (the reference
     documents it as not implemented and ignores it, redist.py:141-145);
-  * ``overload_lengths`` (the halo exchange, redist.py:202-309) is not built
-    yet and raises NotImplementedError;
+  * the overload (halo) exchange (redist.py:202-309, halo.py) needs one rank
+    per grid cell (the reference deadlocks otherwise);
   * payloads are moved as bytes: object dtypes are refused (the reference
     pickles them).
 """
@@ -40,6 +40,7 @@ from . import _lib
 from ._arrays import Positions, Rows, box_dtype_code, device, id_array
 from .comm import SelfComm, as_transport
 from .exchange import exchange
+from .halo import exchange_overload
 
 
 class _Plan:
@@ -169,17 +170,20 @@ class MPIGridRedistributor:
                                  return_positions=False):
         """redist.py:115-166.  Returns the rows of ``data`` whose position
         falls in this rank's cell, from every rank, in source-rank order;
-        ``position`` is wrapped in place when periodic (S1)."""
-        if overload_lengths is not None:
-            raise NotImplementedError(
-                "overload_lengths (halo exchange, redist.py:202-309) is not implemented yet")
+        ``position`` is wrapped in place when periodic (S1).  With
+        ``overload_lengths`` the halo rows follow (redist.py:161-166; the
+        halo exchange always runs periodic, :165)."""
         self._check_host_alias(data, position)
         rows = Rows(data, self._dev)
         pos = Positions(position, self.dim, self._dev, data_rows=rows)
         if pos.n != rows.n:
             raise ValueError(f"data has {rows.n} rows, position has {pos.n}")
+        halo = overload_lengths is not None
+        if halo:
+            self._check_halo(overload_lengths)
+        want_pos = return_positions or halo
         fields = [rows]
-        if return_positions:
+        if want_pos:
             fields.append(None)  # filled after binning (wrapped values)
 
         def binner(dest, tile_rows, ws):
@@ -187,17 +191,78 @@ class MPIGridRedistributor:
                       pos.stride, int(bool(periodic)), _lib.ptr(dest), tile_rows, _lib.ptr(ws),
                       _lib.stream_handle())
             pos.finish()
-            if return_positions:  # redist.py:164: the wrapped positions, full rows
+            if want_pos:  # redist.py:164: the wrapped positions, full rows
                 fields[1] = Rows(position, self._dev)
 
         row_bytes_hint = [rows.row_bytes]
-        if return_positions:
-            row_bytes_hint.append(int(position.shape[1]) * (4 if pos.code == _lib.MGR_F32 else 8))
+        if want_pos:
+            row_bytes_hint.append(self._pos_row_bytes(position, pos))
         outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=row_bytes_hint)
-        res = rows.wrap(outs[0], m)
+        if not halo:
+            res = rows.wrap(outs[0], m)
+            if return_positions:
+                return res, fields[1].wrap(outs[1], m)
+            return res
+        rbd, rbp = rows.row_bytes, fields[1].row_bytes
+        ov_d, ov_p, mo = exchange_overload(self, self.comm, outs[0][: m * rbd], rbd,
+                                           outs[1][: m * rbp], int(position.shape[1]), pos.code,
+                                           m, list(overload_lengths), periodic=True)
+        res = rows.wrap(torch.cat([outs[0][: m * rbd], ov_d]), m + mo)  # redist.py:166
         if return_positions:
-            return res, fields[1].wrap(outs[1], m)
+            return res, fields[1].wrap(torch.cat([outs[1][: m * rbp], ov_p]), m + mo)
         return res
+
+    def exchange_overload_by_position(self, data, position, overload_lengths,
+                                      return_positions=False, periodic=True):
+        """redist.py:202-309: the overload (halo) rows of this rank's cell
+        from its neighbours; ``data``/``position`` are this rank's local rows
+        (already redistributed).  ``return_positions`` (ignored by the
+        reference) returns (data, positions)."""
+        self._check_halo(overload_lengths)
+        rows = Rows(data, self._dev)
+        prow = Rows(position, self._dev)
+        if not (isinstance(position, (np.ndarray, torch.Tensor)) and position.ndim == 2
+                and position.shape[1] >= self.dim):
+            raise ValueError(f"position must be (N, >= {self.dim})")
+        if position.dtype in (np.float32, torch.float32):
+            code = _lib.MGR_F32
+        elif position.dtype in (np.float64, torch.float64):
+            code = _lib.MGR_F64
+        else:
+            raise TypeError(f"position dtype {position.dtype} not supported (float32/float64)")
+        if prow.n != rows.n:
+            raise ValueError(f"data has {rows.n} rows, position has {prow.n}")
+        ov_d, ov_p, mo = exchange_overload(self, self.comm, rows.flat, rows.row_bytes, prow.flat,
+                                           int(position.shape[1]), code, rows.n,
+                                           list(overload_lengths), periodic=bool(periodic))
+        res = rows.wrap(ov_d, mo)
+        return (res, prow.wrap(ov_p, mo)) if return_positions else res
+
+    def get_cell_number_from_indexes_host(self, indexes, periodic=True):
+        """redist.py:73-85 on the host (neighbour ranks of the halo exchange)."""
+        indexes = np.asarray(indexes, dtype=np.int64)
+        cell = np.zeros(len(indexes), dtype=np.int64)
+        for d in range(self.dim):
+            k = indexes[:, d]
+            if periodic:
+                n = self.grid_topology[d]
+                k = ((k % n) + n) % n
+            cell += self.cell_index_offset[d] * k
+        return cell
+
+    def _check_halo(self, overload_lengths):
+        assert len(overload_lengths) == self.dim, \
+            "Overload lengths must be the same length as the dimensions"  # redist.py:245
+        if int(np.prod(self.grid_topology)) != self.size:
+            # ranks without a cell have no neighbours: the reference's isend/irecv
+            # pattern leaves them waiting forever (DESIGN.md §Divergences)
+            raise NotImplementedError("overload exchange needs one rank per grid cell "
+                                      f"({int(np.prod(self.grid_topology))} cells, "
+                                      f"{self.size} ranks)")
+
+    @staticmethod
+    def _pos_row_bytes(position, pos):
+        return int(position.shape[1]) * (4 if pos.code == _lib.MGR_F32 else 8)
 
     def redistribute_by_cell_number(self, data, rank_to_send):
         """redist.py:169-200: send row i to rank ``rank_to_send[i]``; ids
@@ -245,12 +310,6 @@ class MPIGridRedistributor:
     def unstack_position(self, position):
         """Intended behaviour of redist.py:314-318 (which is broken): columns."""
         return [position[:, d] for d in range(self.dim)]
-
-    def exchange_overload_by_position(self, data, position, overload_lengths,
-                                      return_positions=False, periodic=True):
-        """redist.py:202-309 -- SURVEY §8(f) row f1, not built in this round."""
-        raise NotImplementedError("halo/overload exchange (redist.py:202-309) is not "
-                                  "implemented yet")
 
     @staticmethod
     def _check_host_alias(data, position):

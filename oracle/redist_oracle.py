@@ -177,6 +177,91 @@ def redistribute_by_cell_number_all_ranks(size, data_list, ids_list):
     return alltoall_concat([stable_split(d, i, size) for d, i in zip(data_list, ids_list)])
 
 
+# ------------------------------------------------------- overload / halo
+def _send_rows(field_local, pos_local, field_ov, pos_ov, d, thr, right, keep):
+    """One side of ``exchange_overload_by_position``'s selection
+    (redist.py:271-287): rows of the local field and of the overload buffer
+    whose coordinate d is > thr (right) or < thr (left), local first."""
+    if not keep:  # _prepare_data_to_send(..., False) (redist.py:320-326)
+        return field_local[:0]
+    if right:
+        a, b = field_local[pos_local[:, d] > thr], field_ov[pos_ov[:, d] > thr]
+    else:
+        a, b = field_local[pos_local[:, d] < thr], field_ov[pos_ov[:, d] < thr]
+    return np.concatenate([a, b], axis=0)
+
+
+def exchange_overload_all_ranks(grid_topology, box_length, size, data_list, pos_list,
+                                overload_lengths, periodic=True):
+    """``exchange_overload_by_position`` (redist.py:202-309) executed for every
+    rank at once.  Per dimension d, for the data and then the position field
+    (:264): rank r sends the rows beyond its right threshold to its right
+    neighbour a and receives from its left neighbour b (:289-295), then sends
+    the rows below its left threshold to b and receives from a (:298-303);
+    the overload buffer grows as concat(buffer, from_a, from_b) (:305-306).
+    Kept quirks: no periodic shift of positions; with periodic=False the
+    left send uses the RIGHT neighbour's flag (:287); the selection of the
+    buffer uses the positions received in earlier dimensions only.
+    Returns the per-rank overload data (not the positions, :309)."""
+    geos = [Geometry(grid_topology, box_length, size, r) for r in range(size)]
+    dim = geos[0].dim
+    assert len(overload_lengths) == dim
+    ov = [[data_list[r][:0], np.zeros((0, dim), dtype=pos_list[r].dtype)] for r in range(size)]
+    for d in range(dim):
+        nb = []
+        for r in range(size):
+            g = geos[r]
+            ea = np.zeros(dim, dtype=np.int64)
+            ea[d] = 1
+            ia, ib = g.rank_cell_index + ea, g.rank_cell_index - ea
+            a = cell_number_from_indexes(g, np.array([ia]))[0]
+            b = cell_number_from_indexes(g, np.array([ib]))[0]
+            if periodic:
+                keep_a = keep_b = True
+            else:
+                keep_a = cell_number_from_indexes(g, np.array([ia]), periodic=False)[0] == a
+                keep_b = keep_a  # redist.py:287 passes the right neighbour's flag
+            nb.append((int(a), int(b), keep_a, keep_b))
+        for fi, fields in ((0, data_list), (1, pos_list)):
+            to_a, to_b = [], []
+            for r in range(size):
+                g = geos[r]
+                hi = g.rank_cell_limits[d, 1] - overload_lengths[d]
+                lo = g.rank_cell_limits[d, 0] + overload_lengths[d]
+                _, _, keep_a, keep_b = nb[r]
+                to_a.append(_send_rows(fields[r], pos_list[r], ov[r][fi], ov[r][1], d, hi, True,
+                                       keep_a))
+                to_b.append(_send_rows(fields[r], pos_list[r], ov[r][fi], ov[r][1], d, lo, False,
+                                       keep_b))
+            new = []
+            for r in range(size):
+                a, b = nb[r][0], nb[r][1]
+                # my left neighbour b sent its to_a to me (its right neighbour)
+                from_b = to_a[b]
+                from_a = to_b[a]
+                new.append(np.concatenate([ov[r][fi], from_a, from_b]))
+            for r in range(size):
+                ov[r][fi] = new[r]
+    return [ov[r][0] for r in range(size)]
+
+
+def redistribute_by_position_overload_all_ranks(grid_topology, box_length, size, data_list,
+                                                pos_list, overload_lengths):
+    """``redistribute_by_position`` with ``overload_lengths`` (redist.py:157-166):
+    redistribute data and positions with the same destinations, exchange the
+    overload (periodic=True: the flag is not forwarded from :165), and return
+    concat(local, overload) per rank."""
+    dest = []
+    for r in range(size):
+        geo = Geometry(grid_topology, box_length, size, r)
+        dest.append(cell_number_from_position(geo, pos_list[r], periodic=True))
+    local = redistribute_by_cell_number_all_ranks(size, data_list, dest)
+    local_pos = redistribute_by_cell_number_all_ranks(size, pos_list, dest)
+    ovd = exchange_overload_all_ranks(grid_topology, box_length, size, local, local_pos,
+                                      overload_lengths)
+    return [np.concatenate((local[r], ovd[r]), axis=0) for r in range(size)]
+
+
 # --------------------------------------------------------- synthetic inputs
 _M64 = (1 << 64) - 1
 

@@ -3,9 +3,14 @@
 ``alltoall`` follows mpi4py's lowercase semantics (redist.py:199): each rank
 passes a list indexed by destination and gets back a list indexed by source.
 Ranks are threads; a shared barrier separates deposit and collection.
+``isend``/``irecv`` (the halo exchange, redist.py:289-303) are per
+(source, destination, tag) FIFO queues: messages between one pair with one
+tag are received in the order they were sent (MPI non-overtaking); a send
+completes at once (eager, like mpi4py's pickled small messages).
 """
 from __future__ import annotations
 
+import queue
 import threading
 
 import numpy as np
@@ -16,6 +21,20 @@ class FakeWorld:
         self.size = size
         self.barrier = threading.Barrier(size)
         self.slots = [None] * size
+        self.lock = threading.Lock()
+        self.queues = {}
+
+    def q(self, src, dst, tag):
+        with self.lock:
+            return self.queues.setdefault((src, dst, tag), queue.Queue())
+
+
+class _Req:
+    def __init__(self, fn):
+        self.fn = fn
+
+    def wait(self):
+        return self.fn()
 
 
 class FakeComm:
@@ -36,6 +55,14 @@ class FakeComm:
         out = [w.slots[s][self.rank] for s in range(w.size)]
         w.barrier.wait()
         return out
+
+    def isend(self, obj, dest, tag=0):
+        self.world.q(self.rank, int(dest), tag).put(np.array(obj, copy=True))  # pickle == copy
+        return _Req(lambda: None)
+
+    def irecv(self, buf=None, source=0, tag=0):
+        q = self.world.q(int(source), self.rank, tag)
+        return _Req(lambda: q.get(timeout=120))
 
 
 def run_ranks(size, fn):

@@ -2,7 +2,7 @@
 """Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
 
 Run in the survey container only (needs /root/reference, never on the GPU
-box):   python tests/golden/make_golden.py
+box):   python tests/golden/make_golden.py [all|redist|halo]
 
 How the reference is run (SURVEY.md §8c recipe; nothing is copied):
   * stub ``mpi4py`` / ``mpi4py.MPI`` modules are placed in ``sys.modules``
@@ -256,12 +256,107 @@ def make_redistribute(ref, rng):
     return n_files + 1
 
 
+HALO_CASES = [
+    # name, topology, box, dim, pos dtype, payload kind, overload_lengths
+    ("p8_f64_rec32", [2, 2, 2], [1.0, 1.0, 1.0], 3, np.float64, "rec32", [0.1, 0.1, 0.1]),
+    ("p4_2d_mat", [4, 1], [4.0, 1.0], 2, np.float64, "mat3", [0.3, 0.2]),
+    ("p2_f32_rec36", [2, 1, 1], [1.0, 1.0, 1.0], 3, np.float32, "rec36", [0.05, 0.1, 0.2]),
+    ("p27_333_ids", [3, 3, 3], [0.3, 62.5, 7.0], 3, np.float64, "ids", [0.05, 10.0, 3.0]),
+    ("p8_wide", [2, 2, 2], [1.0, 1.0, 1.0], 3, np.float64, "rec32", [0.6, 0.3, 0.55]),
+    ("p1_self", [1, 1, 1], [1.0, 1.0, 1.0], 3, np.float64, "rec32", [0.2, 0.1, 0.3]),
+    ("p6_321_i32", [3, 2, 1], [3.0, 2.0, 1.5], 3, np.float32, "mat_i32", [0.2, 0.4, 0.1]),
+]
+
+
+def make_halo(ref, rng):
+    """redistribute_by_position(..., overload_lengths=ol) (redist.py:161-166,
+    :202-309, periodic); plus direct exchange_overload_by_position calls with
+    periodic=False (the :287 flag quirk)."""
+    n_files = 0
+    for name, topo, box, dim, pdt, kind, ol in HALO_CASES:
+        size = int(np.prod(topo))
+        n_per = rng.integers(40, 300, size)
+        pos_in, data_in = [], []
+        gid = 0
+        for r in range(size):
+            p = positions(rng, int(n_per[r]), dim, box, dtype=pdt)
+            if kind == "rec32":
+                d = rec32(p.astype(np.float64), gid)
+            elif kind == "rec36":
+                d = rec36(p, rng, gid)
+            elif kind == "mat3":
+                d = rng.normal(size=(len(p), 3))
+            elif kind == "ids":
+                d = np.arange(gid, gid + len(p), dtype=np.int64)
+            elif kind == "mat_i32":
+                d = rng.integers(-1000, 1000, (len(p), 5)).astype(np.int32)
+            gid += len(p)
+            pos_in.append(p)
+            data_in.append(d)
+        pos_work = [p.copy() for p in pos_in]
+
+        def fn(comm, r):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            with np.errstate(all="ignore"):
+                return R.redistribute_by_position(data_in[r], pos_work[r], overload_lengths=ol)
+
+        res = run_ranks(size, fn)
+        f = {"topology": np.asarray(topo, dtype=np.int64), "box": np.asarray(box),
+             "size": np.int64(size), "overload": np.asarray(ol, dtype=np.float64)}
+        for r in range(size):
+            f[f"r{r}_pos_in"] = pos_in[r]
+            f[f"r{r}_pos_out"] = pos_work[r]
+            f[f"r{r}_data"] = data_in[r]
+            f[f"r{r}_out"] = res[r]
+        np.savez_compressed(os.path.join(OUT_DIR, f"halo_{name}.npz"), **f)
+        n_files += 1
+
+    # direct calls, periodic=False: neighbours across the box edge get nothing,
+    # and the left send uses the right neighbour's flag (redist.py:287)
+    for name, topo, box, ol in [("p6_321_nonperiodic", [3, 2, 1], [3.0, 2.0, 1.5], [0.4, 0.3, 0.2]),
+                                ("p8_nonperiodic", [2, 2, 2], [1.0, 1.0, 1.0], [0.2, 0.2, 0.2])]:
+        size = int(np.prod(topo))
+        pos_l, data_l = [], []
+
+        def fn0(comm, r):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            return R.rank_cell_limits.copy()
+
+        lims = run_ranks(size, fn0)
+        for r in range(size):
+            n = int(rng.integers(30, 200))
+            lo, hi = lims[r][:, 0], lims[r][:, 1]
+            p = lo + rng.random((n, len(topo))) * (hi - lo)
+            pos_l.append(p)
+            data_l.append(rng.normal(size=(n, 2)))
+
+        def fn1(comm, r):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            return R.exchange_overload_by_position(data_l[r], pos_l[r], ol, periodic=False)
+
+        res = run_ranks(size, fn1)
+        f = {"topology": np.asarray(topo, dtype=np.int64), "box": np.asarray(box),
+             "size": np.int64(size), "overload": np.asarray(ol, dtype=np.float64)}
+        for r in range(size):
+            f[f"r{r}_pos"] = pos_l[r]
+            f[f"r{r}_data"] = data_l[r]
+            f[f"r{r}_out"] = res[r]
+        np.savez_compressed(os.path.join(OUT_DIR, f"halo_direct_{name}.npz"), **f)
+        n_files += 1
+    return n_files
+
+
 def main():
     ref = load_reference()
-    rng = np.random.default_rng(20261015)
-    a = make_bin_edges(ref, rng)
-    b = make_redistribute(ref, rng)
-    print(f"bin_edges arrays: {a}; redistribute fixtures: {b}")
+    only = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if only in ("all", "redist"):
+        rng = np.random.default_rng(20261015)
+        a = make_bin_edges(ref, rng)
+        b = make_redistribute(ref, rng)
+        print(f"bin_edges arrays: {a}; redistribute fixtures: {b}")
+    if only in ("all", "halo"):
+        c = make_halo(ref, np.random.default_rng(20261016))
+        print(f"halo fixtures: {c}")
 
 
 if __name__ == "__main__":

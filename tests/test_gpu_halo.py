@@ -1,0 +1,122 @@
+"""GPU parity of the overload (halo) exchange (redist.py:161-166, :202-309):
+HIP selection kernels (mgr_halo_flags, mgr_select_count, mgr_scan,
+mgr_pack) + the transport's sendrecv, bit-exact against the reference's own
+outputs (tests/golden/halo_*.npz) and the NumPy oracle on larger inputs."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import redist_oracle as ro
+from tests import golden_io as G
+from tests.fake_mpi import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+mgr = pytest.importorskip("mpi_grid_redistribute_amd")
+from mpi_grid_redistribute_amd import MPIGridRedistributor  # noqa: E402
+
+CASES = ["halo_p8_f64_rec32.npz", "halo_p4_2d_mat.npz", "halo_p2_f32_rec36.npz",
+         "halo_p27_333_ids.npz", "halo_p8_wide.npz", "halo_p1_self.npz", "halo_p6_321_i32.npz"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+@pytest.mark.parametrize("as_torch", [False, True])
+@pytest.mark.parametrize("case", CASES)
+def test_halo_golden(case, as_torch):
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, ol = f["topology"], f["box"], list(f["overload"])
+    data = [d.copy() for d in G.per_rank(f, "data", size)]
+    pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
+    if as_torch:
+        data = [torch.from_numpy(d.view(np.uint8).reshape(len(d), -1) if d.dtype.names else d)
+                .cuda() for d in data]
+        pos = [torch.from_numpy(p).cuda() for p in pos]
+
+    def fn(comm, r):
+        out = MPIGridRedistributor(comm if size > 1 else None, topo, box).redistribute_by_position(
+            data[r], pos[r], overload_lengths=ol)
+        torch.cuda.synchronize()
+        return out
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        exp = f[f"r{r}_out"]
+        if as_torch:
+            got = outs[r].cpu().numpy()
+            assert got.tobytes() == np.ascontiguousarray(exp).tobytes(), (case, r)
+            assert G.same_bytes(pos[r].cpu().numpy(), f[f"r{r}_pos_out"]), (case, r)
+        else:
+            assert G.same_bytes(outs[r], exp), (case, r)
+            assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), (case, r)
+
+
+@pytest.mark.parametrize("case", ["halo_direct_p6_321_nonperiodic.npz",
+                                  "halo_direct_p8_nonperiodic.npz"])
+def test_halo_direct_nonperiodic_golden(case):
+    """exchange_overload_by_position(periodic=False): the :287 flag quirk."""
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, ol = f["topology"], f["box"], list(f["overload"])
+
+    def fn(comm, r):
+        return MPIGridRedistributor(comm, topo, box).exchange_overload_by_position(
+            f[f"r{r}_data"], f[f"r{r}_pos"], ol, periodic=False)
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
+
+
+def test_halo_large_vs_oracle_with_positions():
+    """8 ranks x ~60k particles, 32-byte records, f64 positions; also checks
+    return_positions (local + overload positions, same selections)."""
+    rng = np.random.default_rng(31)
+    size, topo, box, ol = 8, [2, 2, 2], [1.0, 1.0, 1.0], [0.07, 0.12, 0.05]
+    pos = [rng.uniform(-0.1, 1.1, (int(rng.integers(40_000, 80_000)), 3)) for _ in range(size)]
+    data = []
+    for r, p in enumerate(pos):
+        rec = np.zeros(len(p), dtype=[("x", "f8"), ("y", "f8"), ("z", "f8"), ("id", "i8")])
+        rec["id"] = np.arange(len(p)) + 1_000_000 * r
+        data.append(rec)
+    pos_o = [p.copy() for p in pos]
+    exp = ro.redistribute_by_position_overload_all_ranks(topo, box, size, data, pos_o, ol)
+
+    def fn(comm, r):
+        return MPIGridRedistributor(comm, topo, box).redistribute_by_position(
+            data[r], pos[r], overload_lengths=ol, return_positions=True)
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        got, gpos = outs[r]
+        assert G.same_bytes(got, exp[r]), r
+        assert G.same_bytes(pos[r], pos_o[r]), r
+        assert len(gpos) == len(got)
+        # the positions travel with the rows: local rows' positions equal the
+        # wrapped coordinates (records hold the unwrapped input here, so check
+        # the id -> position map against the wrapped inputs)
+        src_rank = got["id"] // 1_000_000
+        src_idx = got["id"] % 1_000_000
+        want = np.stack([pos_o[s][i] for s, i in zip(src_rank, src_idx)]) if len(got) else gpos
+        assert G.same_bytes(gpos, want), r
+
+
+def test_halo_rccl_single_rank():
+    """RcclComm at world size 1: neighbours are the rank itself (mgr_sendrecv
+    self copy), periodic self-images without a shift."""
+    from mpi_grid_redistribute_amd import RcclComm
+    f = G.load("halo_p1_self.npz")
+    comm = RcclComm(RcclComm.unique_id(), 1, 0)
+    try:
+        pos = f["r0_pos_in"].copy()
+        out = MPIGridRedistributor(comm, f["topology"], f["box"]).redistribute_by_position(
+            f["r0_data"], pos, overload_lengths=list(f["overload"]))
+        assert G.same_bytes(out, f["r0_out"])
+        assert G.same_bytes(pos, f["r0_pos_out"])
+    finally:
+        comm.close()

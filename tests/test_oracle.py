@@ -3,6 +3,8 @@
 The fixtures were produced by running /root/reference/redist.py itself
 (tests/golden/make_golden.py); these tests run anywhere (no reference, no GPU).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -140,3 +142,29 @@ def test_partition_matches_masks():
     assert G.same_bytes(out, ref)
     out2, off2 = ro.stable_partition(data, dest, 8)
     assert G.same_bytes(out2, ref) and np.array_equal(off, off2)
+
+
+# ------------------------------------------------- overload / halo (f1)
+def _halo_cases():
+    import glob
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(G.GOLDEN, "halo_*.npz")))
+
+
+@pytest.mark.parametrize("case", _halo_cases())
+def test_oracle_halo_matches_reference(case):
+    """exchange_overload_by_position (redist.py:202-309) restated for all
+    ranks at once, against the reference's own outputs."""
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, ol = f["topology"], f["box"], list(f["overload"])
+    data = G.per_rank(f, "data", size)
+    if case.startswith("halo_direct_"):
+        exp = ro.exchange_overload_all_ranks(topo, box, size, data, G.per_rank(f, "pos", size), ol,
+                                             periodic=False)
+    else:
+        pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
+        exp = ro.redistribute_by_position_overload_all_ranks(topo, box, size, data, pos, ol)
+        for r in range(size):
+            assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), (case, r)
+    for r in range(size):
+        assert G.same_bytes(exp[r], f[f"r{r}_out"]), (case, r)
