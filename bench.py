@@ -41,8 +41,8 @@ SEED = 20261015
 N_CFG2 = 1 << 26                 # config 2: 64M on one GPU
 N_CFG3_PER_GPU = 1_000_000_000 // 8  # config 3: 1B over 8 GPUs
 
-# Algorithmic bytes per particle (DESIGN.md §Roofline), 24-byte f64 positions,
-# 32-byte records, 1-byte destinations:
+# Algorithmic bytes per particle (DESIGN.md §3), 24-byte f64 positions,
+# 32-byte records, 1-byte destinations.
 BYTES_PER_PARTICLE = {
     "bin_count": 24 + 24 + 1,    # read pos, write wrapped pos, write dest
     "pack": 1 + 32 + 32,         # read dest, read record, write record
@@ -59,31 +59,29 @@ def topology_for(n):
     return dims
 
 
-def cpu_baseline(seconds_budget=10.0):
-    """NumPy restatement of the reference path (oracle/, 1 core): in-place
-    wrap + bin, one mask pass per destination, concatenate (redist.py:157-199),
-    on 2x2x2 destinations, timed on a bounded sample."""
-    from oracle import redist_oracle as ro
+def cpu_baseline():
+    """The reference algorithm on this host's cores (oracle/, the checker): the
+    NumPy restatement of redistribute_by_position (redist.py:157-199: in-place
+    wrap + bin, one mask pass per destination, pickled all-to-all,
+    concatenate) run as 8 spawned rank processes on a 2x2x2 grid -- the
+    `mpirun -n 8` shape of BASELINE config 1 (mpi4py/mpirun are absent on the
+    box; pipes carry the pickled all-to-all).  Bounded sample: 8 x 2M
+    particles, best of 3 iterations (slowest rank each)."""
+    from oracle import mp_baseline
 
-    n = 1 << 22
-    pos = ro.synth_uniform(SEED, 0, n, 3, 1.0)
-    rec = np.zeros(n, dtype=[("x", "f8"), ("y", "f8"), ("z", "f8"), ("id", "i8")])
-    rec["x"], rec["y"], rec["z"] = pos.T
-    rec["id"] = np.arange(n)
-    geo = ro.Geometry([2, 2, 2], [1.0, 1.0, 1.0], 8, 0)
-    done, t0 = 0, time.perf_counter()
-    while True:
-        cell = ro.cell_number_from_position(geo, pos)
-        parts = ro.stable_split(rec, cell, 8)
-        np.concatenate(parts)
-        done += n
-        el = time.perf_counter() - t0
-        if el > seconds_budget or done >= 8 * n:
-            break
-    return {"value": done / el, "unit": "particles/s", "cores": 1, "kind": "port",
-            "sample": f"{done // n} x {n} uniform particles, 2x2x2 destinations, f64 (N,3) "
-                      f"positions + 32-byte records, numpy {np.__version__} single thread, "
-                      f"{el:.1f} s"}
+    avail = len(os.sched_getaffinity(0))
+    ranks = 8 if avail >= 8 else max(1, avail)
+    topo = {8: (2, 2, 2), 4: (2, 2, 1), 2: (2, 1, 1)}.get(ranks, (1, 1, 1))
+    n = 1 << 21
+    t0 = time.perf_counter()
+    r = mp_baseline.run(size=int(np.prod(topo)), n_per_rank=n, iters=3, topo=topo)
+    el = time.perf_counter() - t0
+    return {"value": r["value"], "unit": "particles/s", "cores": r["ranks"], "kind": "port",
+            "sample": f"{r['ranks']} rank processes x {n} uniform particles, grid {list(topo)}, "
+                      f"f64 (N,3) positions + 32-byte records, numpy {np.__version__} "
+                      f"restatement of redist.py:157-199 with a pickled all-to-all over pipes "
+                      f"(mpirun/mpi4py absent), best of 3 iterations "
+                      f"{[round(x, 3) for x in r['seconds']]} s, {el:.1f} s wall"}
 
 
 def load_traffic(kernel, workload):
@@ -114,6 +112,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    # CPU baseline first: its rank processes are spawned before this process
+    # touches the GPU
+    cpu = cpu_baseline() if (world == 1 and not args.no_cpu_baseline) else None
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -139,6 +140,14 @@ def main():
 
         def step():
             R.redistribute_by_position(rec, pos)
+
+    # Fresh input needs the in-place wrap written back (redist.py:68: x + L
+    # rounds, so most in-box coordinates change on the first call).  The bin
+    # kernel skips slabs whose bits did not change, which after the first
+    # step is every slab of these re-used inputs; that would time a
+    # repeat-call steady state, so every timed step writes back as on fresh
+    # input.
+    _lib.tune("bin_skip_clean", 0)
 
     def barrier():
         if dist is not None:
@@ -190,9 +199,6 @@ def main():
     total = n * world * args.steps
     value = total / elapsed
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline()
         line = {
             "metric": "particles redistributed/sec (whole node)",
             "value": value, "unit": "particles/s", "n_gpus": world, "steps": args.steps,

@@ -202,9 +202,11 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
                       double* pos, void* rec32, void* stream);
 
 /* -------------------------------------------------------------- tuning --
- * Kernel-variant knobs for A/B measurement ("bin_staged", "pack_small", "bin_nt", "pack_nt", "pack_coop",
- * "tile_rounds"); the defaults are the shipped configuration.  Process-wide,
- * not thread-safe against concurrent launches.                           */
+ * Kernel-variant knobs for A/B measurement: "bin_staged", "bin_skip_clean",
+ * "bin_depth", "bin_waves", "xcd_bin", "pack_small", "pack_coop",
+ * "pack_sorted", "pack_nt", "pack_rpw", "xcd_pack", "tile_rounds"
+ * (mgr_internal.h Tune); the defaults are the shipped configuration.
+ * Process-wide, not thread-safe against concurrent launches.             */
 int mgr_tune(const char* key, int64_t value);
 
 /* ----------------------------------------------------------- profiling --

@@ -462,18 +462,18 @@ int mgr_tune(const char* key, int64_t value) {
     if (!key) return fail(MGR_EINVAL, "null key");
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_small")) mgr::g_tune.pack_small = (int)value;
-    else if (!strcmp(key, "bin_nt")) mgr::g_tune.bin_nt = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
     else if (!strcmp(key, "bin_skip_clean")) mgr::g_tune.bin_skip_clean = (int)value;
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
+    else if (!strcmp(key, "offsets_tmaj")) mgr::g_tune.offsets_tmaj = (int)value;
     else if (!strcmp(key, "pack_rpw")) {
         if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
         mgr::g_tune.pack_rpw = (int)value;
     } else if (!strcmp(key, "bin_depth")) {
-        if (value < 1 || value > 4) return fail(MGR_EINVAL, "bin_depth %lld", (long long)value);
+        if (value < 1 || value > 2) return fail(MGR_EINVAL, "bin_depth %lld", (long long)value);
         mgr::g_tune.bin_depth = (int)value;
     } else if (!strcmp(key, "bin_waves")) {
         if (value < 1 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);

@@ -41,6 +41,7 @@ struct Workspace {
     int64_t* offsets;    // [nbins][T] exclusive scan of counts
     int64_t* bin_starts; // [nbins + 1]
     int64_t* partials;   // [kScanMaxBlocks]
+    int64_t* offsets_t;  // [T][nbins] tile-major copy of offsets (offsets_tmaj)
     int64_t T;
 };
 int64_t num_tiles(int64_t n, int tile_rows);
@@ -84,16 +85,16 @@ struct Tune {
     int bin_staged = 1;    // stage 64-row position slabs through LDS
     int pack_small = 1;    // register-resident pack for <= 64 bins, <= 64-byte rows
     int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
-    int bin_nt = 1;        // nontemporal loads/stores of position slabs
     int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
-    int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores
+    int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores (small/coop)
     int bin_skip_clean = 1;  // write a position slab back only if a row changed
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
     int xcd_pack = 1;      // ... in the pack kernels
     int pack_sorted = 0;   // pack through an LDS image sorted by destination
+    int offsets_tmaj = 0;  // scan also writes tile-major offsets; coop pack reads them
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
-    int bin_depth = 2;     // position slabs in flight per bin wave (1..4)
-    int bin_waves = 1;     // waves per bin workgroup (1..16; a tile's rounds split over them)
+    int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
+    int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
 };
 extern Tune g_tune;
 

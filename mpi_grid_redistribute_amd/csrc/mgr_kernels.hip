@@ -364,9 +364,19 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
     for (int b = threadIdx.x; b < g.nbins; b += blockDim.x) hist[b] = 0;
     __syncthreads();
 
-    // destination byte + wave-aggregated histogram add of one round
+    // destination byte + wave-aggregated histogram add of one round.  A full
+    // round of 1-byte destinations is stored as 16 dwords (lane 4k gathers
+    // lanes 4k..4k+3): byte stores cost ~5x their bytes in HBM writes.
     auto account = [&](unsigned b, bool valid, int r0) {
-        if (valid) dest[row0 + r0 + lane] = (DestT)b;
+        if (sizeof(DestT) == 1 && rows - r0 >= 64) {
+            const unsigned v1 = __shfl_down(b, 1, 64), v2 = __shfl_down(b, 2, 64),
+                           v3 = __shfl_down(b, 3, 64);
+            if ((lane & 3) == 0)
+                *(uint32_t*)(dest + row0 + r0 + lane) =
+                    (b & 0xffu) | ((v1 & 0xffu) << 8) | ((v2 & 0xffu) << 16) | (v3 << 24);
+        } else if (valid) {
+            dest[row0 + r0 + lane] = (DestT)b;
+        }
         const unsigned long long peers = match_bin(b, valid, g.nbits);
         if (valid && rank_in(peers) == 0) atomicAdd(&hist[b], __popcll(peers));
     };
@@ -377,13 +387,14 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
         uint4 a0 = z, a1 = z, a2 = z, a3 = z, b0 = z, b1 = z, b2 = z, b3 = z;
         uint4 c0 = z, c1 = z, c2 = z, c3 = z, e0 = z, e1 = z, e2 = z, e3 = z;
         // Every lane issues every load, without branches (index clamped into
-        // the slab; a slab past the wave's rows re-reads its first one), so the
+        // the slab; a slab past the wave's rows re-reads its last one), so the
         // compiler's wait for the oldest slab is a counted vmcnt that leaves
         // the younger one in flight.  A slab's last 16-byte unit may extend
         // past its last row: an aligned 16-byte read that starts inside the
         // buffer stays inside its page, and those bytes are never stored.
+        const int last = (rows - 1) & ~63;   // start of the wave's last round
         auto load = [&](uint4& x0, uint4& x1, uint4& x2, uint4& x3, int r) {
-            const int rr = r < rows ? r : 0;
+            const int rr = r < rows ? r : last;   // past the end: the slab just read (L2)
             const int cu = (min(64, rows - rr) * rb + 15) / 16;
             const uint4* gs = (const uint4*)((const uint8_t*)pos + (row0 + rr) * rb);
             if (NU > 0) x0 = ld<NT>(gs + min(lane, cu - 1));
@@ -402,7 +413,10 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             if (NU > 1 && lane + 64 < cu) sg[lane + 64] = x1;
             if (NU > 2 && lane + 128 < cu) sg[lane + 128] = x2;
             if (NU > 3 && lane + 192 < cu) sg[lane + 192] = x3;
-            load(x0, x1, x2, x3, r0 + 64 * DEPTH);  // DEPTH slabs in flight while this one is binned
+            // DEPTH slabs in flight while this one is binned.  DEPTH 1: only
+            // a real next slab (one register set: nothing to count past);
+            // DEPTH 2: unconditional (see load)
+            if (DEPTH > 1 || r0 + 64 < rows) load(x0, x1, x2, x3, r0 + 64 * DEPTH);
             wave_sync();
             unsigned b = 0;
             bool dirty = false;
@@ -549,7 +563,8 @@ __global__ __launch_bounds__(kBlock) void scan_apply_kernel(const int32_t* __res
                                                             const int64_t* __restrict__ partials,
                                                             int64_t* __restrict__ offsets, int64_t T,
                                                             int64_t* __restrict__ bin_starts,
-                                                            int nbins) {
+                                                            int nbins,
+                                                            int64_t* __restrict__ offsets_t) {
     __shared__ long long s_w[kWaves];
     long long carry = 0;
     for (int j = threadIdx.x; j < (int)blockIdx.x; j += kBlock) carry += partials[j];
@@ -563,6 +578,7 @@ __global__ __launch_bounds__(kBlock) void scan_apply_kernel(const int32_t* __res
         const long long ex = block_excl_scan(v, &tot, s_w) + carry;
         if (i < hi) {
             offsets[i] = ex;
+            if (offsets_t) offsets_t[(i % T) * nbins + i / T] = ex;   // tile-major copy
             if (i % T == 0) bin_starts[i / T] = ex;
         }
         carry += tot;
@@ -733,12 +749,12 @@ __global__ __launch_bounds__(kBlock) void pack_small_kernel(
 // barrier) to get each bin's base inside the tile.  Unit-transposed moves:
 // lane l moves W-byte units 64k + l of the round, so each load instruction
 // reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
-template <int W, int UPR, bool NT, int RPW>
+template <int W, int UPR, bool NT, int RPW, bool NTS>
 __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int tmaj) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kMaxTileRows / 64][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -756,7 +772,8 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
     long long tbase = 0;
     if (lane < nb) {
-        tbase = offsets[(int64_t)lane * T + tile];
+        // tile-major copy (one line per tile) or the bin-major scan output
+        tbase = tmaj ? offsets[tile * nb + lane] : offsets[(int64_t)lane * T + tile];
         if (lane == redirect_bin) tbase -= bin_starts[lane];
     }
 #pragma unroll
@@ -801,7 +818,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
             const long long t = __shfl(tgt, r, 64);
             if (u < nr[q] * UPR && t >= 0) {
                 U* o = (t >> 62) ? r_u : d_u;
-                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
+                st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[q][k]);
             }
         }
     }
@@ -1014,7 +1031,8 @@ static int64_t a256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
     const int64_t T = num_tiles(n, tile_rows);
     const int64_t M = (int64_t)nbins * (T > 0 ? T : 1);
-    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) + a256(kScanMaxBlocks * 8);
+    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) + a256(kScanMaxBlocks * 8) +
+           a256(M * 8);
 }
 
 Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
@@ -1025,7 +1043,8 @@ Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
     ws.counts = (int32_t*)p;     p += a256(M * 4);
     ws.offsets = (int64_t*)p;    p += a256(M * 8);
     ws.bin_starts = (int64_t*)p; p += a256((nbins + 1) * 8);
-    ws.partials = (int64_t*)p;
+    ws.partials = (int64_t*)p;   p += a256(kScanMaxBlocks * 8);
+    ws.offsets_t = (int64_t*)p;
     return ws;
 }
 
@@ -1046,18 +1065,10 @@ static int waves_per_block(int per_wave_lds) {
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    auto pick = [](int depth, auto k1, auto k2, auto k3, auto k4) {
-        return depth >= 4 ? k4 : depth == 3 ? k3 : depth == 2 ? k2 : k1;
-    };
-    auto k = g_tune.bin_nt
-                 ? pick(g_tune.bin_depth, bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>,
-                        bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 2>,
-                        bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 3>,
-                        bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 4>)
-                 : pick(g_tune.bin_depth, bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 1>,
-                        bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 2>,
-                        bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 3>,
-                        bin_count_kernel<PosT, kP, DestT, NU, DIM, false, 4>);
+    // nontemporal slab loads/stores always (every A/B favoured them); one or
+    // two slabs in flight per wave (deeper measured no faster)
+    auto k = g_tune.bin_depth >= 2 ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 2>
+                                   : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
     int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each
@@ -1213,7 +1224,8 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     if (e != hipSuccess) return e;
     prof_begin(s, K_SCAN_APPLY);
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)G), dim3(kBlock), 0, s, ws.counts, M,
-                       chunk, ws.partials, ws.offsets, ws.T, ws.bin_starts, nbins);
+                       chunk, ws.partials, ws.offsets, ws.T, ws.bin_starts, nbins,
+                       (g_tune.offsets_tmaj && nbins <= 64) ? ws.offsets_t : nullptr);
     prof_end(s, K_SCAN_APPLY);
     e = hipGetLastError();
     if (e != hipSuccess || !bin_counts) return e;
@@ -1278,15 +1290,20 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
         // one wave per RPW 64-row rounds of the tile (<= 16 waves)
         const int rpw = tile_rows > 1024 ? 2 : 1;
         const int threads = tile_rows / rpw;
-#define MGR_PCK(NT_, RPW_)                                                                    \
-        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_>), dim3((unsigned)ws.T),       \
+        const int tmaj = g_tune.offsets_tmaj && nb <= 64;
+        const int64_t* offs = tmaj ? ws.offsets_t : ws.offsets;
+#define MGR_PCK(NT_, RPW_, NTS_)                                                              \
+        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T), \
                            dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
-                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
-        if (g_tune.pack_nt) {
-            if (rpw == 2) MGR_PCK(true, 2); else MGR_PCK(true, 1);
+                           nbits_for(nb), drop_bin, offs, ws.bin_starts, ws.T, tile_rows,       \
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, \
+                           tmaj)
+        if (g_tune.pack_nt >= 2) {
+            if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
+        } else if (g_tune.pack_nt == 1) {
+            if (rpw == 2) MGR_PCK(true, 2, false); else MGR_PCK(true, 1, false);
         } else {
-            if (rpw == 2) MGR_PCK(false, 2); else MGR_PCK(false, 1);
+            if (rpw == 2) MGR_PCK(false, 2, false); else MGR_PCK(false, 1, false);
         }
 #undef MGR_PCK
         return hipGetLastError();
