@@ -66,6 +66,16 @@ const char* mgr_version(void);
  * (redist.py:43-44 asserts prod(topology) <= size).                        */
 int mgr_plan_create(int dim, const int64_t* grid_topology, const double* box_length,
                     int box_dtype, int nbins, mgr_plan** out);
+/* Fine-cell plan (BASELINE config 5): the destination-side
+ * stable sort of a rank's particles by the fine cell they fall in, for
+ * particle-mesh deposition.  The fine cell of a position is the reference's
+ * own binning (redist.py:63-90, S1-S3) over the global grid topology*fine,
+ * reduced to the index inside the rank's cell, k_d % fine[d], and numbered
+ * row-major over fine (last axis fastest).  nbins = prod(fine) <= 4096.
+ * Use with mgr_bin_count (periodic = 0: the rows were already wrapped by the
+ * redistribution; the indexes still wrap, :90), mgr_scan and mgr_pack.     */
+int mgr_plan_create_fine(int dim, const int64_t* grid_topology, const int64_t* fine,
+                         const double* box_length, int box_dtype, mgr_plan** out);
 int mgr_plan_destroy(mgr_plan* plan);
 
 /* Rows per tile used by the histogram / pack kernels for rows of at most

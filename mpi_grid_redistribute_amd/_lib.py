@@ -30,6 +30,7 @@ SIGNATURES = {
     "mgr_last_error": (ctypes.c_char_p, []),
     "mgr_version": (ctypes.c_char_p, []),
     "mgr_plan_create": (_I, [_I, _P, _P, _I, _I, ctypes.POINTER(_P)]),
+    "mgr_plan_create_fine": (_I, [_I, _P, _P, _P, _I, ctypes.POINTER(_P)]),
     "mgr_plan_destroy": (_I, [_P]),
     "mgr_tile_rows": (_I, [_I64, _I]),
     "mgr_workspace_bytes": (_I64, [_I64, _I, _I]),

@@ -125,29 +125,15 @@ extern "C" {
 const char* mgr_last_error(void) { return g_err.c_str(); }
 const char* mgr_version(void) { return MGR_VERSION_STRING; }
 
-int mgr_plan_create(int dim, const int64_t* topo, const double* box, int box_dtype, int nbins,
-                    mgr_plan** out) {
-    if (!out || !topo || !box) return fail(MGR_EINVAL, "null argument");
-    if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d not in [1, %d]", dim, MGR_MAX_DIM);
-    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d not in [1, %d]", nbins, MGR_MAX_BINS);
+// Box geometry of a plan: L, 2L, fast-wrap and exact power-of-two division
+// flags per dimension, and the per-dimension cell counts n[d].
+static int fill_box(mgr::Geom& g, int dim, const int64_t* n, const double* box, int box_dtype) {
     if (box_dtype != MGR_F32 && box_dtype != MGR_F64 && box_dtype != MGR_I64 && box_dtype != MGR_I32)
         return fail(MGR_EINVAL, "box_dtype %d", box_dtype);
-    mgr::Geom g;
-    memset(&g, 0, sizeof g);
     g.dim = dim;
-    g.nbins = nbins;
-    g.nbits = mgr::nbits_for(nbins);
     g.compute_f32 = box_dtype == MGR_F32;
-    int64_t prod = 1;
-    for (int d = dim - 1; d >= 0; --d) {
-        if (topo[d] < 1) return fail(MGR_EINVAL, "grid_topology[%d] = %lld < 1", d, (long long)topo[d]);
-        g.off[d] = prod;
-        prod *= topo[d];
-        if (prod > nbins)
-            return fail(MGR_EINVAL, "topology needs %lld ranks, have %d (redist.py:43-44)",
-                        (long long)prod, nbins);
-    }
     for (int d = 0; d < dim; ++d) {
+        if (n[d] < 1) return fail(MGR_EINVAL, "grid_topology[%d] = %lld < 1", d, (long long)n[d]);
         const double L = box[d];
         g.L[d] = L;
         g.twoL[d] = L + L;
@@ -156,14 +142,72 @@ int mgr_plan_create(int dim, const int64_t* topo, const double* box, int box_dty
         g.Lf[d] = Lf;
         g.twoLf[d] = Lf + Lf;
         g.fastf[d] = (Lf > 0.0f) && isfinite(Lf + Lf);
-        g.n[d] = topo[d];
-        g.nd[d] = (double)topo[d];
+        g.n[d] = n[d];
+        g.nd[d] = (double)n[d];
         int e;
         g.pow2[d] = L > 0.0 && isfinite(L) && frexp(L, &e) == 0.5 && isnormal(1.0 / L);
         g.invL[d] = g.pow2[d] ? 1.0 / L : 0.0;
         g.pow2f[d] = Lf > 0.0f && isfinite(Lf) && frexpf(Lf, &e) == 0.5f && isnormal(1.0f / Lf);
         g.invLf[d] = g.pow2f[d] ? 1.0f / Lf : 0.0f;
     }
+    return MGR_OK;
+}
+
+int mgr_plan_create(int dim, const int64_t* topo, const double* box, int box_dtype, int nbins,
+                    mgr_plan** out) {
+    if (!out || !topo || !box) return fail(MGR_EINVAL, "null argument");
+    if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d not in [1, %d]", dim, MGR_MAX_DIM);
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d not in [1, %d]", nbins, MGR_MAX_BINS);
+    mgr::Geom g;
+    memset(&g, 0, sizeof g);
+    int rc = fill_box(g, dim, topo, box, box_dtype);
+    if (rc) return rc;
+    g.nbins = nbins;
+    g.nbits = mgr::nbits_for(nbins);
+    int64_t prod = 1;
+    for (int d = dim - 1; d >= 0; --d) {
+        g.off[d] = prod;
+        prod *= topo[d];
+        if (prod > nbins)
+            return fail(MGR_EINVAL, "topology needs %lld ranks, have %d (redist.py:43-44)",
+                        (long long)prod, nbins);
+    }
+    mgr_plan* p = new mgr_plan;
+    p->g = g;
+    *out = p;
+    return MGR_OK;
+}
+
+int mgr_plan_create_fine(int dim, const int64_t* topo, const int64_t* fine, const double* box,
+                         int box_dtype, mgr_plan** out) {
+    if (!out || !topo || !fine || !box) return fail(MGR_EINVAL, "null argument");
+    if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d not in [1, %d]", dim, MGR_MAX_DIM);
+    mgr::Geom g;
+    memset(&g, 0, sizeof g);
+    int64_t global[MGR_MAX_DIM];
+    int64_t nb = 1;
+    for (int d = 0; d < dim; ++d) {
+        if (topo[d] < 1 || fine[d] < 1)
+            return fail(MGR_EINVAL, "topology and fine cells must be >= 1 (dim %d)", d);
+        if (topo[d] > ((int64_t)1 << 31) || fine[d] > MGR_MAX_BINS)
+            return fail(MGR_EINVAL, "topology/fine cells too large (dim %d)", d);
+        global[d] = topo[d] * fine[d];
+        nb *= fine[d];
+        if (nb > MGR_MAX_BINS) return fail(MGR_EINVAL, "more than %d fine cells", MGR_MAX_BINS);
+    }
+    // the reference's binning over the global fine grid topology * fine ...
+    int rc = fill_box(g, dim, global, box, box_dtype);
+    if (rc) return rc;
+    // ... then the index inside the rank's cell, row-major over fine
+    g.fine = 1;
+    int64_t off = 1;
+    for (int d = dim - 1; d >= 0; --d) {
+        g.fmod[d] = fine[d];
+        g.off[d] = off;
+        off *= fine[d];
+    }
+    g.nbins = (int)nb;
+    g.nbits = mgr::nbits_for((int)nb);
     mgr_plan* p = new mgr_plan;
     p->g = g;
     *out = p;

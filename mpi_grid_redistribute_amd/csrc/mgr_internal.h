@@ -33,6 +33,8 @@ struct Geom {
     double nd[MGR_MAX_DIM];              // (double)n[d], the int64 multiplier promoted
     int64_t n[MGR_MAX_DIM];
     int64_t off[MGR_MAX_DIM];            // row-major offsets, last axis fastest (S4)
+    int fine;                            // fine-cell plan (mgr_plan_create_fine)
+    int64_t fmod[MGR_MAX_DIM];           // fine cells per rank cell and dimension
 };
 
 // Workspace carve for (n, nbins, tile_rows).

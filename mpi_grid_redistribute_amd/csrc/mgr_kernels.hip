@@ -179,6 +179,7 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
     if (raw) *raw = k;
     const long long n = g.n[d];
     if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
+    if (g.fine) k %= g.fmod[d];   // fine-cell plan: index inside the rank's cell
     return k;
 }
 

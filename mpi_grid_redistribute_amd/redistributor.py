@@ -44,15 +44,23 @@ from .halo import exchange_overload
 
 
 class _Plan:
-    """Owns one native mgr_plan (geometry + number of destinations)."""
+    """Owns one native mgr_plan (geometry + number of destinations), or with
+    ``fine`` a fine-cell plan (mgr_plan_create_fine, prod(fine) bins)."""
 
-    def __init__(self, grid_topology: np.ndarray, box_length: np.ndarray, nbins: int):
+    def __init__(self, grid_topology: np.ndarray, box_length: np.ndarray, nbins: int,
+                 fine=None):
         topo = np.ascontiguousarray(grid_topology.astype(np.int64))
         box = np.ascontiguousarray(box_length.astype(np.float64))
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
         h = ctypes.c_void_p()
-        _lib.call("mgr_plan_create", len(topo), topo.ctypes.data_as(ctypes.c_void_p),
-                  box.ctypes.data_as(ctypes.c_void_p), box_dtype_code(box_length), int(nbins),
-                  ctypes.byref(h))
+        if fine is None:
+            _lib.call("mgr_plan_create", len(topo), vp(topo), vp(box),
+                      box_dtype_code(box_length), int(nbins), ctypes.byref(h))
+        else:
+            fn = np.ascontiguousarray(np.asarray(fine).astype(np.int64))
+            _lib.call("mgr_plan_create_fine", len(topo), vp(topo), vp(fn), vp(box),
+                      box_dtype_code(box_length), ctypes.byref(h))
+            nbins = int(np.prod(fn))
         self.h = h
         self.nbins = int(nbins)
         self.dim = len(topo)
@@ -63,6 +71,36 @@ class _Plan:
                 _lib.load().mgr_plan_destroy(self.h)
         except Exception:
             pass
+
+
+def _fine_sort(plan, dim, dev, data, position, return_positions):
+    """bin (fine plan, no wrap) -> scan -> stable pack of data (and positions)."""
+    rows = Rows(data, dev)
+    pos = Positions(position, dim, dev, data_rows=rows)
+    if pos.n != rows.n:
+        raise ValueError(f"data has {rows.n} rows, position has {pos.n}")
+    n, nb = rows.n, plan.nbins
+    prow = Rows(position, dev) if return_positions else None
+    hint = max(rows.row_bytes, prow.row_bytes if prow else 1)
+    tile_rows, ws, dest = _scratch(n, nb, hint, dev)
+    s = _lib.stream_handle()
+    counts = torch.empty(nb, dtype=torch.int64, device=dev)
+    _lib.call("mgr_bin_count", plan.h, ctypes.c_void_p(pos.addr), pos.code, n, pos.stride, 0,
+              _lib.ptr(dest), tile_rows, _lib.ptr(ws), s)
+    _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+    outs = []
+    for f in [rows] + ([prow] if prow else []):
+        o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
+        _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
+                  tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
+        outs.append(f.wrap(o, n))
+    offsets = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+    offsets[1:] = torch.cumsum(counts, 0)
+    if isinstance(data, torch.Tensor):
+        offsets = offsets if data.is_cuda else offsets.cpu()
+    else:
+        offsets = offsets.cpu().numpy()
+    return tuple(outs) + (offsets,)
 
 
 def _scratch(n, nbins, max_row_bytes, dev):
@@ -109,6 +147,7 @@ class MPIGridRedistributor:
         self.rank_cell_limits = self.get_cell_limits_from_indexes(
             np.array([self.rank_cell_index]))[0]
         self._plan = _Plan(self.grid_topology, self.box_length, self.size)
+        self._fine_plans = {}
         self._dev = device()
 
     # ------------------------------------------------------ binning (L1)
@@ -237,6 +276,26 @@ class MPIGridRedistributor:
                                            list(overload_lengths), periodic=bool(periodic))
         res = rows.wrap(ov_d, mo)
         return (res, prow.wrap(ov_p, mo)) if return_positions else res
+
+    def fine_cell_sort(self, data, position, fine_cells, return_positions=False):
+        """Destination-side stable sort of this rank's rows by fine cell, for
+        particle-mesh deposition (the reference has
+        no such step).  The fine cell of a row is the reference's binning
+        (redist.py:63-90) over the global grid grid_topology * fine_cells,
+        reduced to the index inside the rank's cell (k_d % fine_cells[d]) and
+        numbered row-major.  ``position`` is read, never wrapped (the rows were
+        wrapped by the redistribution).  Returns (sorted data, offsets
+        [prod(fine_cells)+1]) -- or (data, positions, offsets) with
+        ``return_positions`` -- in the containers of the inputs."""
+        fine = np.array(fine_cells).astype(np.int64)
+        if fine.ndim != 1 or len(fine) != self.dim:
+            raise ValueError(f"fine_cells must have {self.dim} entries")
+        key = tuple(int(x) for x in fine)
+        plan = self._fine_plans.get(key)
+        if plan is None:
+            plan = self._fine_plans[key] = _Plan(self.grid_topology, self.box_length, 0,
+                                                 fine=fine)
+        return _fine_sort(plan, self.dim, self._dev, data, position, return_positions)
 
     def get_cell_number_from_indexes_host(self, indexes, periodic=True):
         """redist.py:73-85 on the host (neighbour ranks of the halo exchange)."""

@@ -262,6 +262,33 @@ def redistribute_by_position_overload_all_ranks(grid_topology, box_length, size,
     return [np.concatenate((local[r], ovd[r]), axis=0) for r in range(size)]
 
 
+# --------------------------------------------------- fine cells (f4, Cfg5)
+def fine_cell_ids(grid_topology, fine_cells, box_length, position):
+    """Fine cell of every row inside its rank's cell:
+    the reference's binning (redist.py:63-71) over the global fine grid
+    topology * fine, without a position wrap (the rows were wrapped by the
+    redistribution), the integer index wrap that get_cell_number_from_position
+    always applies (:90, S3), then k % fine per dimension, numbered row-major
+    over fine (last axis fastest)."""
+    topo = np.array(grid_topology).astype(np.int64)
+    fine = np.array(fine_cells).astype(np.int64)
+    glob = topo * fine
+    geo = Geometry(glob, box_length, int(np.prod(glob)))
+    with np.errstate(invalid="ignore"):
+        idx = cell_indexes_from_position(geo, position.copy(), periodic=False)
+    k = periodic_wrap(idx, glob) % fine
+    off = np.ones(len(fine), dtype=np.int64)
+    for j in range(len(fine) - 2, -1, -1):
+        off[j] = off[j + 1] * fine[j + 1]
+    return (k * off).sum(axis=1)
+
+
+def fine_cell_sort(data, fine_id, nfine):
+    """Stable sort of a rank's rows by fine cell: data[argsort(fine_id,
+    kind='stable')] plus the nfine+1 cell offsets."""
+    return stable_partition(data, fine_id, nfine)
+
+
 # --------------------------------------------------------- synthetic inputs
 _M64 = (1 << 64) - 1
 

@@ -2,7 +2,7 @@
 """Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
 
 Run in the survey container only (needs /root/reference, never on the GPU
-box):   python tests/golden/make_golden.py [all|redist|halo]
+box):   python tests/golden/make_golden.py [all|redist|halo|fine]
 
 How the reference is run (SURVEY.md §8c recipe; nothing is copied):
   * stub ``mpi4py`` / ``mpi4py.MPI`` modules are placed in ``sys.modules``
@@ -346,6 +346,64 @@ def make_halo(ref, rng):
     return n_files
 
 
+def _ref_fine_ids(ref, topo, fine, box, pos):
+    """Fine cell ids from the REFERENCE's binning at the global topology
+    topo*fine (get_cell_number_from_position, redist.py:87-90, periodic=False:
+    positions are already wrapped; the index wrap of :90 still applies), then
+    decomposed and reduced to the index inside the rank's cell."""
+    glob = [int(t) * int(f) for t, f in zip(topo, fine)]
+    R = ref.MPIGridRedistributor(SingleComm(int(np.prod(glob))), glob, box)
+    with np.errstate(all="ignore"):
+        cell = R.get_cell_number_from_position(pos.copy(), periodic=False)
+    fid = np.zeros(len(pos), dtype=np.int64)
+    for d in range(len(glob)):
+        k = (cell // R.cell_index_offset[d]) % glob[d]
+        fid = fid * int(fine[d]) + k % int(fine[d])
+    return fid
+
+
+def make_fine(ref, rng):
+    """SURVEY §8d Cfg5 oracle: the reference output followed by a stable
+    argsort of the fine id (the reference has no fine sort of its own)."""
+    n_files = 0
+    # Cfg5 shape: the 2x2x2 redistribution of 36-byte records (f32 positions
+    # as a view of the record), fine cells 8x8x8 inside each rank's cell
+    f = np.load(os.path.join(OUT_DIR, "redist_p8_rec36_view.npz"), allow_pickle=False)
+    size, topo, box, fine = int(f["size"]), f["topology"], f["box"], [8, 8, 8]
+    g = {"topology": np.asarray(topo), "box": np.asarray(box), "size": np.int64(size),
+         "fine": np.asarray(fine, dtype=np.int64)}
+    for r in range(size):
+        data = f[f"r{r}_out"]
+        fid = _ref_fine_ids(ref, topo, fine, box, data["pos"])
+        g[f"r{r}_data"] = data
+        g[f"r{r}_fine_id"] = fid
+        g[f"r{r}_sorted"] = data[np.argsort(fid, kind="stable")]
+    np.savez_compressed(os.path.join(OUT_DIR, "fine_p8_rec36_888.npz"), **g)
+    n_files += 1
+    # non-power-of-two fine grid, f64 positions with the rows' own ids, 3x2x1
+    size, topo, box, fine = 6, [3, 2, 1], [3.0, 2.0, 1.5], [4, 5, 6]
+
+    def fn0(comm, r):
+        return ref.MPIGridRedistributor(comm, topo, box).rank_cell_limits.copy()
+
+    lims = run_ranks(size, fn0)
+    g = {"topology": np.asarray(topo), "box": np.asarray(box), "size": np.int64(size),
+         "fine": np.asarray(fine, dtype=np.int64)}
+    for r in range(size):
+        n = int(rng.integers(500, 3000))
+        lo, hi = lims[r][:, 0], lims[r][:, 1]
+        pos = lo + rng.random((n, 3)) * (hi - lo)
+        pos[:5] = lo  # cell faces
+        fid = _ref_fine_ids(ref, topo, fine, box, pos)
+        data = np.arange(n, dtype=np.int64) + 100_000 * r
+        g[f"r{r}_pos"] = pos
+        g[f"r{r}_data"] = data
+        g[f"r{r}_fine_id"] = fid
+        g[f"r{r}_sorted"] = data[np.argsort(fid, kind="stable")]
+    np.savez_compressed(os.path.join(OUT_DIR, "fine_p6_321_456.npz"), **g)
+    return n_files + 1
+
+
 def main():
     ref = load_reference()
     only = sys.argv[1] if len(sys.argv) > 1 else "all"
@@ -357,6 +415,9 @@ def main():
     if only in ("all", "halo"):
         c = make_halo(ref, np.random.default_rng(20261016))
         print(f"halo fixtures: {c}")
+    if only in ("all", "fine"):
+        e = make_fine(ref, np.random.default_rng(20261017))
+        print(f"fine-cell fixtures: {e}")
 
 
 if __name__ == "__main__":

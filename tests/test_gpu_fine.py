@@ -1,0 +1,101 @@
+"""GPU parity of the destination-side fine-cell sort (SURVEY §8d config 5,
+§8f f4): mgr_plan_create_fine + mgr_bin_count + mgr_scan + mgr_pack, bit-exact
+against the reference's binning at topology*fine plus a stable argsort
+(tests/golden/fine_*.npz) and the C oracle at larger sizes."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import c_oracle
+from oracle import redist_oracle as ro
+from tests import golden_io as G
+from tests.fake_mpi import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+mgr = pytest.importorskip("mpi_grid_redistribute_amd")
+from mpi_grid_redistribute_amd import MPIGridRedistributor  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _redistributors(f):
+    size = int(f["size"])
+    return run_ranks(size, lambda comm, r: MPIGridRedistributor(comm, f["topology"], f["box"]))
+
+
+@pytest.mark.parametrize("as_torch", [False, True])
+def test_fine_golden_rec36_view(as_torch):
+    """Cfg5 layout: 36-byte records, positions = the f32 view of the record."""
+    f = G.load("fine_p8_rec36_888.npz")
+    Rs = _redistributors(f)
+    nfine = int(np.prod(f["fine"]))
+    for r, R in enumerate(Rs):
+        d = f[f"r{r}_data"].copy()
+        if as_torch:
+            raw = torch.from_numpy(d.view(np.uint8).reshape(len(d), 36)).cuda()
+            out, off = R.fine_cell_sort(raw, raw.view(torch.float32)[:, :3], f["fine"])
+            got = out.cpu().numpy().reshape(-1).view(d.dtype)
+            off = off.cpu().numpy()
+        else:
+            got, off = R.fine_cell_sort(d, d["pos"], f["fine"])
+        assert G.same_bytes(got, f[f"r{r}_sorted"]), r
+        assert G.same_bytes(d, f[f"r{r}_data"]), r          # input untouched
+        assert np.array_equal(np.diff(off), np.bincount(f[f"r{r}_fine_id"], minlength=nfine))
+
+
+def test_fine_golden_456_with_positions():
+    f = G.load("fine_p6_321_456.npz")
+    Rs = _redistributors(f)
+    for r, R in enumerate(Rs):
+        pos = f[f"r{r}_pos"]
+        got, gpos, off = R.fine_cell_sort(f[f"r{r}_data"], pos, f["fine"], return_positions=True)
+        assert G.same_bytes(got, f[f"r{r}_sorted"]), r
+        order = np.argsort(f[f"r{r}_fine_id"], kind="stable")
+        assert G.same_bytes(gpos, pos[order]), r
+
+
+@pytest.mark.parametrize("fine", [[8, 8, 8], [16, 16, 16], [2, 3, 4], [1, 1, 64]])
+def test_fine_large_vs_c_oracle(fine):
+    """1M rows of one rank's cell (2x2x2 grid, rank 5), 36-byte records."""
+    rng = np.random.default_rng(sum(fine))
+    topo, box = [2, 2, 2], [1.0, 1.0, 1.0]
+    R = run_ranks(8, lambda comm, r: MPIGridRedistributor(comm, topo, box) if r == 5 else None)[5]
+    n = 1_000_003
+    lo, hi = R.rank_cell_limits[:, 0], R.rank_cell_limits[:, 1]
+    dt = np.dtype([("pos", "f4", 3), ("vel", "f4", 3), ("mass", "f4"), ("id", "i8")])
+    rec = np.zeros(n, dtype=dt)
+    rec["pos"] = (lo + rng.random((n, 3)) * (hi - lo)).astype(np.float32)
+    rec["id"] = np.arange(n)
+    glob = [t * k for t, k in zip(topo, fine)]
+    pos = np.ascontiguousarray(rec["pos"])
+    _, idx = c_oracle.bin_positions(pos.copy(), glob, box, periodic=False, want_idx=True)
+    k = ro.periodic_wrap(idx, np.array(glob)) % np.array(fine)
+    fid = (k[:, 0] * fine[1] + k[:, 1]) * fine[2] + k[:, 2]
+    exp, exp_off = c_oracle.partition(rec, fid, int(np.prod(fine)))
+    t = torch.from_numpy(rec.view(np.uint8).reshape(n, 36).copy()).cuda()
+    out, off = R.fine_cell_sort(t, t.view(torch.float32)[:, :3], fine)
+    assert np.array_equal(off.cpu().numpy(), exp_off)
+    assert out.cpu().numpy().tobytes() == exp.tobytes()
+
+
+def test_fine_after_redistribution_golden():
+    """redistribute_by_position then fine_cell_sort == the Cfg5 pipeline on
+    the reference's own redistribution fixture."""
+    f = G.load("redist_p8_rec36_view.npz")
+    fine = G.load("fine_p8_rec36_888.npz")
+    size = int(f["size"])
+    data = [d.copy() for d in G.per_rank(f, "data", size)]
+
+    def fn(comm, r):
+        R = MPIGridRedistributor(comm, f["topology"], f["box"])
+        local = R.redistribute_by_position(data[r], data[r]["pos"])
+        return R.fine_cell_sort(local, local["pos"], [8, 8, 8])[0]
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], fine[f"r{r}_sorted"]), r

@@ -168,3 +168,21 @@ def test_oracle_halo_matches_reference(case):
             assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), (case, r)
     for r in range(size):
         assert G.same_bytes(exp[r], f[f"r{r}_out"]), (case, r)
+
+
+# ------------------------------------------------- fine cells (f4, Cfg5)
+@pytest.mark.parametrize("case", ["fine_p8_rec36_888.npz", "fine_p6_321_456.npz"])
+def test_oracle_fine_cells_match_reference_binning(case):
+    """Fine ids from the reference's own binning at topology*fine, and the
+    stable argsort (SURVEY §8d Cfg5 oracle)."""
+    f = G.load(case)
+    size = int(f["size"])
+    nfine = int(np.prod(f["fine"]))
+    for r in range(size):
+        d = f[f"r{r}_data"]
+        pos = np.ascontiguousarray(d["pos"]) if d.dtype.names else f[f"r{r}_pos"]
+        fid = ro.fine_cell_ids(f["topology"], f["fine"], f["box"], pos)
+        assert np.array_equal(fid, f[f"r{r}_fine_id"]), (case, r)
+        out, off = ro.fine_cell_sort(d, fid, nfine)
+        assert G.same_bytes(out, f[f"r{r}_sorted"]), (case, r)
+        assert off[-1] == len(d) and np.all(np.diff(off) == np.bincount(fid, minlength=nfine))

@@ -17,9 +17,11 @@ ITERS = int(os.environ.get("KB_ITERS", 10))
 
 
 def run(variant):
+    variant = dict(variant)
+    topo = variant.pop("topo", None) or [2, 2, 2]
     for k, v in variant.items():
         _lib.tune(k, v)
-    part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
+    part = mgr.GridPartitioner(topo, [1.0] * len(topo))
     pos, rec = mgr.synth_uniform(N)
     flat = rec.reshape(-1)
     for _ in range(3):
