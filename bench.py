@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=0, help="particles per GPU (default: config size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the N>1 path (config 3, RCCL exchange) even at one GPU")
     args = ap.parse_args()
 
     import mpi_grid_redistribute_amd as mgr
@@ -117,11 +119,12 @@ def main():
     cpu = cpu_baseline() if (world == 1 and not args.no_cpu_baseline) else None
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    multi = world > 1 or args.exchange
+    if multi:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    if world == 1:
+    if not multi:
         n = args.n or N_CFG2
         workload = "cfg2_64M_uniform_2x2x2_local_partition"
         part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
@@ -206,9 +209,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (splitmix64 uniform, generated on device)",
             "config": {"workload": workload, "particles_per_gpu": n,
-                       "grid": topology_for(world) if world > 1 else [2, 2, 2],
+                       "grid": topology_for(world) if multi else [2, 2, 2],
                        "payload_bytes": 32, "position": "(N,3) float64, wrapped in place",
-                       "parallelism": f"{world} rank(s), one GPU per grid cell" if world > 1
+                       "parallelism": f"{world} rank(s), one GPU per grid cell" if multi
                        else "1 GPU, 8 virtual subdomains"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -35,3 +35,31 @@ def synth_uniform(n, seed=20261015, gid0=0, dim=3, box=1.0, records=True, stream
               _lib.stream_handle(stream))
     torch.cuda.current_stream().synchronize()
     return pos, rec
+
+
+def synth_clustered(n, seed=20261015, gid0=0, box=1.0, n_halos=64, sigma=0.02, frac_bg=0.2,
+                    alpha=1.0, records=True):
+    """BASELINE config 4 input: 80 % of the particles in
+    ``n_halos`` Gaussian halos (sigma = 0.02 L, centres uniform in the box,
+    halo weights ~ Pareto(alpha)), 20 % uniform background; offsets may leave
+    the box (the wrap, S1/S3).  3-D; (positions (n,3) f64, 32-byte records
+    [x,y,z,id]) on the GPU.  Test/bench input only (torch RNG)."""
+    import torch
+
+    _lib.require_gpu()
+    g = torch.Generator(device="cuda").manual_seed(int(seed))
+    L = torch.as_tensor(box, dtype=torch.float64, device="cuda").expand(3)
+    centres = torch.rand((n_halos, 3), generator=g, dtype=torch.float64, device="cuda") * L
+    w = (1.0 - torch.rand(n_halos, generator=g, dtype=torch.float64, device="cuda")) ** (-1.0 / alpha)
+    halo = torch.multinomial(w / w.sum(), n, replacement=True, generator=g)
+    pos = centres[halo] + torch.randn((n, 3), generator=g, dtype=torch.float64,
+                                      device="cuda") * (sigma * L)
+    bg = torch.rand(n, generator=g, device="cuda") < frac_bg
+    pos[bg] = torch.rand((int(bg.sum()), 3), generator=g, dtype=torch.float64, device="cuda") * L
+    rec = None
+    if records:
+        rec = torch.empty((n, 4), dtype=torch.float64, device="cuda")
+        rec[:, :3] = pos
+        rec.view(torch.int64)[:, 3] = torch.arange(gid0, gid0 + n, device="cuda")
+        rec = rec.view(torch.uint8).reshape(n, 32)
+    return pos.contiguous(), rec

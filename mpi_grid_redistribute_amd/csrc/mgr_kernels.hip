@@ -1335,10 +1335,13 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // [nbins][tiles] histogram small next to the payload.
     (void)row_bytes;
     if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
-    // <= 64 bins: 512-row tiles (bin: 4 waves x 2 rounds; pack: 8 waves x
-    // 1 round; A/B against 1024: bin -3 %, pack within noise); more bins:
-    // longer tiles keep the [nbins][tiles] histogram small next to the payload.
-    if (nbins <= 64) return 512 * g_tune.pack_rpw;
+    // <= 16 bins: 512-row tiles (bin: 4 waves x 2 rounds; pack: 8 waves x
+    // 1 round; A/B against 1024 at 8 bins: bin -3 %, pack within noise);
+    // <= 64 bins: 1024 rows (64 bins: pack 0.92 vs 1.07 ms at 512: longer
+    // same-bin runs); more bins: longer tiles keep the [nbins][tiles]
+    // histogram small next to the payload.
+    if (nbins <= 16) return 512 * g_tune.pack_rpw;
+    if (nbins <= 64) return 1024 * g_tune.pack_rpw;
     int r = 16;
     while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;

@@ -19,10 +19,11 @@ ITERS = int(os.environ.get("KB_ITERS", 10))
 def run(variant):
     variant = dict(variant)
     topo = variant.pop("topo", None) or [2, 2, 2]
+    clustered = variant.pop("input", "uniform") == "clustered"
     for k, v in variant.items():
         _lib.tune(k, v)
     part = mgr.GridPartitioner(topo, [1.0] * len(topo))
-    pos, rec = mgr.synth_uniform(N)
+    pos, rec = mgr.synth_clustered(N) if clustered else mgr.synth_uniform(N)
     flat = rec.reshape(-1)
     for _ in range(3):
         part.partition_device(flat, 32, pos)
