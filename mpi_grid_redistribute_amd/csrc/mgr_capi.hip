@@ -512,11 +512,6 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
-    else if (!strcmp(key, "offsets_tmaj")) mgr::g_tune.offsets_tmaj = (int)value;
-    else if (!strcmp(key, "pack_pipe")) {
-        if (value < 0 || value > 8) return fail(MGR_EINVAL, "pack_pipe %lld", (long long)value);
-        mgr::g_tune.pack_pipe = (int)value;
-    }
     else if (!strcmp(key, "pack_rpw")) {
         if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
         mgr::g_tune.pack_rpw = (int)value;

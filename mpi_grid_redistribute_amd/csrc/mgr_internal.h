@@ -43,7 +43,6 @@ struct Workspace {
     int64_t* offsets;    // [nbins][T] exclusive scan of counts
     int64_t* bin_starts; // [nbins + 1]
     int64_t* partials;   // [kScanMaxBlocks]
-    int64_t* offsets_t;  // [T][nbins] tile-major copy of offsets (offsets_tmaj)
     int64_t T;
 };
 int64_t num_tiles(int64_t n, int tile_rows);
@@ -93,8 +92,6 @@ struct Tune {
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
     int xcd_pack = 1;      // ... in the pack kernels
     int pack_sorted = 0;   // pack through an LDS image sorted by destination
-    int pack_pipe = 0;     // >0: persistent pipelined pack, that many workgroups per CU
-    int offsets_tmaj = 0;  // scan also writes tile-major offsets; coop pack reads them
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)

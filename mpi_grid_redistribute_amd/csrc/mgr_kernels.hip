@@ -564,8 +564,7 @@ __global__ __launch_bounds__(kBlock) void scan_apply_kernel(const int32_t* __res
                                                             const int64_t* __restrict__ partials,
                                                             int64_t* __restrict__ offsets, int64_t T,
                                                             int64_t* __restrict__ bin_starts,
-                                                            int nbins,
-                                                            int64_t* __restrict__ offsets_t) {
+                                                            int nbins) {
     __shared__ long long s_w[kWaves];
     long long carry = 0;
     for (int j = threadIdx.x; j < (int)blockIdx.x; j += kBlock) carry += partials[j];
@@ -579,7 +578,6 @@ __global__ __launch_bounds__(kBlock) void scan_apply_kernel(const int32_t* __res
         const long long ex = block_excl_scan(v, &tot, s_w) + carry;
         if (i < hi) {
             offsets[i] = ex;
-            if (offsets_t) offsets_t[(i % T) * nbins + i / T] = ex;   // tile-major copy
             if (i % T == 0) bin_starts[i / T] = ex;
         }
         carry += tot;
@@ -755,7 +753,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int tmaj) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kMaxTileRows / 64][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -773,8 +771,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
     long long tbase = 0;
     if (lane < nb) {
-        // tile-major copy (one line per tile) or the bin-major scan output
-        tbase = tmaj ? offsets[tile * nb + lane] : offsets[(int64_t)lane * T + tile];
+        tbase = offsets[(int64_t)lane * T + tile];
         if (lane == redirect_bin) tbase -= bin_starts[lane];
     }
 #pragma unroll
@@ -822,99 +819,6 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
                 st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[q][k]);
             }
         }
-    }
-}
-
-// Persistent, software-pipelined form of pack_coop_kernel: a grid of G
-// resident workgroups, workgroup b packing tiles b, b+G, b+2G, ... (XCD-
-// contiguous order), with the NEXT tile's destinations, offsets and rows
-// loaded into a second register set while the current tile is ranked and
-// stored.  The barrier between the per-round count exchange and its use is
-// a raw s_barrier behind an LDS wait only (a __syncthreads would also drain
-// the prefetch: cdna_hip_programming.md "Pipelining across barriers"); the
-// count table is double-buffered so one barrier per tile suffices.
-template <int W, int UPR>
-__global__ __launch_bounds__(1024) void pack_pipe_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
-    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
-    using U = typename Unit<W>::T;
-    static_assert(UPR <= 4, "register sets hold up to 4 units per lane");
-    __shared__ int s_cnt[2][16][64];
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t G = gridDim.x;
-    U* __restrict__ d_u = (U*)dst;
-    U* __restrict__ r_u = (U*)redirect_dst;
-
-    auto tile_of = [&](int64_t i) { return xcd ? xcd_tile(i, T) : i; };
-    // loads of tile t (clamped: a t past the end re-reads the current tile)
-    auto load = [&](int64_t t, unsigned& b, long long& tb, U* v) {
-        const int64_t row0 = t * (int64_t)tile_rows + 64 * w;
-        const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
-        b = lane < nr ? (unsigned)dest[row0 + lane] : 0u;
-        tb = 0;
-        if (lane < nb) {
-            tb = offsets[(int64_t)lane * T + t];
-            if (lane == redirect_bin) tb -= bin_starts[lane];
-        }
-        const U* __restrict__ sp = (const U*)src + row0 * UPR;
-#pragma unroll
-        for (int k = 0; k < UPR; ++k)
-            if (64 * k + lane < nr * UPR) v[k] = sp[64 * k + lane];
-    };
-    auto process = [&](int64_t t, unsigned b, long long tbase, const U* v, int buf) {
-        const int64_t row0 = t * (int64_t)tile_rows + 64 * w;
-        const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
-        const bool valid = lane < nr;
-        unsigned long long peers = __ballot(valid);
-        unsigned long long mine = peers;
-        for (int i = 0; i < nbits; ++i) {
-            const unsigned long long m = __ballot((b >> i) & 1u);
-            peers &= ((b >> i) & 1u) ? m : ~m;
-            mine &= ((lane >> i) & 1) ? m : ~m;
-        }
-        if (!valid) peers = 0;
-        s_cnt[buf][w][lane] = __popcll(mine);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        for (int j = 0; j < w; ++j) tbase += s_cnt[buf][j][lane];
-        const long long base = __shfl(tbase, (int)b, 64);
-        long long tgt = -1;
-        if (valid && (int)b != drop_bin)
-            tgt = (base + rank_in(peers)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
-#pragma unroll
-        for (int k = 0; k < UPR; ++k) {
-            const int u = 64 * k + lane;
-            const int r = u / UPR, part = u - r * UPR;
-            const long long tt = __shfl(tgt, r, 64);
-            if (u < nr * UPR && tt >= 0) {
-                U* o = (tt >> 62) ? r_u : d_u;
-                o[(tt & ((1ll << 62) - 1)) * UPR + part] = v[k];
-            }
-        }
-    };
-
-    int64_t i = blockIdx.x;
-    if (i >= T) return;
-    unsigned ba, bb;
-    long long ta, tb;
-    U va[UPR], vb[UPR];
-    load(tile_of(i), ba, ta, va);
-    int buf = 0;
-    // two tiles per trip, one register set each: the loads of one set stay
-    // in flight while the other is stored
-    for (;;) {
-        const int64_t ia = i, ib = i + G;
-        load(tile_of(ib < T ? ib : ia), bb, tb, vb);
-        process(tile_of(ia), ba, ta, va, buf);
-        buf ^= 1;
-        if (ib >= T) break;
-        const int64_t ic = ib + G;
-        load(tile_of(ic < T ? ic : ib), ba, ta, va);
-        process(tile_of(ib), bb, tb, vb, buf);
-        buf ^= 1;
-        if (ic >= T) break;
-        i = ic;
     }
 }
 
@@ -1125,8 +1029,7 @@ static int64_t a256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
     const int64_t T = num_tiles(n, tile_rows);
     const int64_t M = (int64_t)nbins * (T > 0 ? T : 1);
-    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) + a256(kScanMaxBlocks * 8) +
-           a256(M * 8);
+    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) + a256(kScanMaxBlocks * 8);
 }
 
 Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
@@ -1137,8 +1040,7 @@ Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
     ws.counts = (int32_t*)p;     p += a256(M * 4);
     ws.offsets = (int64_t*)p;    p += a256(M * 8);
     ws.bin_starts = (int64_t*)p; p += a256((nbins + 1) * 8);
-    ws.partials = (int64_t*)p;   p += a256(kScanMaxBlocks * 8);
-    ws.offsets_t = (int64_t*)p;
+    ws.partials = (int64_t*)p;
     return ws;
 }
 
@@ -1318,8 +1220,7 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     if (e != hipSuccess) return e;
     prof_begin(s, K_SCAN_APPLY);
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)G), dim3(kBlock), 0, s, ws.counts, M,
-                       chunk, ws.partials, ws.offsets, ws.T, ws.bin_starts, nbins,
-                       (g_tune.offsets_tmaj && nbins <= 64) ? ws.offsets_t : nullptr);
+                       chunk, ws.partials, ws.offsets, ws.T, ws.bin_starts, nbins);
     prof_end(s, K_SCAN_APPLY);
     e = hipGetLastError();
     if (e != hipSuccess || !bin_counts) return e;
@@ -1368,16 +1269,6 @@ template <int W, int UPR>
 static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                                int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                                void* redirect_dst, hipStream_t s) {
-    if constexpr (UPR <= 4) if (g_tune.pack_pipe && tile_rows <= 1024) {
-        // resident grid: pack_pipe workgroups per CU (256 CUs), multiple of 8
-        int64_t G = (int64_t)256 * g_tune.pack_pipe;
-        if (G > ws.T) G = ws.T;
-        hipLaunchKernelGGL((pack_pipe_kernel<W, UPR>), dim3((unsigned)G), dim3(tile_rows), 0, s,
-                           (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,
-                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack);
-        return hipGetLastError();
-    }
     if (g_tune.pack_sorted && tile_rows <= 1024) {
         const int threads = tile_rows;   // one wave per 64-row round of the tile
         const int lds = tile_rows * UPR * W + (tile_rows / 64) * 64 * 4 + tile_rows;
@@ -1397,14 +1288,11 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
         // one wave per RPW 64-row rounds of the tile (<= 16 waves)
         const int rpw = tile_rows > 1024 ? 2 : 1;
         const int threads = tile_rows / rpw;
-        const int tmaj = g_tune.offsets_tmaj && nb <= 64;
-        const int64_t* offs = tmaj ? ws.offsets_t : ws.offsets;
 #define MGR_PCK(NT_, RPW_, NTS_)                                                              \
         hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T), \
                            dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
-                           nbits_for(nb), drop_bin, offs, ws.bin_starts, ws.T, tile_rows,       \
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, \
-                           tmaj)
+                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
         if (g_tune.pack_nt >= 2) {
             if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
         } else if (g_tune.pack_nt == 1) {

@@ -19,7 +19,7 @@ mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
 DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
-            "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "offsets_tmaj": 0, "pack_pipe": 0}
+            "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1}
 VARIANTS = [
     {"pack_sorted": 1},
     {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
@@ -36,13 +36,11 @@ VARIANTS = [
     {"bin_depth": 2, "bin_waves": 2},
     {"bin_depth": 1, "bin_waves": 4},
     {"pack_rpw": 2},
-    {"offsets_tmaj": 1},
-    {"offsets_tmaj": 1, "pack_nt": 2, "pack_rpw": 2},
     {"pack_nt": 2},
-    {"pack_pipe": 1},
-    {"pack_pipe": 2, "xcd_pack": 0},
-    {"pack_pipe": 1, "tile_rounds": 8},
     {"pack_rpw": 2, "pack_nt": 1, "bin_depth": 1},
+    {"pack_coop": 0},
+    {"pack_coop": 0, "pack_nt": 2},
+    {"pack_small": 0},
 ]
 
 
