@@ -20,18 +20,26 @@ def run(variant):
     variant = dict(variant)
     topo = variant.pop("topo", None) or [2, 2, 2]
     clustered = variant.pop("input", "uniform") == "clustered"
+    rb = variant.pop("rec", 32)
     for k, v in variant.items():
         _lib.tune(k, v)
     part = mgr.GridPartitioner(topo, [1.0] * len(topo))
-    pos, rec = mgr.synth_clustered(N) if clustered else mgr.synth_uniform(N)
+    if rb == 36:   # config 5 record: f32 pos x3, vel x3, mass, i64 id; position = its view
+        rec = torch.zeros((N, 36), dtype=torch.uint8, device="cuda")
+        f = rec.view(torch.float32)
+        f[:, :3] = torch.rand((N, 3), device="cuda")
+        rec.view(torch.int32)[:, 7] = torch.arange(N, device="cuda", dtype=torch.int32)
+        pos = f[:, :3]
+    else:
+        pos, rec = mgr.synth_clustered(N) if clustered else mgr.synth_uniform(N)
     flat = rec.reshape(-1)
     for _ in range(3):
-        part.partition_device(flat, 32, pos)
+        part.partition_device(flat, rb, pos)
     torch.cuda.synchronize()
     _lib.profile_reset()
     _lib.profile_enable(True)
     for _ in range(ITERS):
-        part.partition_device(flat, 32, pos)
+        part.partition_device(flat, rb, pos)
     torch.cuda.synchronize()
     _lib.profile_enable(False)
     out = {}
@@ -39,7 +47,7 @@ def run(variant):
         ms, cnt = _lib.profile_read(k)
         out[k] = round(ms / max(cnt, 1), 4)
     out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
-    out["pack_GBps"] = round(65 * N / (out["pack"] / 1e3) / 1e9, 1)
+    out["pack_GBps"] = round((2 * rb + 1) * N / (out["pack"] / 1e3) / 1e9, 1)
     for k, v in {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0,
                  "pack_nt": 0, "pack_coop": 1, "pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0,
                  "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1}.items():
