@@ -512,6 +512,7 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
+    else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
     else if (!strcmp(key, "pack_rpw")) {
         if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
         mgr::g_tune.pack_rpw = (int)value;

@@ -92,6 +92,7 @@ struct Tune {
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
     int xcd_pack = 1;      // ... in the pack kernels
     int pack_sorted = 0;   // pack through an LDS image sorted by destination
+    int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)

@@ -822,6 +822,89 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
 }
 
+// Many-destination pack (65..1024 bins, e.g. the 512 fine cells of config
+// 5) in the cooperative shape: one workgroup of 16 waves per tile of R = 16*RPW
+// rounds, wave w ranking and moving rounds w*RPW.. with unit-transposed
+// coalesced loads and stores.  The per-(round, bin) counts go to an LDS table
+// (uint16 [R][nbins], written by each peer group's leader lane), one pass
+// turns every bin column into an exclusive prefix over the rounds, and a
+// row's slot = the tile's segment start of its bin (staged once per tile in
+// LDS) + its round's prefix + its ballot rank.
+template <int W, int UPR, typename DestT, int RPW>
+__global__ __launch_bounds__(1024) void pack_many_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const DestT* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    using U = typename Unit<W>::T;
+    constexpr int R = 16 * RPW;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    long long* s_off = (long long*)smem;                       // [nb]
+    uint16_t* tab = (uint16_t*)(smem + align16(nb * 8));       // [R][nb]
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
+    for (int i = threadIdx.x; i < R * nb; i += blockDim.x) tab[i] = 0;
+    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {
+        long long o = offsets[(int64_t)bb * T + tile];
+        if (bb == redirect_bin) o -= bin_starts[bb];
+        s_off[bb] = o;
+    }
+    int nr[RPW];
+    unsigned b[RPW];
+    U v[RPW][UPR];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
+        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+#pragma unroll
+        for (int k = 0; k < UPR; ++k)
+            if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
+    }
+    __syncthreads();   // table zeroed, tile offsets staged
+    unsigned long long peers[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const bool valid = lane < nr[q];
+        peers[q] = match_bin(b[q], valid, nbits);
+        if (valid && rank_in(peers[q]) == 0)
+            tab[(w * RPW + q) * nb + b[q]] = (uint16_t)__popcll(peers[q]);
+    }
+    __syncthreads();
+    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {   // exclusive prefix per bin
+        int run = 0;
+        for (int r = 0; r < R; ++r) {
+            const int c = tab[r * nb + bb];
+            tab[r * nb + bb] = (uint16_t)run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        long long tgt = -1;
+        if (lane < nr[q] && (int)b[q] != drop_bin)
+            tgt = (s_off[b[q]] + tab[(w * RPW + q) * nb + b[q]] + rank_in(peers[q])) |
+                  ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane;
+            const int r = u / UPR, part = u - r * UPR;
+            const long long t = __shfl(tgt, r, 64);
+            if (u < nr[q] * UPR && t >= 0) {
+                U* o = (t >> 62) ? r_u : d_u;
+                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
+            }
+        }
+    }
+}
+
 // Destination-sorted pack for <= 64 bins and rows of <= 64 bytes.  As
 // pack_coop_kernel, one workgroup per tile and wave w ranks round w; but the
 // rows are first written into an LDS image of the tile SORTED by destination
@@ -1231,10 +1314,11 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     return hipGetLastError();
 }
 
+// pack_many_kernel tiles: 64 rounds (4096 rows) up to 512 bins, 32 rounds up
+// to 1024 bins -- the uint16 [rounds][nbins] LDS table stays <= 64 KiB.
+static int many_tile_rows(int nbins) { return nbins <= 512 ? 4096 : 2048; }
+
 int pack_tile_rows(int64_t row_bytes, int nbins) {
-    // 1024-row wave tiles (16 rounds); more rounds for many bins keep the
-    // [nbins][tiles] histogram small next to the payload.
-    (void)row_bytes;
     if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
     // <= 16 bins: 512-row tiles (bin: 4 waves x 2 rounds; pack: 8 waves x
     // 1 round; A/B against 1024 at 8 bins: bin -3 %, pack within noise);
@@ -1243,6 +1327,7 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // histogram small next to the payload.
     if (nbins <= 16) return 512 * g_tune.pack_rpw;
     if (nbins <= 64) return 1024 * g_tune.pack_rpw;
+    if (g_tune.pack_many && nbins <= 1024 && row_bytes <= 64) return many_tile_rows(nbins);
     int r = 16;
     while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
@@ -1345,10 +1430,64 @@ static hipError_t pack_small_t(const void* src, int64_t row_bytes, int64_t n, co
     return hipErrorNotSupported;
 }
 
+template <int W, int UPR, typename DestT>
+static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                              int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
+                              void* redirect_dst, hipStream_t s) {
+    const int lds = align16(nb * 8) + (tile_rows / 64) * nb * 2;
+#define MGR_PMK(RPW_)                                                                          \
+    {                                                                                          \
+        auto k = pack_many_kernel<W, UPR, DestT, RPW_>;                                        \
+        ensure_lds(k, lds);                                                                    \
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,                \
+                           (const uint8_t*)src, n, (const DestT*)dest, nb, nbits_for(nb),      \
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, \
+                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack);             \
+    }
+    if (tile_rows == 4096) MGR_PMK(4)
+    else MGR_PMK(2)
+#undef MGR_PMK
+    return hipGetLastError();
+}
+
+template <int W, typename DestT>
+static hipError_t pack_many_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                              int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                              int redirect_bin, void* redirect_dst, hipStream_t s) {
+#define MGR_PM(U_) case U_: return pack_many_u<W, U_, DestT>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    switch ((int)(row_bytes / W)) {
+        MGR_PM(1) MGR_PM(2) MGR_PM(3) MGR_PM(4)
+        default: break;
+    }
+    if (W <= 8) {
+        switch ((int)(row_bytes / W)) {
+            MGR_PM(5) MGR_PM(6) MGR_PM(7) MGR_PM(8)
+            default: break;
+        }
+    }
+    if (W == 4) {
+        switch ((int)(row_bytes / W)) {
+            MGR_PM(9) MGR_PM(10) MGR_PM(11) MGR_PM(12) MGR_PM(13) MGR_PM(14) MGR_PM(15) MGR_PM(16)
+            default: break;
+        }
+    }
+#undef MGR_PM
+    return hipErrorNotSupported;
+}
+
 template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                          int redirect_bin, void* redirect_dst, hipStream_t s) {
+    if constexpr (W >= 4) {
+        if (g_tune.pack_many && nb > 64 && nb <= 1024 && row_bytes <= 64 &&
+            tile_rows == many_tile_rows(nb)) {
+            const hipError_t e = dest_bytes(nb) == 1
+                ? pack_many_t<W, uint8_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
+                : pack_many_t<W, uint16_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+            if (e != hipErrorNotSupported) return e;
+        }
+    }
     if (g_tune.pack_small && nb <= 64 && row_bytes <= 64 && W >= 4) {
         const hipError_t e = pack_small_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
                                              ws, dst, redirect_bin, redirect_dst, s);

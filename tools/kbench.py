@@ -50,7 +50,7 @@ def run(variant):
     out["pack_GBps"] = round((2 * rb + 1) * N / (out["pack"] / 1e3) / 1e9, 1)
     for k, v in {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0,
                  "pack_nt": 0, "pack_coop": 1, "pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0,
-                 "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1}.items():
+                 "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1, "pack_many": 1}.items():
         _lib.tune(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
