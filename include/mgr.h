@@ -214,7 +214,9 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
 /* -------------------------------------------------------------- tuning --
  * Kernel-variant knobs for A/B measurement: "bin_staged", "bin_skip_clean",
  * "bin_depth", "bin_waves", "xcd_bin", "pack_small", "pack_coop",
- * "pack_sorted", "pack_nt", "pack_rpw", "xcd_pack", "tile_rounds"
+ * "pack_sorted", "pack_nt", "pack_rpw", "xcd_pack", "tile_rounds",
+ * "scan_onepass", "scan_chunk", and "prof_mask" (bit k: time profiler kernel id k, in the
+ * order of the names listed under profiling below; default all)
  * (mgr_internal.h Tune); the defaults are the shipped configuration.
  * Process-wide, not thread-safe against concurrent launches.             */
 int mgr_tune(const char* key, int64_t value);
@@ -223,12 +225,14 @@ int mgr_tune(const char* key, int64_t value);
  * Per-kernel HIP-event timing of every launch made while enabled, on the
  * launch's own stream.  mgr_profile_read synchronises those events and
  * returns the accumulated device time (ms) and launch count of the named
- * kernel ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack",
+ * kernel ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack",
  * "cell_ids", "bin_ids", "cellnum_idx", "synth", "halo") or of the RCCL
  * grouped row exchange ("exchange").                                               */
 int mgr_profile_enable(int on);
 int mgr_profile_reset(void);
 int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);
+/* Profiler id of a kernel name (its bit in the "prof_mask" knob), < 0 if unknown. */
+int mgr_profile_kernel_id(const char* kernel);
 
 #ifdef __cplusplus
 }

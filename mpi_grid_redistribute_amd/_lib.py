@@ -60,6 +60,7 @@ SIGNATURES = {
     "mgr_profile_enable": (_I, [_I]),
     "mgr_profile_reset": (_I, []),
     "mgr_profile_read": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _PI64]),
+    "mgr_profile_kernel_id": (_I, [ctypes.c_char_p]),
 }
 
 
@@ -122,8 +123,28 @@ def tune(key, value):
 
 
 # --------------------------------------------------------------- profiler
+# Profiler kernel names (mgr_internal.h KernelId).
+PROFILE_KERNELS = ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack",
+                   "cell_ids", "bin_ids", "cellnum_idx", "synth", "exchange", "halo")
+
+
 def profile_enable(on=True):
     call("mgr_profile_enable", int(bool(on)))
+
+
+def profile_select(kernels=None):
+    """Time only these kernels (None: all).  Every timed launch adds two HIP
+    event records to its stream, so a benchmark times just what it reports."""
+    if kernels is None:
+        tune("prof_mask", -1)
+        return
+    mask = 0
+    for k in kernels:
+        kid = load().mgr_profile_kernel_id(k.encode())
+        if kid < 0:
+            check(kid, "mgr_profile_kernel_id")
+        mask |= 1 << kid
+    tune("prof_mask", mask)
 
 
 def profile_reset():

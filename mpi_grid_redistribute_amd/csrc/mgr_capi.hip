@@ -93,22 +93,24 @@ void collect_locked() {
 }  // namespace
 
 const char* kernel_name(int k) {
-    static const char* names[K_NUM_KERNELS] = {"bin_count", "scan_reduce", "scan_apply",
+    static const char* names[K_NUM_KERNELS] = {"bin_count", "scan", "scan_reduce", "scan_apply",
                                                "bin_totals", "pack", "cell_ids",
                                                "bin_ids", "cellnum_idx", "synth",
                                                "exchange", "halo"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 
-void prof_begin(hipStream_t s, int) {
-    if (!g_prof_on) return;
+static bool prof_selected(int k) { return g_prof_on && ((g_tune.prof_mask >> k) & 1); }
+
+void prof_begin(hipStream_t s, int k) {
+    if (!prof_selected(k)) return;
     std::lock_guard<std::mutex> lk(g_prof_mu);
     t_open = take_event();
     if (t_open) (void)hipEventRecord(t_open, s);
 }
 
 void prof_end(hipStream_t s, int k) {
-    if (!g_prof_on || !t_open) return;
+    if (!prof_selected(k) || !t_open) return;
     std::lock_guard<std::mutex> lk(g_prof_mu);
     hipEvent_t b = take_event();
     if (!b) return;
@@ -513,6 +515,12 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
     else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
+    else if (!strcmp(key, "scan_onepass")) mgr::g_tune.scan_onepass = (int)value;
+    else if (!strcmp(key, "scan_chunk")) {
+        if (value < 256 || value > (1 << 20)) return fail(MGR_EINVAL, "scan_chunk %lld", (long long)value);
+        mgr::g_tune.scan_chunk = (int)value;
+    }
+    else if (!strcmp(key, "prof_mask")) mgr::g_tune.prof_mask = value;
     else if (!strcmp(key, "pack_rpw")) {
         if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
         mgr::g_tune.pack_rpw = (int)value;
@@ -547,6 +555,13 @@ int mgr_profile_reset(void) {
         mgr::g_cnt[k] = 0;
     }
     return MGR_OK;
+}
+
+int mgr_profile_kernel_id(const char* kernel) {
+    if (!kernel) return fail(MGR_EINVAL, "null kernel name");
+    for (int k = 0; k < mgr::K_NUM_KERNELS; ++k)
+        if (strcmp(kernel, mgr::kernel_name(k)) == 0) return k;
+    return fail(MGR_EINVAL, "unknown kernel '%s'", kernel);
 }
 
 int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches) {

@@ -1,0 +1,367 @@
+// Device-side building blocks shared by the kernel translation units
+// (mgr_bin.hip, mgr_pack.hip, mgr_kernels.hip): IEEE/x86-exact scalar math
+// of the reference's wrap and binning, wave primitives, one-pass scan words,
+// streaming load/store policies, XCD-aware tile order; plus launch helpers.
+#pragma once
+
+#include "mgr_internal.h"
+
+#include <limits.h>
+
+#include <type_traits>
+
+namespace mgr {
+
+// ------------------------------------------------------------ scalar math
+__device__ __forceinline__ long long trunc_i64(double v) {
+    // numpy astype(int64) on x86 (cvttsd2si): NaN / out of range -> INT64_MIN (S10).
+    // |v| < 2^31 (every in-box particle): one v_cvt_i32_f64.
+    if (v > -2147483648.0 && v < 2147483648.0) return (long long)(int)v;
+    return (v >= -9223372036854775808.0 && v < 9223372036854775808.0) ? (long long)v : LLONG_MIN;
+}
+
+// ---- x86/glibc NaN semantics (numpy runs on x86: SSE + glibc fmod) ----
+// An invalid operation (fmod(inf, L), fmod(x, 0), inf - inf) yields the x86
+// "default NaN" -- sign bit SET (0xFFF8... / 0xFFC00000); a NaN operand
+// propagates quieted, first operand first.  The GPU's own default NaN is
+// positive, so these cases are spelled out bit by bit.  They only occur on
+// the slow path (non-finite input or box), never for in-box particles.
+constexpr unsigned long long kDefaultNaN64 = 0xFFF8000000000000ull;
+constexpr unsigned kDefaultNaN32 = 0xFFC00000u;
+
+__device__ __forceinline__ double quiet64(double x) {
+    return __longlong_as_double(__double_as_longlong(x) | 0x0008000000000000ll);
+}
+__device__ __forceinline__ float quiet32(float x) {
+    return __uint_as_float(__float_as_uint(x) | 0x00400000u);
+}
+// cvtss2sd / cvtsd2ss on NaN: keep sign, quiet, shift the payload.
+__device__ __forceinline__ double f32_to_f64_x86(float x) {
+    if (!isnan(x)) return (double)x;
+    const unsigned u = __float_as_uint(x) | 0x00400000u;
+    const unsigned long long b = ((unsigned long long)(u >> 31) << 63) | 0x7FF0000000000000ull |
+                                 ((unsigned long long)(u & 0x007FFFFFu) << 29);
+    return __longlong_as_double((long long)b);
+}
+__device__ __forceinline__ float f64_to_f32_x86(double x) {
+    if (!isnan(x)) return (float)x;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x) | 0x0008000000000000ull;
+    const unsigned u = ((unsigned)(b >> 63) << 31) | 0x7F800000u | (unsigned)((b >> 29) & 0x007FFFFFu);
+    return __uint_as_float(u);
+}
+
+__device__ __forceinline__ double fmod_x86(double a, double b) {
+    if (isnan(a)) return quiet64(a);
+    if (isnan(b)) return quiet64(b);
+    if (isinf(a) || b == 0.0) return __longlong_as_double((long long)kDefaultNaN64);
+    if (isinf(b)) return a;
+    return fmod(a, b);  // finite / finite nonzero: exact
+}
+__device__ __forceinline__ float fmodf_x86(float a, float b) {
+    if (isnan(a)) return quiet32(a);
+    if (isnan(b)) return quiet32(b);
+    if (isinf(a) || b == 0.0f) return __uint_as_float(kDefaultNaN32);
+    if (isinf(b)) return a;
+    return fmodf(a, b);
+}
+
+// numpy npy_remainder: floor remainder, sign of the divisor.  A NaN result
+// is final: every later x86 operation propagates it unchanged.
+__device__ __forceinline__ double pymod(double a, double b) {
+    double m = fmod_x86(a, b);
+    if (b == 0.0 || isnan(m)) return m;
+    if (m != 0.0) {
+        if ((b < 0.0) != (m < 0.0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+
+__device__ __forceinline__ float pymodf(float a, float b) {
+    float m = fmodf_x86(a, b);
+    if (b == 0.0f || isnan(m)) return m;
+    if (m != 0.0f) {
+        if ((b < 0.0f) != (m < 0.0f)) m += b;
+    } else {
+        m = copysignf(0.0f, b);
+    }
+    return m;
+}
+
+// ((x % L) + L) % L.  Fast path for 0 <= x < L (every in-box particle):
+// x % L == x, y = x + L in [L, 2L], and fmod(y, L) == y - L exactly
+// (Sterbenz), 0 when y == 2L.  Bit-identical to the general path.
+// General path (outside the box, non-finite, odd boxes): out of line so its
+// registers do not weigh on the streaming fast path.
+static __device__ __attribute__((noinline)) double wrap_f64_slow(double x, double L) {
+    const double m = pymod(x, L);
+    if (isnan(m)) return m;
+    return pymod(m + L, L);
+}
+
+static __device__ __attribute__((noinline)) float wrap_f32_slow(float x, float L) {
+    const float m = pymodf(x, L);
+    if (isnan(m)) return m;
+    return pymodf(m + L, L);
+}
+
+__device__ __forceinline__ double wrap_f64(double x, double L, double twoL, int fast) {
+    if (fast && x >= 0.0 && x < L) {
+        const double y = x + L;
+        return (y == twoL) ? 0.0 : y - L;
+    }
+    return wrap_f64_slow(x, L);
+}
+
+__device__ __forceinline__ float wrap_f32(float x, float L, float twoL, int fast) {
+    if (fast && x >= 0.0f && x < L) {
+        const float y = x + L;
+        return (y == twoL) ? 0.0f : y - L;
+    }
+    return wrap_f32_slow(x, L);
+}
+
+__device__ __forceinline__ long long floormod_i64(long long a, long long n) {
+    if (n == 0 || n == -1) return 0;
+    long long r = a % n;
+    if (r != 0 && ((r < 0) != (n < 0))) r += n;
+    return r;
+}
+
+template <typename PosT>
+__device__ __forceinline__ bool same_bits(PosT a, PosT b) {
+    if constexpr (sizeof(PosT) == 8) return __double_as_longlong((double)a) == __double_as_longlong((double)b);
+    else return __float_as_uint((float)a) == __float_as_uint((float)b);
+}
+
+// One coordinate: wrap (+ write back), bin, index wrap.  Returns the wrapped
+// index; *raw gets trunc(t/L*n) before the index wrap (cell indexes API).
+// The wrapped value is stored only when its bits differ from the input
+// (the in-place mutation of redist.py:68 / :328-329 is then complete: an
+// in-box coordinate wraps to itself) and *dirty records that a store happened.
+template <typename PosT, bool kPeriodic>
+__device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw,
+                                               bool* dirty) {
+    long long k;
+    const PosT in = *p;
+    if (sizeof(PosT) == 4 && g.compute_f32) {
+        float x = (float)in;
+        if (kPeriodic) {
+            x = wrap_f32(x, g.Lf[d], g.twoLf[d], g.fastf[d]);
+            if (!same_bits((PosT)x, in)) { *p = (PosT)x; *dirty = true; }
+        }
+        const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];  // f32 / f32 -> f32
+        k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
+    } else {
+        double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)in) : (double)in;
+        if (kPeriodic) {
+            const double t = wrap_f64(x, g.L[d], g.twoL[d], g.fast[d]);
+            const PosT w = sizeof(PosT) == 4 ? (PosT)f64_to_f32_x86(t) : (PosT)t;  // round (S9)
+            if (!same_bits(w, in)) { *p = w; *dirty = true; }
+            x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)w) : (double)w;  // bin reads it (S2)
+        }
+        k = trunc_i64((g.pow2[d] ? x * g.invL[d] : x / g.L[d]) * g.nd[d]);
+    }
+    if (raw) *raw = k;
+    const long long n = g.n[d];
+    if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
+    if (g.fine) k %= g.fmod[d];   // fine-cell plan: index inside the rank's cell
+    return k;
+}
+
+// DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
+template <typename PosT, bool kPeriodic, int DIM = 0>
+__device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx,
+                                             bool* dirty) {
+    long long cell = 0;
+    if (DIM > 0) {
+#pragma unroll
+        for (int d = 0; d < DIM; ++d)
+            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr, dirty);
+    } else {
+        for (int d = 0; d < g.dim; ++d)
+            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr, dirty);
+    }
+    return cell;
+}
+
+// ------------------------------------------------------ wave primitives
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Lanes of this wave holding the same bin b (valid lanes only): nbits
+// ballots, one per bit of the bin id (gfx950 wave64 ballot + popc match).
+__device__ __forceinline__ unsigned long long match_bin(unsigned b, bool valid, int nbits) {
+    unsigned long long peers = __ballot(valid);
+    for (int i = 0; i < nbits; ++i) {
+        const bool bit = (b >> i) & 1u;
+        const unsigned long long m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return valid ? peers : 0ull;
+}
+
+__device__ __forceinline__ int rank_in(unsigned long long peers) {
+    const unsigned lo = (unsigned)peers, hi = (unsigned)(peers >> 32);
+    return __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+}
+
+// Block-wide exclusive scan of one int64 per thread (256 threads).
+__device__ __forceinline__ long long block_excl_scan(long long v, long long* total,
+                                                     long long* s_w /* [kWaves] */) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    long long x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    long long pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWaves; ++i) {
+        const long long t = s_w[i];
+        pre += (i < w) ? t : 0;
+        tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
+// ------------------------------------------------- one-pass scan words
+constexpr uint64_t kScanAgg = 1ull << 62, kScanInc = 2ull << 62, kScanVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ void clear_scan_flags(uint64_t* __restrict__ flags) {
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kScanFlags; i += step)
+        flags[i] = 0;
+}
+
+__device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Poll until the word's status reaches `need` (bounded: a lost producer
+// would yield a wrong scan, never a hung GPU).
+__device__ __forceinline__ uint64_t flag_poll(uint64_t* p, uint64_t need) {
+    uint64_t w = 0;
+    for (int spin = 0; spin < (1 << 24); ++spin) {
+        w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w >> 62) >= need) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return w;
+}
+
+// ------------------------------------------------------ wave-private tiles
+// A tile is tile_rows = 64 * R consecutive rows owned by ONE wavefront; a
+// workgroup of wpb waves runs tiles blockIdx.x * wpb + wave.  Row
+// (tile, round r, lane l) = tile * tile_rows + 64 r + l, so (round, lane)
+// order IS the original row order: a ballot rank inside a round plus a
+// running per-bin count across rounds is a stable rank.  Tiles never share
+// data, so the kernels have no workgroup barriers at all.
+__device__ __forceinline__ void wave_sync() {
+    // LDS traffic of one wave is performed in order; this only stops the
+    // compiler from moving LDS accesses across the point.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int W> struct Unit;
+template <> struct Unit<16> { using T = uint4; };
+template <> struct Unit<8> { using T = uint2; };
+template <> struct Unit<4> { using T = uint32_t; };
+template <> struct Unit<2> { using T = uint16_t; };
+template <> struct Unit<1> { using T = uint8_t; };
+
+// Copy nbytes (a multiple of 4) between 16-byte-aligned regions with one
+// wave: W-byte units, 4-byte tail.
+template <int W>
+__device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t* __restrict__ s,
+                                          int nbytes, int lane) {
+    using U = typename Unit<W>::T;
+    const int units = nbytes / W;
+    for (int u = lane; u < units; u += 64) ((U*)d)[u] = ((const U*)s)[u];
+    for (int q = units * (W / 4) + lane; q < nbytes / 4; q += 64)
+        ((uint32_t*)d)[q] = ((const uint32_t*)s)[q];
+}
+
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+// XCD-contiguous tile order.  Workgroups are dealt to the 8 XCDs round-robin
+// (blockIdx % 8 labels the XCD, MI355X_MICROARCH.md "Workgroup dispatch"), so
+// tile = blockIdx would put neighbouring tiles on different L2s.  This
+// bijection gives each XCD label one contiguous run of T/8 tiles: the cache
+// lines that two neighbouring tiles' output segments share are then written
+// through ONE L2 and leave it as whole lines.  Speed only, never correctness.
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t T) {
+    const int64_t per = T >> 3;
+    if (bid < per * 8) return (bid & 7) * per + (bid >> 3);
+    return bid;
+}
+
+// Streaming accesses: NT selects the nontemporal (nt) cache policy for data
+// that is read or written exactly once.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (!NT) {
+        return *p;
+    } else if constexpr (sizeof(T) == 16) {
+        const u32x4_t x = __builtin_nontemporal_load((const u32x4_t*)p);
+        T r;
+        __builtin_memcpy(&r, &x, 16);
+        return r;
+    } else if constexpr (sizeof(T) == 8) {
+        const u32x2_t x = __builtin_nontemporal_load((const u32x2_t*)p);
+        T r;
+        __builtin_memcpy(&r, &x, 8);
+        return r;
+    } else {
+        return __builtin_nontemporal_load(p);
+    }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T* p, const T& v) {
+    if constexpr (!NT) {
+        *p = v;
+    } else if constexpr (sizeof(T) == 16) {
+        u32x4_t x;
+        __builtin_memcpy(&x, &v, 16);
+        __builtin_nontemporal_store(x, (u32x4_t*)p);
+    } else if constexpr (sizeof(T) == 8) {
+        u32x2_t x;
+        __builtin_memcpy(&x, &v, 8);
+        __builtin_nontemporal_store(x, (u32x2_t*)p);
+    } else {
+        __builtin_nontemporal_store(v, p);
+    }
+}
+
+
+// ----------------------------------------------------------- launch helpers
+static inline int grid_for(int64_t n, int per_block_rows = kBlock) {
+    int64_t g = (n + per_block_rows - 1) / per_block_rows;
+    if (g > 256 * 16) g = 256 * 16;   // grid-stride beyond 16 blocks per CU
+    return (int)(g < 1 ? 1 : g);
+}
+
+template <typename K>
+static void ensure_lds(K kernel, int bytes) {
+    if (bytes > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+// Waves per workgroup for a per-wave LDS footprint: 4 when a 4-wave
+// workgroup stays within 64 KiB, fewer otherwise (never above 160 KiB).
+static inline int waves_per_block(int per_wave_lds) {
+    if (per_wave_lds * kWaves <= 64 * 1024) return kWaves;
+    int w = (160 * 1024) / (per_wave_lds > 0 ? per_wave_lds : 1);
+    return w < 1 ? 1 : (w > kWaves ? kWaves : w);
+}
+
+}  // namespace mgr

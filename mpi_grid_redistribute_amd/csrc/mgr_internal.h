@@ -12,7 +12,8 @@ constexpr int kBlock = 256;              // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
 constexpr int kMaxTileRows = 4096;       // 16 rounds of 256 rows; spos fits uint16
 constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
-constexpr int kScanMaxBlocks = 1024;
+constexpr int kScanMaxBlocks = 1024;      // two-pass scan (A/B knob scan_onepass = 0)
+constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups) at most
 
 // Geometry of one plan, passed to kernels by value (kernarg segment).
 struct Geom {
@@ -42,7 +43,9 @@ struct Workspace {
     int32_t* counts;     // [nbins][T] destination-major tile histogram
     int64_t* offsets;    // [nbins][T] exclusive scan of counts
     int64_t* bin_starts; // [nbins + 1]
-    int64_t* partials;   // [kScanMaxBlocks]
+    int64_t* partials;   // [kScanMaxBlocks] (two-pass scan)
+    uint64_t* flags;     // [kScanFlags] one-pass scan chunk words; zeroed by the
+                         // count producers (bin_count, bin_ids, select_count)
     int64_t T;
 };
 int64_t num_tiles(int64_t n, int tile_rows);
@@ -52,7 +55,7 @@ int dest_bytes(int nbins);
 int nbits_for(int nbins);
 
 // Kernel ids for the profiler.
-enum KernelId { K_BIN_COUNT, K_SCAN_REDUCE, K_SCAN_APPLY, K_BIN_TOTALS, K_PACK, K_CELL_IDS,
+enum KernelId { K_BIN_COUNT, K_SCAN, K_SCAN_REDUCE, K_SCAN_APPLY, K_BIN_TOTALS, K_PACK, K_CELL_IDS,
                 K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_EXCHANGE, K_HALO, K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
@@ -96,6 +99,9 @@ struct Tune {
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
+    int scan_onepass = 1;  // one-pass decoupled look-back scan (0: reduce + apply + totals)
+    int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)
+    int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)
 };
 extern Tune g_tune;
 

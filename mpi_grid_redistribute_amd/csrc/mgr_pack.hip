@@ -1,0 +1,619 @@
+// Pack kernels of the hot path (gfx950): the stable partition of every
+// payload field into the bin-major send buffer / output (redist.py:195-198,
+// send_buff[i] = data[rank_to_send == i], order kept), with their launchers
+// and tile-size policy.  Helpers: mgr_device.h.
+#include "mgr_device.h"
+
+namespace mgr {
+
+// ------------------------------------------------------------------ pack
+// Kernel 3 of the hot path.  Per round: ballot match -> rank inside the
+// wave; slot = tile segment start of the bin + running count + rank; the
+// row is copied straight to its slot.  Same-bin lanes hold consecutive
+// slots, so each store instruction writes a few contiguous runs, and the
+// runs of consecutive rounds continue each other (merged in L2).
+// kWide (rows > 256 B): the wave copies one row at a time, 64 lanes wide.
+template <int W, typename DestT, bool kWide>
+__global__ __launch_bounds__(kBlock) void pack_kernel(
+    const uint8_t* __restrict__ src, int64_t upr /* W-units per row */, int64_t n,
+    const DestT* __restrict__ dest, int nb, int nbits, int drop_bin,
+    const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts, int64_t T,
+    int tile_rows, int per_wave_lds, uint8_t* __restrict__ dst, int redirect_bin,
+    uint8_t* __restrict__ redirect_dst) {
+    using U = typename Unit<W>::T;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    if (tile >= T) return;
+    int64_t* goff = (int64_t*)(smem + w * per_wave_lds);
+    int32_t* run = (int32_t*)(smem + w * per_wave_lds + align16(nb * 8));
+    for (int b = lane; b < nb; b += 64) {
+        int64_t o = offsets[(int64_t)b * T + tile];
+        if (b == redirect_bin) o -= bin_starts[b];
+        goff[b] = o;
+        run[b] = 0;
+    }
+    wave_sync();
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    const U* __restrict__ s_u = (const U*)src;
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const bool valid = r0 + lane < rows;
+        const int64_t row = row0 + r0 + lane;
+        const unsigned b = valid ? (unsigned)dest[row] : 0u;
+        const unsigned long long peers = match_bin(b, valid, nbits);
+        const int rk = rank_in(peers);
+        int64_t slot = 0;
+        if (valid) slot = goff[b] + run[b] + rk;
+        wave_sync();
+        if (valid && rk == 0) run[b] += __popcll(peers);
+        const bool live = valid && (int)b != drop_bin;
+        if (!kWide) {
+            if (live) {
+                const U* sp = s_u + row * upr;
+                U* dp = ((int)b == redirect_bin ? r_u : d_u) + slot * upr;
+                int64_t k = 0;
+                for (; k + 4 <= upr; k += 4) {
+                    const U a0 = sp[k], a1 = sp[k + 1], a2 = sp[k + 2], a3 = sp[k + 3];
+                    dp[k] = a0; dp[k + 1] = a1; dp[k + 2] = a2; dp[k + 3] = a3;
+                }
+                for (; k < upr; ++k) dp[k] = sp[k];
+            }
+        } else {
+            const unsigned long long todo = __ballot(live);
+            for (int j = 0; j < 64; ++j) {
+                if (!((todo >> j) & 1ull)) continue;
+                const int bj = __shfl((int)b, j, 64);
+                const int64_t sj = __shfl((long long)slot, j, 64);
+                const U* sp = s_u + (row0 + r0 + j) * upr;
+                U* dp = (bj == redirect_bin ? r_u : d_u) + sj * upr;
+                for (int64_t k = lane; k < upr; k += 64) dp[k] = sp[k];
+            }
+        }
+        wave_sync();
+    }
+}
+
+// Register-resident pack for <= 64 bins and rows of <= 64 bytes (the
+// common case, e.g. 8 grid cells x 32-byte records).  Lane l keeps the next
+// free slot of bin l in a register; a row finds its slot with one
+// cross-lane read (bpermute) of its bin's lane; per-bin round counts come
+// from the same nbits ballots as the rank, so there is no LDS traffic.  The
+// next round's destinations and rows are prefetched while the current
+// round is ranked and stored.
+template <int W, int UPR, bool NT, bool NTS>
+__global__ __launch_bounds__(kBlock) void pack_small_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
+    int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst) {
+    using U = typename Unit<W>::T;
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    if (tile >= T) return;
+    long long next_slot = 0;  // lane l: next free slot of bin l
+    if (lane < nb) {
+        next_slot = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) next_slot -= bin_starts[lane];
+    }
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    // Round = 64 rows = 64*UPR units of W bytes, contiguous in src.  Lane l
+    // moves units 64k + l (k < UPR): every load instruction reads 64*W
+    // contiguous bytes.  The unit's row (compile-time division by UPR) gets
+    // its slot from the lane that ranked it.
+    const U* __restrict__ s_u = (const U*)src + row0 * UPR;
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+    unsigned nb_next = 0;
+    U nv[UPR];
+    if (lane < rows) nb_next = dest[row0 + lane];
+#pragma unroll
+    for (int k = 0; k < UPR; ++k)
+        if (64 * k + lane < rows * UPR) nv[k] = ld<NT>(s_u + 64 * k + lane);
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const int nr = min(64, rows - r0);
+        const bool valid = lane < nr;
+        const unsigned b = valid ? nb_next : 0u;
+        U v[UPR];
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) v[k] = nv[k];
+        if (r0 + 64 < rows) {  // next round in flight
+            const int nn = min(64, rows - r0 - 64);
+            if (lane < nn) nb_next = dest[row0 + r0 + 64 + lane];
+            const U* sp = s_u + (int64_t)(r0 + 64) * UPR;
+#pragma unroll
+            for (int k = 0; k < UPR; ++k)
+                if (64 * k + lane < nn * UPR) nv[k] = ld<NT>(sp + 64 * k + lane);
+        }
+        // nbits ballots: rank inside the wave + per-bin counts for lane == bin
+        unsigned long long peers = __ballot(valid);
+        unsigned long long mine = peers;  // lanes whose bin == this lane's index
+        for (int i = 0; i < nbits; ++i) {
+            const unsigned long long m = __ballot((b >> i) & 1u);
+            peers &= ((b >> i) & 1u) ? m : ~m;
+            mine &= ((lane >> i) & 1) ? m : ~m;
+        }
+        if (!valid) peers = 0;
+        const long long base = __shfl(next_slot, (int)b, 64);
+        next_slot += __popcll(mine);
+        // per-row target: slot, or -1 (dropped / past the end); bit 62 = redirect
+        long long tgt = -1;
+        if (valid && (int)b != drop_bin)
+            tgt = (base + rank_in(peers)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane;
+            const int r = u / UPR, part = u - r * UPR;
+            const long long t = __shfl(tgt, r, 64);
+            if (u < nr * UPR && t >= 0) {
+                U* o = (t >> 62) ? r_u : d_u;
+                st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[k]);
+            }
+        }
+    }
+}
+
+// Block-cooperative pack for <= 64 bins and rows of <= 64 bytes: one
+// workgroup per tile of R rounds, wave w ranks and moves round w (64 rows)
+// in one shot -- the short-lived, fully parallel shape that streams best.
+// The waves exchange their per-bin counts through a [R][64] LDS table (one
+// barrier) to get each bin's base inside the tile.  Unit-transposed moves:
+// lane l moves W-byte units 64k + l of the round, so each load instruction
+// reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
+template <int W, int UPR, bool NT, int RPW, bool NTS>
+__global__ __launch_bounds__(1024) void pack_coop_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    using U = typename Unit<W>::T;
+    __shared__ int s_cnt[kMaxTileRows / 64][64];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
+    // issue every load of the wave's rounds first
+    int nr[RPW];
+    unsigned b[RPW];
+    U v[RPW][UPR];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
+        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+    }
+    long long tbase = 0;
+    if (lane < nb) {
+        tbase = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) tbase -= bin_starts[lane];
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+#pragma unroll
+        for (int k = 0; k < UPR; ++k)
+            if (64 * k + lane < nr[q] * UPR) v[q][k] = ld<NT>(sp + 64 * k + lane);
+    }
+    // rank inside each round; lane l counts bin l
+    unsigned long long peers[RPW];
+    int cnt[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const bool valid = lane < nr[q];
+        unsigned long long pe = __ballot(valid);
+        unsigned long long mine = pe;
+        for (int i = 0; i < nbits; ++i) {
+            const unsigned long long m = __ballot((b[q] >> i) & 1u);
+            pe &= ((b[q] >> i) & 1u) ? m : ~m;
+            mine &= ((lane >> i) & 1) ? m : ~m;
+        }
+        peers[q] = valid ? pe : 0ull;
+        cnt[q] = __popcll(mine);
+        s_cnt[w * RPW + q][lane] = cnt[q];
+    }
+    __syncthreads();
+    for (int j = 0; j < w * RPW; ++j) tbase += s_cnt[j][lane];
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const long long base = __shfl(tbase, (int)b[q], 64);
+        long long tgt = -1;
+        if (lane < nr[q] && (int)b[q] != drop_bin)
+            tgt = (base + rank_in(peers[q])) | ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
+        tbase += cnt[q];
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane;
+            const int r = u / UPR, part = u - r * UPR;
+            const long long t = __shfl(tgt, r, 64);
+            if (u < nr[q] * UPR && t >= 0) {
+                U* o = (t >> 62) ? r_u : d_u;
+                st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[q][k]);
+            }
+        }
+    }
+}
+
+// Many-destination pack (65..1024 bins, e.g. the 512 fine cells of config
+// 5) in the cooperative shape: one workgroup of 16 waves per tile of R = 16*RPW
+// rounds, wave w ranking and moving rounds w*RPW.. with unit-transposed
+// coalesced loads and stores.  The per-(round, bin) counts go to an LDS table
+// (uint16 [R][nbins], written by each peer group's leader lane), one pass
+// turns every bin column into an exclusive prefix over the rounds, and a
+// row's slot = the tile's segment start of its bin (staged once per tile in
+// LDS) + its round's prefix + its ballot rank.
+template <int W, int UPR, typename DestT, int RPW>
+__global__ __launch_bounds__(1024) void pack_many_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const DestT* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    using U = typename Unit<W>::T;
+    constexpr int R = 16 * RPW;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    long long* s_off = (long long*)smem;                       // [nb]
+    uint16_t* tab = (uint16_t*)(smem + align16(nb * 8));       // [R][nb]
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
+    for (int i = threadIdx.x; i < R * nb; i += blockDim.x) tab[i] = 0;
+    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {
+        long long o = offsets[(int64_t)bb * T + tile];
+        if (bb == redirect_bin) o -= bin_starts[bb];
+        s_off[bb] = o;
+    }
+    int nr[RPW];
+    unsigned b[RPW];
+    U v[RPW][UPR];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
+        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+#pragma unroll
+        for (int k = 0; k < UPR; ++k)
+            if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
+    }
+    __syncthreads();   // table zeroed, tile offsets staged
+    unsigned long long peers[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const bool valid = lane < nr[q];
+        peers[q] = match_bin(b[q], valid, nbits);
+        if (valid && rank_in(peers[q]) == 0)
+            tab[(w * RPW + q) * nb + b[q]] = (uint16_t)__popcll(peers[q]);
+    }
+    __syncthreads();
+    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {   // exclusive prefix per bin
+        int run = 0;
+        for (int r = 0; r < R; ++r) {
+            const int c = tab[r * nb + bb];
+            tab[r * nb + bb] = (uint16_t)run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        long long tgt = -1;
+        if (lane < nr[q] && (int)b[q] != drop_bin)
+            tgt = (s_off[b[q]] + tab[(w * RPW + q) * nb + b[q]] + rank_in(peers[q])) |
+                  ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane;
+            const int r = u / UPR, part = u - r * UPR;
+            const long long t = __shfl(tgt, r, 64);
+            if (u < nr[q] * UPR && t >= 0) {
+                U* o = (t >> 62) ? r_u : d_u;
+                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
+            }
+        }
+    }
+}
+
+// Destination-sorted pack for <= 64 bins and rows of <= 64 bytes.  As
+// pack_coop_kernel, one workgroup per tile and wave w ranks round w; but the
+// rows are first written into an LDS image of the tile SORTED by destination
+// (bin, then original order), and the image is then streamed out in order:
+// each store instruction writes 64*W contiguous bytes of one or two
+// destination runs instead of ~nbins short runs.  LDS: the image
+// (tile_rows * row bytes), the [rounds][64] count table and one bin byte per
+// sorted row.
+template <int W, int UPR, bool NT>
+__global__ __launch_bounds__(1024) void pack_sorted_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    using U = typename Unit<W>::T;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int R = tile_rows >> 6;
+    U* img = (U*)smem;
+    int* s_cnt = (int*)(smem + (size_t)tile_rows * UPR * W);
+    uint8_t* s_bin = (uint8_t*)(s_cnt + R * 64);
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t trow0 = tile * (int64_t)tile_rows;
+    const int64_t row0 = trow0 + 64 * w;
+    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
+    const int trows = (int)min((int64_t)tile_rows, n - trow0);
+    const bool valid = lane < nr;
+    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
+    long long tbase = 0;
+    if (lane < nb) {
+        tbase = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) tbase -= bin_starts[lane];
+    }
+    const U* __restrict__ sp = (const U*)src + row0 * UPR;
+    U v[UPR];
+#pragma unroll
+    for (int k = 0; k < UPR; ++k)
+        if (64 * k + lane < nr * UPR) v[k] = ld<NT>(sp + 64 * k + lane);
+    unsigned long long peers = __ballot(valid);
+    unsigned long long mine = peers;
+    for (int i = 0; i < nbits; ++i) {
+        const unsigned long long m = __ballot((b >> i) & 1u);
+        peers &= ((b >> i) & 1u) ? m : ~m;
+        mine &= ((lane >> i) & 1) ? m : ~m;
+    }
+    if (!valid) peers = 0;
+    s_cnt[w * 64 + lane] = __popcll(mine);
+    __syncthreads();
+    // lane = bin: rows of this bin in earlier rounds, and in the whole tile
+    int before = 0, tot = 0;
+    for (int j = 0; j < R; ++j) {
+        const int c = s_cnt[j * 64 + lane];
+        before += (j < w) ? c : 0;
+        tot += c;
+    }
+    // exclusive scan of the per-bin tile totals over the lanes: local bin start
+    int lstart = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(lstart, o, 64);
+        if (lane >= o) lstart += y;
+    }
+    lstart -= tot;
+    const int lpos = __shfl(lstart + before, (int)b, 64) + rank_in(peers);
+#pragma unroll
+    for (int k = 0; k < UPR; ++k) {
+        const int u = 64 * k + lane;
+        const int r = u / UPR, part = u - r * UPR;
+        const int t = __shfl(lpos, r, 64);
+        if (u < nr * UPR) img[t * UPR + part] = v[k];
+    }
+    if (valid) s_bin[lpos] = (uint8_t)b;
+    __syncthreads();
+    // stream the sorted image out: wave w writes sorted units [w*64*UPR, ...)
+    const long long delta = tbase - lstart;   // lane = bin: global slot - local position
+    U* __restrict__ d_u = (U*)dst;
+    U* __restrict__ r_u = (U*)redirect_dst;
+#pragma unroll
+    for (int k = 0; k < UPR; ++k) {
+        const int u = w * 64 * UPR + 64 * k + lane;
+        const int p = u / UPR, part = u - p * UPR;
+        const int bb = p < trows ? (int)s_bin[p] : 0;
+        const long long dl = __shfl(delta, bb, 64);
+        if (p < trows && bb != drop_bin) {
+            U* o = bb == redirect_bin ? r_u : d_u;
+            o[(p + dl) * UPR + part] = img[u];
+        }
+    }
+}
+
+// ============================================================ launchers
+// pack_many_kernel tiles: 64 rounds (4096 rows) up to 512 bins, 32 rounds up
+// to 1024 bins -- the uint16 [rounds][nbins] LDS table stays <= 64 KiB.
+static int many_tile_rows(int nbins) { return nbins <= 512 ? 4096 : 2048; }
+
+int pack_tile_rows(int64_t row_bytes, int nbins) {
+    if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
+    // <= 16 bins: 512-row tiles (bin: 4 waves x 2 rounds; pack: 8 waves x
+    // 1 round; A/B against 1024 at 8 bins: bin -3 %, pack within noise);
+    // <= 64 bins: 1024 rows (64 bins: pack 0.92 vs 1.07 ms at 512: longer
+    // same-bin runs); more bins: longer tiles keep the [nbins][tiles]
+    // histogram small next to the payload.
+    if (nbins <= 16) return 512 * g_tune.pack_rpw;
+    if (nbins <= 64) return 1024 * g_tune.pack_rpw;
+    if (g_tune.pack_many && nbins <= 1024 && row_bytes <= 64) return many_tile_rows(nbins);
+    int r = 16;
+    while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
+    return 64 * r;
+}
+
+template <int W, typename DestT, bool kWide>
+static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
+                         int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                         int redirect_bin, void* redirect_dst, hipStream_t s) {
+    auto k = pack_kernel<W, DestT, kWide>;
+    const int per_wave = align16(nb * 8) + align16(nb * 4);
+    const int wpb = waves_per_block(per_wave);
+    const int lds = per_wave * wpb;
+    ensure_lds(k, lds);
+    const int64_t grid = (ws.T + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s,
+                       (const uint8_t*)src, row_bytes / W, n, (const DestT*)dest, nb,
+                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,
+                       per_wave, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
+    return hipGetLastError();
+}
+
+template <int W, int UPR>
+static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
+                               void* redirect_dst, hipStream_t s) {
+    if (g_tune.pack_sorted && tile_rows <= 1024) {
+        const int threads = tile_rows;   // one wave per 64-row round of the tile
+        const int lds = tile_rows * UPR * W + (tile_rows / 64) * 64 * 4 + tile_rows;
+#define MGR_PSS(NT_)                                                                          \
+        {                                                                                     \
+        ensure_lds(pack_sorted_kernel<W, UPR, NT_>, lds);                                      \
+        hipLaunchKernelGGL((pack_sorted_kernel<W, UPR, NT_>), dim3((unsigned)ws.T), dim3(threads), \
+                           (size_t)lds, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb,   \
+                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack); }
+        if (g_tune.pack_nt) MGR_PSS(true)
+        else MGR_PSS(false)
+#undef MGR_PSS
+        return hipGetLastError();
+    }
+    if (g_tune.pack_coop) {
+        // one wave per RPW 64-row rounds of the tile (<= 16 waves)
+        const int rpw = tile_rows > 1024 ? 2 : 1;
+        const int threads = tile_rows / rpw;
+#define MGR_PCK(NT_, RPW_, NTS_)                                                              \
+        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T), \
+                           dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
+                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
+        if (g_tune.pack_nt >= 2) {
+            if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
+        } else if (g_tune.pack_nt == 1) {
+            if (rpw == 2) MGR_PCK(true, 2, false); else MGR_PCK(true, 1, false);
+        } else {
+            if (rpw == 2) MGR_PCK(false, 2, false); else MGR_PCK(false, 1, false);
+        }
+#undef MGR_PCK
+        return hipGetLastError();
+    }
+    const int64_t grid = (ws.T + kWaves - 1) / kWaves;
+#define MGR_PSK(NT_, NTS_)                                                                  \
+    hipLaunchKernelGGL((pack_small_kernel<W, UPR, NT_, NTS_>), dim3((unsigned)grid), dim3(kBlock), \
+                       0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),    \
+                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,     \
+                       redirect_bin, (uint8_t*)redirect_dst)
+    if (g_tune.pack_nt >= 2) MGR_PSK(true, true);
+    else if (g_tune.pack_nt == 1) MGR_PSK(true, false);
+    else MGR_PSK(false, false);
+#undef MGR_PSK
+    return hipGetLastError();
+}
+
+// Compile-time units per row for rows of <= 64 bytes in 16/8/4-byte units
+// (registers, no scratch); returns hipErrorNotSupported for other shapes.
+template <int W>
+static hipError_t pack_small_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                               int nb, int drop_bin, int tile_rows, const Workspace& ws,
+                               void* dst, int redirect_bin, void* redirect_dst, hipStream_t s) {
+#define MGR_PS(U_) case U_: return pack_small_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    if (W >= 4) {
+        switch ((int)(row_bytes / W)) {
+            MGR_PS(1) MGR_PS(2) MGR_PS(3) MGR_PS(4)
+            default: break;
+        }
+        if (W <= 8) {
+            switch ((int)(row_bytes / W)) {
+                MGR_PS(5) MGR_PS(6) MGR_PS(7) MGR_PS(8)
+                default: break;
+            }
+        }
+        if (W == 4) {
+            switch ((int)(row_bytes / W)) {
+                MGR_PS(9) MGR_PS(10) MGR_PS(11) MGR_PS(12) MGR_PS(13) MGR_PS(14) MGR_PS(15) MGR_PS(16)
+                default: break;
+            }
+        }
+    }
+#undef MGR_PS
+    return hipErrorNotSupported;
+}
+
+template <int W, int UPR, typename DestT>
+static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                              int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
+                              void* redirect_dst, hipStream_t s) {
+    const int lds = align16(nb * 8) + (tile_rows / 64) * nb * 2;
+#define MGR_PMK(RPW_)                                                                          \
+    {                                                                                          \
+        auto k = pack_many_kernel<W, UPR, DestT, RPW_>;                                        \
+        ensure_lds(k, lds);                                                                    \
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,                \
+                           (const uint8_t*)src, n, (const DestT*)dest, nb, nbits_for(nb),      \
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, \
+                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack);             \
+    }
+    if (tile_rows == 4096) MGR_PMK(4)
+    else MGR_PMK(2)
+#undef MGR_PMK
+    return hipGetLastError();
+}
+
+template <int W, typename DestT>
+static hipError_t pack_many_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                              int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                              int redirect_bin, void* redirect_dst, hipStream_t s) {
+#define MGR_PM(U_) case U_: return pack_many_u<W, U_, DestT>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    switch ((int)(row_bytes / W)) {
+        MGR_PM(1) MGR_PM(2) MGR_PM(3) MGR_PM(4)
+        default: break;
+    }
+    if (W <= 8) {
+        switch ((int)(row_bytes / W)) {
+            MGR_PM(5) MGR_PM(6) MGR_PM(7) MGR_PM(8)
+            default: break;
+        }
+    }
+    if (W == 4) {
+        switch ((int)(row_bytes / W)) {
+            MGR_PM(9) MGR_PM(10) MGR_PM(11) MGR_PM(12) MGR_PM(13) MGR_PM(14) MGR_PM(15) MGR_PM(16)
+            default: break;
+        }
+    }
+#undef MGR_PM
+    return hipErrorNotSupported;
+}
+
+template <int W>
+static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
+                         int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                         int redirect_bin, void* redirect_dst, hipStream_t s) {
+    if constexpr (W >= 4) {
+        if (g_tune.pack_many && nb > 64 && nb <= 1024 && row_bytes <= 64 &&
+            tile_rows == many_tile_rows(nb)) {
+            const hipError_t e = dest_bytes(nb) == 1
+                ? pack_many_t<W, uint8_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
+                : pack_many_t<W, uint16_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+            if (e != hipErrorNotSupported) return e;
+        }
+    }
+    if (g_tune.pack_small && nb <= 64 && row_bytes <= 64 && W >= 4) {
+        const hipError_t e = pack_small_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
+                                             ws, dst, redirect_bin, redirect_dst, s);
+        if (e != hipErrorNotSupported) return e;
+    }
+    const bool wide = row_bytes > 256;
+    if (dest_bytes(nb) == 1)
+        return wide ? pack_t<W, uint8_t, true>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
+                    : pack_t<W, uint8_t, false>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    return wide ? pack_t<W, uint16_t, true>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
+                : pack_t<W, uint16_t, false>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+}
+
+hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                       int nbins, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                       int redirect_bin, void* redirect_dst, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    // Widest unit dividing the row and every base address.
+    uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
+    if (redirect_dst) a |= (uintptr_t)redirect_dst;
+    prof_begin(s, K_PACK);
+    hipError_t e;
+    if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    prof_end(s, K_PACK);
+    return e;
+}
+
+}  // namespace mgr

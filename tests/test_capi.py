@@ -69,9 +69,11 @@ def test_plan_validation(lib):
 def test_profiler_names(lib):
     from mpi_grid_redistribute_amd import _lib
     _lib.profile_reset()
-    for k in ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack", "synth"):
+    for k in _lib.PROFILE_KERNELS:   # every id the library names, in enum order
         ms, cnt = _lib.profile_read(k)
         assert cnt == 0 and ms == 0.0
+    _lib.profile_select(["bin_count", "pack"])
+    _lib.profile_select(None)
     with pytest.raises(_lib.MgrError):
         _lib.profile_read("nope")
 

@@ -19,7 +19,8 @@ mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
 DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
-            "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1}
+            "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
+            "scan_onepass": 1, "scan_chunk": 2048}
 VARIANTS = [
     {"pack_sorted": 1},
     {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
@@ -42,6 +43,12 @@ VARIANTS = [
     {"pack_coop": 0, "pack_nt": 2},
     {"pack_small": 0},
     {"pack_many": 0},
+    {"scan_onepass": 0},
+    {"scan_onepass": 0, "tile_rounds": 1},
+    {"tile_rounds": 1},
+    {"scan_chunk": 256, "tile_rounds": 1},
+    {"scan_chunk": 4096},
+    {"scan_chunk": 65536},
 ]
 
 

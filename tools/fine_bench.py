@@ -42,7 +42,7 @@ def main():
     torch.cuda.synchronize()
     _lib.profile_enable(False)
     out = {"n": N, "fine": FINE, "ms_per_sort": a.elapsed_time(b) / ITERS}
-    for k in ("bin_count", "scan_reduce", "scan_apply", "bin_totals", "pack"):
+    for k in ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack"):
         ms, cnt = _lib.profile_read(k)
         if cnt:
             out[k] = round(ms / cnt, 4)

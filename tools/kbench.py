@@ -42,15 +42,23 @@ def run(variant):
         part.partition_device(flat, rb, pos)
     torch.cuda.synchronize()
     _lib.profile_enable(False)
-    out = {}
-    for k in ("bin_count", "scan_reduce", "scan_apply", "pack"):
+    # whole step (bin + scan + pack) without profiler events
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(ITERS):
+        part.partition_device(flat, rb, pos)
+    b.record()
+    torch.cuda.synchronize()
+    out = {"step": round(a.elapsed_time(b) / ITERS, 4)}
+    for k in ("bin_count", "scan", "scan_reduce", "scan_apply", "pack"):
         ms, cnt = _lib.profile_read(k)
         out[k] = round(ms / max(cnt, 1), 4)
     out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
     out["pack_GBps"] = round((2 * rb + 1) * N / (out["pack"] / 1e3) / 1e9, 1)
     for k, v in {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0,
                  "pack_nt": 0, "pack_coop": 1, "pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0,
-                 "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1, "pack_many": 1}.items():
+                 "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1, "pack_many": 1,
+                 "scan_onepass": 1, "scan_chunk": 2048}.items():
         _lib.tune(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
@@ -75,6 +83,15 @@ def copy_ceiling():
 if __name__ == "__main__":
     vf = os.environ.get("KB_VARIANTS_FILE")
     variants = json.load(open(vf)) if vf else json.loads(os.environ.get("KB_VARIANTS", "[{}]"))
+    repeat = int(os.environ.get("KB_REPEAT", 1))
     print(json.dumps({"n": N, **copy_ceiling()}), flush=True)
-    for v in variants:
-        print(json.dumps({"variant": v, **run(v)}), flush=True)
+    results = {}
+    for _ in range(repeat):          # interleaved A/B: box drift hits every variant alike
+        for v in variants:
+            r = run(v)
+            results.setdefault(json.dumps(v, sort_keys=True), []).append(r)
+            print(json.dumps({"variant": v, **r}), flush=True)
+    if repeat > 1:
+        for key, rs in results.items():
+            med = {k: sorted(r[k] for r in rs)[len(rs) // 2] for k in rs[0]}
+            print(json.dumps({"median_of": len(rs), "variant": json.loads(key), **med}), flush=True)
