@@ -516,6 +516,7 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
     else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
     else if (!strcmp(key, "scan_onepass")) mgr::g_tune.scan_onepass = (int)value;
+    else if (!strcmp(key, "pack_img")) mgr::g_tune.pack_img = (int)value;
     else if (!strcmp(key, "scan_chunk")) {
         if (value < 256 || value > (1 << 20)) return fail(MGR_EINVAL, "scan_chunk %lld", (long long)value);
         mgr::g_tune.scan_chunk = (int)value;

@@ -99,6 +99,7 @@ struct Tune {
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
+    int pack_img = 1;      // 16-byte-unit image pack for 4-byte-multiple rows (1: 24..60 B, 2: 12..60 B)
     int scan_onepass = 1;  // one-pass decoupled look-back scan (0: reduce + apply + totals)
     int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)
     int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)

@@ -237,6 +237,128 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
 }
 
+// Image pack for rows of RB bytes, RB a multiple of 4 but not of 16 (e.g.
+// the 36-byte records of config 5), <= 64 bins: the cooperative shape of
+// pack_coop_kernel (one wave per 64-row round, per-bin bases exchanged
+// through LDS behind one barrier) but every global access is 16 bytes wide.
+// The round (64 * RB bytes, 16-byte aligned) is loaded in 16-byte units,
+// parked in wave-private LDS, each row moved to its slot of a round image
+// ordered by destination (bin-major, stable), and the image stored back in
+// 16-byte units: a unit inside one bin's run is one 16-byte store to the
+// run's (4-byte aligned) place in the output, a unit straddling two runs is
+// stored dword by dword.  Plain 4-byte units would need RB/4 load and RB/4
+// store instructions per round instead of ~RB/16.
+typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int RB>
+__global__ __launch_bounds__(1024) void pack_img_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
+    constexpr int RBYTES = 64 * RB;                 // one round, a multiple of 16
+    constexpr int NU = (RBYTES / 16 + 63) / 64;     // 16-byte units per lane
+    constexpr int DW = RB / 4;
+    constexpr int WAVE_LDS = RBYTES + 64 * 8 + 64;  // image, per-bin output address, row bins
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int nw = blockDim.x >> 6;
+    int* s_cnt = (int*)smem;                                    // [nw][64]
+    uint8_t* img = smem + nw * 64 * 4 + w * WAVE_LDS;
+    unsigned long long* gaddr = (unsigned long long*)(img + RBYTES);
+    uint8_t* ibin = img + RBYTES + 64 * 8;
+    uint32_t* imgw = (uint32_t*)img;
+    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * w;
+    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
+    const int nbytes = nr * RB;
+    const bool valid = lane < nr;
+    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
+    long long tbase = 0;
+    if (lane < nb) {
+        tbase = offsets[(int64_t)lane * T + tile];
+        if (lane == redirect_bin) tbase -= bin_starts[lane];
+    }
+    const uint8_t* __restrict__ sp = src + row0 * RB;
+    u32x4_t v[NU];
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+        const int x = 16 * (64 * k + lane);
+        if (x + 16 <= nbytes) {
+            v[k] = *(const u32x4_t*)(sp + x);
+        } else if (x < nbytes) {            // last partial unit of the array
+            const uint32_t* q = (const uint32_t*)(sp + x);
+            v[k] = u32x4_t{q[0], x + 4 < nbytes ? q[1] : 0u, x + 8 < nbytes ? q[2] : 0u,
+                           x + 12 < nbytes ? q[3] : 0u};
+        }
+    }
+    // rank inside the round; lane l counts bin l
+    unsigned long long pe = __ballot(valid), mine = pe;
+    for (int i = 0; i < nbits; ++i) {
+        const unsigned long long m = __ballot((b >> i) & 1u);
+        pe &= ((b >> i) & 1u) ? m : ~m;
+        mine &= ((lane >> i) & 1) ? m : ~m;
+    }
+    const int cnt = __popcll(mine);
+    s_cnt[w * 64 + lane] = cnt;
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+        const int x = 16 * (64 * k + lane);
+        if (x < nbytes) *(u32x4_t*)(img + x) = v[k];
+    }
+    __syncthreads();
+    for (int j = 0; j < w; ++j) tbase += s_cnt[j * 64 + lane];
+    // round image order: exclusive prefix of the round's bin counts
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const int excl = incl - cnt;
+    const int slot = __shfl(excl, (int)b, 64) + (valid ? rank_in(pe) : 0);
+    if (lane < nb) {
+        uint8_t* base = lane == redirect_bin ? redirect_dst : dst;
+        gaddr[lane] = lane == drop_bin ? 0ull
+                                       : (unsigned long long)(base + (tbase - excl) * (long long)RB);
+    }
+    uint32_t row[DW];
+    if (valid) {
+#pragma unroll
+        for (int p = 0; p < DW; ++p) row[p] = imgw[lane * DW + p];
+    }
+    wave_sync();
+    if (valid) {
+#pragma unroll
+        for (int p = 0; p < DW; ++p) imgw[slot * DW + p] = row[p];
+        ibin[slot] = (uint8_t)b;
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+        const int x = 16 * (64 * k + lane);
+        if (x < nbytes) {
+            const u32x4_t q = *(const u32x4_t*)(img + x);
+            const int bf = ibin[x / RB];
+            const int last = min(x + 15, nbytes - 1);
+            if (x + 16 <= nbytes && ibin[last / RB] == bf) {
+                const unsigned long long a = gaddr[bf];
+                if (a) *(u32x4_a4*)(a + x) = q;
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) {
+                        const unsigned long long a = gaddr[ibin[xd / RB]];
+                        if (a) *(uint32_t*)(a + xd) = q[d];
+                    }
+                }
+            }
+        }
+    }
+}
+
 // Many-destination pack (65..1024 bins, e.g. the 512 fine cells of config
 // 5) in the cooperative shape: one workgroup of 16 waves per tile of R = 16*RPW
 // rounds, wave w ranking and moving rounds w*RPW.. with unit-transposed
@@ -572,6 +694,47 @@ static hipError_t pack_many_t(const void* src, int64_t row_bytes, int64_t n, con
     return hipErrorNotSupported;
 }
 
+template <int RB>
+static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                             int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
+                             void* redirect_dst, hipStream_t s) {
+    const int nw = tile_rows / 64;
+    const int lds = nw * 64 * 4 + nw * (64 * RB + 64 * 8 + 64);
+    auto k = pack_img_kernel<RB>;
+    ensure_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s,
+                       (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
+                       ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
+                       (uint8_t*)redirect_dst, g_tune.xcd_pack);
+    return hipGetLastError();
+}
+
+// Rows of 24..60 (pack_img 2: 12..60) bytes, 4-byte multiples but not 16-byte ones: the
+// image pack (16-byte global accesses) when the source is 16-byte aligned,
+// the outputs 4-byte aligned, <= 64 bins and <= 16 waves per tile.
+static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                           int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                           int redirect_bin, void* redirect_dst, hipStream_t s) {
+    uintptr_t a = (uintptr_t)dst | (uintptr_t)row_bytes;
+    if (redirect_dst) a |= (uintptr_t)redirect_dst;
+    // pack_img 1: rows of >= 24 bytes (A/B: 36 B 0.90 vs 1.05 ms, 40 B 0.97 vs
+    // 1.00, 24 B 0.70 vs 0.71; 12 B 0.56 vs 0.48 -- the LDS passes cost more
+    // than narrow units for small rows); 2: every size it takes (tests)
+    const int64_t min_rb = g_tune.pack_img >= 2 ? 12 : 24;
+    if (!g_tune.pack_img || ((uintptr_t)src & 15) || (a & 3) || row_bytes % 16 == 0 ||
+        row_bytes < min_rb || row_bytes > 60 || nb > 64 || tile_rows > 1024 ||
+        dest_bytes(nb) != 1)
+        return hipErrorNotSupported;
+#define MGR_PI(RB_) case RB_: return pack_img_t<RB_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    switch ((int)row_bytes) {
+        MGR_PI(12) MGR_PI(20) MGR_PI(24) MGR_PI(28) MGR_PI(36) MGR_PI(40) MGR_PI(44)
+        MGR_PI(52) MGR_PI(56) MGR_PI(60)
+        default: break;
+    }
+#undef MGR_PI
+    return hipErrorNotSupported;
+}
+
 template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
@@ -606,7 +769,12 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
     uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
     prof_begin(s, K_PACK);
-    hipError_t e;
+    hipError_t e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
+                            redirect_bin, redirect_dst, s);
+    if (e != hipErrorNotSupported) {
+        prof_end(s, K_PACK);
+        return e;
+    }
     if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
     else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
     else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);

@@ -20,7 +20,7 @@ from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _li
 
 DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
             "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
-            "scan_onepass": 1, "scan_chunk": 2048}
+            "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1}
 VARIANTS = [
     {"pack_sorted": 1},
     {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
@@ -48,6 +48,9 @@ VARIANTS = [
     {"tile_rounds": 1},
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},
+    {"pack_img": 0},
+    {"pack_img": 1, "tile_rounds": 16, "pack_rpw": 2},
+    {"pack_img": 1, "xcd_pack": 0, "tile_rounds": 1},
     {"scan_chunk": 65536},
 ]
 
@@ -123,3 +126,29 @@ def test_cellnum_drop_variant(variant):
     outs = run_ranks(size, fn)
     for r in range(size):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), r
+
+
+@pytest.mark.parametrize("row_bytes", [12, 20, 24, 28, 36, 40, 44, 52, 56, 60])
+@pytest.mark.parametrize("topo", [[2, 2, 2], [4, 4, 4], [7], [1]])
+def test_image_pack_row_sizes(row_bytes, topo):
+    """pack_img (16-byte image pack) for every row size it takes, ragged n,
+    1..64 bins, against the C oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    _lib.tune("pack_img", 2)     # every row size the image pack takes
+    try:
+        rng = np.random.default_rng(row_bytes * 31 + len(topo))
+        n = 50_003 + 7 * row_bytes
+        dim = len(topo)
+        pos = rng.uniform(-0.5, 1.5, (n, dim))
+        data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
+        exp_pos = pos.copy()
+        cell = c_oracle.bin_positions(exp_pos, topo, [1.0] * dim)
+        exp, exp_off = c_oracle.partition(data, cell, int(np.prod(topo)))
+        P = GridPartitioner(topo, [1.0] * dim)
+        out, off = P.partition_by_position(torch.from_numpy(data).cuda(),
+                                           torch.from_numpy(pos).cuda())
+        assert np.array_equal(off.cpu().numpy(), exp_off)
+        assert np.array_equal(out.cpu().numpy(), exp)
+    finally:
+        _lib.tune("pack_img", DEFAULTS["pack_img"])

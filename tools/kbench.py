@@ -32,6 +32,8 @@ def run(variant):
         pos = f[:, :3]
     else:
         pos, rec = mgr.synth_clustered(N) if clustered else mgr.synth_uniform(N)
+        if rb != 32:   # other payload widths: random bytes beside the (N,3) f64 positions
+            rec = torch.randint(0, 256, (N, rb), dtype=torch.uint8, device="cuda")
     flat = rec.reshape(-1)
     for _ in range(3):
         part.partition_device(flat, rb, pos)
@@ -58,7 +60,7 @@ def run(variant):
     for k, v in {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0,
                  "pack_nt": 0, "pack_coop": 1, "pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0,
                  "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1, "pack_many": 1,
-                 "scan_onepass": 1, "scan_chunk": 2048}.items():
+                 "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1}.items():
         _lib.tune(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
