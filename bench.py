@@ -40,6 +40,7 @@ XGMI_PEAK_GBS = 7 * 153.0        # per GPU: 7 links x ~153 GB/s (task statement)
 SEED = 20261015
 N_CFG2 = 1 << 26                 # config 2: 64M on one GPU
 N_CFG3_PER_GPU = 1_000_000_000 // 8  # config 3: 1B over 8 GPUs
+N_CFG5_PER_GPU = 512_000_000 // 8    # config 5: 512M over 8 GPUs
 
 # Algorithmic bytes per particle, 24-byte f64 positions,
 # 32-byte records, 1-byte destinations.
@@ -106,6 +107,9 @@ def main():
     ap.add_argument("--prof", choices=("report", "all", "none"), default="report",
                     help="kernels timed with HIP events inside the timed region: report = "
                          "pack (+ exchange) only, all, none")
+    ap.add_argument("--config", type=int, choices=(2, 3, 4, 5), default=0,
+                    help="BASELINE config (default: 2 at one GPU, 3 for N > 1); 4 = clustered, "
+                         "5 = 36-byte records + 8x8x8 fine-cell sort")
     ap.add_argument("--exchange", action="store_true",
                     help="run the N>1 path (config 3, RCCL exchange) even at one GPU")
     args = ap.parse_args()
@@ -125,27 +129,71 @@ def main():
     multi = world > 1 or args.exchange
     if multi:
         import torch.distributed as dist
+        if world == 1:   # --exchange without a launcher: a one-rank group
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"),
+                         ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    cfg = args.config or (3 if multi else 2)
+    if multi and cfg == 2:
+        cfg = 3
+    topo = topology_for(world) if multi else [2, 2, 2]
+    rb, pos_desc = 32, "(N,3) float64, wrapped in place"
+    bytes_pp = dict(BYTES_PER_PARTICLE)
     if not multi:
         n = args.n or N_CFG2
-        workload = "cfg2_64M_uniform_2x2x2_local_partition"
         part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
-        pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=0)
-        flat = rec.reshape(-1)
+        if cfg == 5:
+            # one GPU's share of config 5: 64M 36-byte records; the local stage
+            # (bin + scan + pack into 8 destinations) and the destination-side
+            # fine-cell sort (8x8x8) of 64M rows inside one cell
+            workload = "cfg5_64M_rec36_2x2x2_local_partition_plus_fine_sort_888"
+            rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
+            rec, pos = mgr.synth_wide(n, seed=SEED, gid0=0)
+            recv, rpos = mgr.synth_wide(n, seed=SEED + 1, gid0=0, hi=0.5)
+            # rank 0's cell of the 2x2x2 grid as a one-rank system (same fine bins)
+            R1 = mgr.MPIGridRedistributor(None, [1, 1, 1], [0.5, 0.5, 0.5])
+            flat = rec.reshape(-1)
+            bytes_pp = {"bin_count": 12 + 12 + 1, "pack": 1 + 36 + 36}
 
-        def step():
-            part.partition_device(flat, 32, pos)
+            def step():
+                part.partition_device(flat, 36, pos)
+                R1.fine_cell_sort(recv, rpos, [8, 8, 8])
+        else:
+            if cfg == 4:
+                workload = "cfg4_64M_clustered_2x2x2_local_partition"
+                pos, rec = mgr.synth_clustered(n, seed=SEED, gid0=0)
+            else:
+                workload = "cfg2_64M_uniform_2x2x2_local_partition"
+                pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=0)
+            flat = rec.reshape(-1)
+
+            def step():
+                part.partition_device(flat, 32, pos)
     else:
-        n = args.n or N_CFG3_PER_GPU
-        workload = "cfg3_uniform_per_gpu_125M_full_exchange"
+        n = args.n or (N_CFG5_PER_GPU if cfg == 5 else N_CFG3_PER_GPU)
         comm = mgr.RcclComm.from_torch_distributed()
-        topo = topology_for(world)
         R = mgr.MPIGridRedistributor(comm, topo, [1.0, 1.0, 1.0])
-        pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=rank * n)
+        if cfg == 5:
+            workload = "cfg5_rec36_per_gpu_64M_full_exchange_plus_fine_sort_888"
+            rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
+            rec, pos = mgr.synth_wide(n, seed=SEED, gid0=rank * n)
+            bytes_pp = {"bin_count": 12 + 12 + 1, "pack": 1 + 36 + 36}
 
-        def step():
-            R.redistribute_by_position(rec, pos)
+            def step():
+                out = R.redistribute_by_position(rec, pos)
+                R.fine_cell_sort(out, out.view(torch.float32)[:, :3], [8, 8, 8])
+        else:
+            if cfg == 4:
+                workload = "cfg4_clustered_per_gpu_125M_full_exchange"
+                pos, rec = mgr.synth_clustered(n, seed=SEED, gid0=rank * n)
+            else:
+                workload = "cfg3_uniform_per_gpu_125M_full_exchange"
+                pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=rank * n)
+
+            def step():
+                R.redistribute_by_position(rec, pos)
 
     # Fresh input needs the in-place wrap written back (redist.py:68: x + L
     # rounds, so most in-box coordinates change on the first call).  The bin
@@ -212,7 +260,7 @@ def main():
     if world > 1 and "exchange" in kernels:
         # bytes this rank moved over xGMI per exchange: its off-rank sends +
         # receives (uniform input: (P-1)/P of the rows each way)
-        moved = 2 * n * 32 * (world - 1) / world
+        moved = 2 * n * rb * (world - 1) / world
         gbps = moved / (kernels["exchange"]["avg_ms"] / 1e3) / 1e9
         xgmi = {"achieved": gbps, "peak": XGMI_PEAK_GBS, "unit": "GB/s",
                 "frac": gbps / XGMI_PEAK_GBS,
@@ -223,11 +271,11 @@ def main():
     assert args.prof == "none" or kernels[dom]["in_timed_region"], \
         f"dominant kernel {dom} was not timed inside the timed region"
     avg_s = kernels[dom]["avg_ms"] / 1e3
-    alg_bytes = BYTES_PER_PARTICLE[dom] * n
+    alg_bytes = bytes_pp[dom] * n
     achieved = alg_bytes / avg_s / 1e9
     for k in ("bin_count", "pack"):
         if k in kernels:
-            kernels[k]["alg_GBps"] = BYTES_PER_PARTICLE[k] * n / (kernels[k]["avg_ms"] / 1e3) / 1e9
+            kernels[k]["alg_GBps"] = bytes_pp[k] * n / (kernels[k]["avg_ms"] / 1e3) / 1e9
     traffic = load_traffic(dom, workload)
 
     total = n * world * args.steps
@@ -238,11 +286,11 @@ def main():
             "value": value, "unit": "particles/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "gpu_ms_per_step": gpu_ms / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" if cfg == 5 else "f64",
             "data": "synthetic (splitmix64 uniform, generated on device)",
             "config": {"workload": workload, "particles_per_gpu": n,
-                       "grid": topology_for(world) if multi else [2, 2, 2],
-                       "payload_bytes": 32, "position": "(N,3) float64, wrapped in place",
+                       "grid": topo, "payload_bytes": rb, "position": pos_desc,
                        "parallelism": f"{world} rank(s), one GPU per grid cell" if multi
                        else "1 GPU, 8 virtual subdomains"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,

@@ -51,6 +51,9 @@ def synth_clustered(n, seed=20261015, gid0=0, box=1.0, n_halos=64, sigma=0.02, f
     L = torch.as_tensor(box, dtype=torch.float64, device="cuda").expand(3)
     centres = torch.rand((n_halos, 3), generator=g, dtype=torch.float64, device="cuda") * L
     w = (1.0 - torch.rand(n_halos, generator=g, dtype=torch.float64, device="cuda")) ** (-1.0 / alpha)
+    # the halos are global (same seed on every rank); each rank's particles
+    # come from its own stream (gid0)
+    g.manual_seed(int(seed) ^ (int(gid0) * 0x9E3779B97F4A7C15 & 0x7FFFFFFFFFFFFFFF))
     halo = torch.multinomial(w / w.sum(), n, replacement=True, generator=g)
     pos = centres[halo] + torch.randn((n, 3), generator=g, dtype=torch.float64,
                                       device="cuda") * (sigma * L)
@@ -63,3 +66,27 @@ def synth_clustered(n, seed=20261015, gid0=0, box=1.0, n_halos=64, sigma=0.02, f
         rec.view(torch.int64)[:, 3] = torch.arange(gid0, gid0 + n, device="cuda")
         rec = rec.view(torch.uint8).reshape(n, 32)
     return pos.contiguous(), rec
+
+
+def synth_wide(n, seed=20261015, gid0=0, box=1.0, lo=0.0, hi=None):
+    """BASELINE config 5 input: 36-byte records [pos f32 x3, vel f32 x3, mass
+    f32, id i64] as an (n, 36) uint8 GPU tensor, positions uniform in
+    [lo, hi)^3 (default the whole box), plus the (n, 3) float32 position view
+    into the records (row stride 9 elements) that redistribute_by_position /
+    fine_cell_sort take.  Test/bench input only (torch RNG)."""
+    import torch
+
+    _lib.require_gpu()
+    hi = box if hi is None else hi
+    g = torch.Generator(device="cuda").manual_seed(int(seed) ^ (int(gid0) * 0x9E3779B97F4A7C15
+                                                               & 0x7FFFFFFFFFFFFFFF))
+    rec = torch.empty((n, 36), dtype=torch.uint8, device="cuda")
+    f = rec.view(torch.float32)                       # (n, 9)
+    f[:, :3] = (lo + torch.rand((n, 3), generator=g, dtype=torch.float64, device="cuda")
+                * (hi - lo)).to(torch.float32)
+    f[:, 3:6] = torch.randn((n, 3), generator=g, device="cuda")
+    f[:, 6] = 1.0
+    ids = torch.arange(gid0, gid0 + n, dtype=torch.int64, device="cuda")
+    rec.view(torch.int32)[:, 7] = (ids & 0xFFFFFFFF).to(torch.int32)
+    rec.view(torch.int32)[:, 8] = (ids >> 32).to(torch.int32)
+    return rec, f[:, :3]
