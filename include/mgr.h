@@ -215,7 +215,8 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
  * Kernel-variant knobs for A/B measurement: "bin_staged", "bin_skip_clean",
  * "bin_depth", "bin_waves", "xcd_bin", "pack_small", "pack_coop",
  * "pack_sorted", "pack_nt", "pack_rpw", "xcd_pack", "tile_rounds",
- * "scan_onepass", "scan_chunk", and "prof_mask" (bit k: time profiler kernel id k, in the
+ * "scan_onepass", "scan_chunk", "scan_max_chunks", "pack_img", "many_super",
+ * and "prof_mask" (bit k: time profiler kernel id k, in the
  * order of the names listed under profiling below; default all)
  * (mgr_internal.h Tune); the defaults are the shipped configuration.
  * Process-wide, not thread-safe against concurrent launches.             */

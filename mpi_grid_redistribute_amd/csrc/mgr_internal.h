@@ -10,7 +10,8 @@ namespace mgr {
 
 constexpr int kBlock = 256;              // 4 waves of 64
 constexpr int kWaves = kBlock / 64;
-constexpr int kMaxTileRows = 4096;       // 16 rounds of 256 rows; spos fits uint16
+constexpr int kMaxTileRows = 65536;      // many-bin pack tiles (super-rounds of 4096 rows)
+constexpr int kCoopMaxRounds = 64;       // cooperative pack tiles <= 4096 rows
 constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
 constexpr int kScanMaxBlocks = 1024;      // two-pass scan (A/B knob scan_onepass = 0)
 constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups) at most
@@ -99,9 +100,11 @@ struct Tune {
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
+    int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
     int pack_img = 1;      // 16-byte-unit image pack for 4-byte-multiple rows (1: 24..60 B, 2: 12..60 B)
     int scan_onepass = 1;  // one-pass decoupled look-back scan (0: reduce + apply + totals)
     int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)
+    int scan_max_chunks = 1024;  // one-pass scan: at most this many chunks (look-back depth)
     int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)
 };
 extern Tune g_tune;

@@ -324,7 +324,8 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     if (g_tune.scan_onepass) {
         const int64_t target = g_tune.scan_chunk;         // counts per chunk (workgroup)
         int64_t cpb = (ws.T + target - 1) / target;
-        const int64_t cap = kScanFlags / nbins;           // >= 1 (nbins <= MGR_MAX_BINS)
+        int64_t cap = min((int64_t)g_tune.scan_max_chunks, (int64_t)kScanFlags) / nbins;
+        if (cap < 1) cap = 1;                             // nbins <= MGR_MAX_BINS = kScanFlags
         if (cpb > cap) cpb = cap;
         const int64_t chunk = (ws.T + cpb - 1) / cpb;
         cpb = (ws.T + chunk - 1) / chunk;                 // no empty chunk

@@ -170,7 +170,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
     int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
     using U = typename Unit<W>::T;
-    __shared__ int s_cnt[kMaxTileRows / 64][64];
+    __shared__ int s_cnt[kCoopMaxRounds][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
     // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
@@ -374,71 +374,82 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
     int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
     using U = typename Unit<W>::T;
-    constexpr int R = 16 * RPW;
+    constexpr int R = 16 * RPW;                                // rounds per super-round
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    long long* s_off = (long long*)smem;                       // [nb]
+    long long* s_off = (long long*)smem;                       // [nb] running bin bases
     uint16_t* tab = (uint16_t*)(smem + align16(nb * 8));       // [R][nb]
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
-    const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
-    for (int i = threadIdx.x; i < R * nb; i += blockDim.x) tab[i] = 0;
     for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {
         long long o = offsets[(int64_t)bb * T + tile];
         if (bb == redirect_bin) o -= bin_starts[bb];
         s_off[bb] = o;
     }
-    int nr[RPW];
-    unsigned b[RPW];
-    U v[RPW][UPR];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-        nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
-        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
-#pragma unroll
-        for (int k = 0; k < UPR; ++k)
-            if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
-    }
-    __syncthreads();   // table zeroed, tile offsets staged
-    unsigned long long peers[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-        const bool valid = lane < nr[q];
-        peers[q] = match_bin(b[q], valid, nbits);
-        if (valid && rank_in(peers[q]) == 0)
-            tab[(w * RPW + q) * nb + b[q]] = (uint16_t)__popcll(peers[q]);
-    }
-    __syncthreads();
-    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {   // exclusive prefix per bin
-        int run = 0;
-        for (int r = 0; r < R; ++r) {
-            const int c = tab[r * nb + bb];
-            tab[r * nb + bb] = (uint16_t)run;
-            run += c;
-        }
-    }
-    __syncthreads();
     U* __restrict__ d_u = (U*)dst;
     U* __restrict__ r_u = (U*)redirect_dst;
+    // the tile's super-rounds of 64 * R rows, in order: a bin's rows of
+    // consecutive super-rounds continue each other's output run, so the
+    // tile writes one run of ~tile_rows / nb rows per bin
+    for (int64_t sr0 = tile * (int64_t)tile_rows; sr0 < min(n, (tile + 1) * (int64_t)tile_rows);
+         sr0 += 64 * R) {
+        const int64_t row0 = sr0 + 64 * RPW * w;
+        for (int i = threadIdx.x; i < R * nb; i += blockDim.x) tab[i] = 0;
+        int nr[RPW];
+        unsigned b[RPW];
+        U v[RPW][UPR];
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-        long long tgt = -1;
-        if (lane < nr[q] && (int)b[q] != drop_bin)
-            tgt = (s_off[b[q]] + tab[(w * RPW + q) * nb + b[q]] + rank_in(peers[q])) |
-                  ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
+        for (int q = 0; q < RPW; ++q) {
+            nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
+            b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+        }
 #pragma unroll
-        for (int k = 0; k < UPR; ++k) {
-            const int u = 64 * k + lane;
-            const int r = u / UPR, part = u - r * UPR;
-            const long long t = __shfl(tgt, r, 64);
-            if (u < nr[q] * UPR && t >= 0) {
-                U* o = (t >> 62) ? r_u : d_u;
-                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
+        for (int q = 0; q < RPW; ++q) {
+            const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+#pragma unroll
+            for (int k = 0; k < UPR; ++k)
+                if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
+        }
+        __syncthreads();   // table zeroed (and, first time, tile offsets staged)
+        unsigned long long peers[RPW];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const bool valid = lane < nr[q];
+            peers[q] = match_bin(b[q], valid, nbits);
+            if (valid && rank_in(peers[q]) == 0)
+                tab[(w * RPW + q) * nb + b[q]] = (uint16_t)__popcll(peers[q]);
+        }
+        __syncthreads();
+        // per bin (one per thread, nb <= 1024): exclusive prefix over the
+        // super-round's rounds; the total moves the bin's running base later
+        int total = 0;
+        if (threadIdx.x < nb) {
+            const int bb = threadIdx.x;
+            for (int r = 0; r < R; ++r) {
+                const int c = tab[r * nb + bb];
+                tab[r * nb + bb] = (uint16_t)total;
+                total += c;
             }
         }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            long long tgt = -1;
+            if (lane < nr[q] && (int)b[q] != drop_bin)
+                tgt = (s_off[b[q]] + tab[(w * RPW + q) * nb + b[q]] + rank_in(peers[q])) |
+                      ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
+#pragma unroll
+            for (int k = 0; k < UPR; ++k) {
+                const int u = 64 * k + lane;
+                const int r = u / UPR, part = u - r * UPR;
+                const long long t = __shfl(tgt, r, 64);
+                if (u < nr[q] * UPR && t >= 0) {
+                    U* o = (t >> 62) ? r_u : d_u;
+                    o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
+                }
+            }
+        }
+        __syncthreads();   // every base and prefix read before they move on
+        if (threadIdx.x < nb) s_off[threadIdx.x] += total;
     }
 }
 
@@ -533,9 +544,11 @@ __global__ __launch_bounds__(1024) void pack_sorted_kernel(
 }
 
 // ============================================================ launchers
-// pack_many_kernel tiles: 64 rounds (4096 rows) up to 512 bins, 32 rounds up
-// to 1024 bins -- the uint16 [rounds][nbins] LDS table stays <= 64 KiB.
-static int many_tile_rows(int nbins) { return nbins <= 512 ? 4096 : 2048; }
+// pack_many_kernel: super-rounds of 64 rounds (4096 rows) up to 512 bins, 32
+// rounds up to 1024 bins -- the uint16 [rounds][nbins] LDS table stays <= 64
+// KiB -- and many_super super-rounds per tile (longer runs per bin).
+static int many_round_rows(int nbins) { return nbins <= 512 ? 4096 : 2048; }
+static int many_tile_rows(int nbins) { return many_round_rows(nbins) * g_tune.many_super; }
 
 int pack_tile_rows(int64_t row_bytes, int nbins) {
     if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
@@ -548,7 +561,7 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     if (nbins <= 64) return 1024 * g_tune.pack_rpw;
     if (g_tune.pack_many && nbins <= 1024 && row_bytes <= 64) return many_tile_rows(nbins);
     int r = 16;
-    while (r < kMaxTileRows / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
+    while (r < 4096 / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
 }
 
@@ -588,7 +601,7 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
 #undef MGR_PSS
         return hipGetLastError();
     }
-    if (g_tune.pack_coop) {
+    if (g_tune.pack_coop && tile_rows <= 2048) {
         // one wave per RPW 64-row rounds of the tile (<= 16 waves)
         const int rpw = tile_rows > 1024 ? 2 : 1;
         const int threads = tile_rows / rpw;
@@ -653,7 +666,9 @@ template <int W, int UPR, typename DestT>
 static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                               void* redirect_dst, hipStream_t s) {
-    const int lds = align16(nb * 8) + (tile_rows / 64) * nb * 2;
+    const int round_rows = many_round_rows(nb);
+    if (tile_rows % round_rows) return hipErrorNotSupported;
+    const int lds = align16(nb * 8) + (round_rows / 64) * nb * 2;
 #define MGR_PMK(RPW_)                                                                          \
     {                                                                                          \
         auto k = pack_many_kernel<W, UPR, DestT, RPW_>;                                        \
@@ -663,7 +678,7 @@ static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int 
                            drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, \
                            redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack);             \
     }
-    if (tile_rows == 4096) MGR_PMK(4)
+    if (round_rows == 4096) MGR_PMK(4)
     else MGR_PMK(2)
 #undef MGR_PMK
     return hipGetLastError();

@@ -20,7 +20,8 @@ from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _li
 
 DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
             "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
-            "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1}
+            "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
+            "scan_max_chunks": 1024}
 VARIANTS = [
     {"pack_sorted": 1},
     {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
@@ -49,6 +50,10 @@ VARIANTS = [
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},
     {"pack_img": 0},
+    {"many_super": 4},
+    {"scan_max_chunks": 4096},
+    {"scan_max_chunks": 8, "scan_chunk": 256},
+    {"many_super": 16, "xcd_pack": 0},
     {"pack_img": 1, "tile_rounds": 16, "pack_rpw": 2},
     {"pack_img": 1, "xcd_pack": 0, "tile_rounds": 1},
     {"scan_chunk": 65536},
@@ -67,7 +72,8 @@ def variant(request):
 
 
 @pytest.mark.parametrize("topo,row_bytes", [([2, 2, 2], 32), ([2, 2, 2], 36), ([7], 8),
-                                            ([4, 4, 4], 12), ([3, 3, 3], 64), ([2], 4)])
+                                            ([4, 4, 4], 12), ([3, 3, 3], 64), ([2], 4),
+                                            ([8, 8, 8], 36), ([5, 6, 10], 24)])
 def test_partition_variant_vs_c_oracle(variant, topo, row_bytes):
     rng = np.random.default_rng(row_bytes * 7 + len(topo))
     n = 70_001 + row_bytes

@@ -19,6 +19,8 @@ FINE = json.loads(os.environ.get("FB_FINE", "[8, 8, 8]"))
 
 
 def main():
+    for k, v in json.loads(os.environ.get("FB_VARIANT", "{}")).items():
+        _lib.tune(k, v)
     R = mgr.MPIGridRedistributor(None, [1, 1, 1], [0.5, 0.5, 0.5])  # rank 0's cell of 2x2x2
     g = torch.Generator(device="cuda").manual_seed(5)
     rec = torch.empty((N, 36), dtype=torch.uint8, device="cuda")
@@ -41,7 +43,8 @@ def main():
     b.record()
     torch.cuda.synchronize()
     _lib.profile_enable(False)
-    out = {"n": N, "fine": FINE, "ms_per_sort": a.elapsed_time(b) / ITERS}
+    out = {"n": N, "fine": FINE, "variant": json.loads(os.environ.get("FB_VARIANT", "{}")),
+           "ms_per_sort": a.elapsed_time(b) / ITERS}
     for k in ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack"):
         ms, cnt = _lib.profile_read(k)
         if cnt:
