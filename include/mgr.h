@@ -123,7 +123,10 @@ int mgr_cell_number_from_indexes(const mgr_plan* plan, const int64_t* idx, int64
  * Device-wide exclusive scan of the destination-major tile histogram:
  * segment start of every (bin, tile), bin starts, and per-bin totals
  * (bin_counts, int64[nbins], device) = the element counts of the
- * reference's send_buff[i] (redist.py:195-198).                           */
+ * reference's send_buff[i] (redist.py:195-198).  Consumes what a count
+ * producer (mgr_bin_count / mgr_bin_ids / mgr_select_count) left in the
+ * workspace, including the zeroed one-pass scan words: one producer
+ * launch precedes every scan on the same stream.                          */
 int mgr_scan(int64_t n, int nbins, int tile_rows, void* workspace, int64_t* bin_counts,
              void* stream);
 
