@@ -85,6 +85,33 @@ def cpu_baseline():
                       f"{[round(x, 3) for x in r['seconds']]} s, {el:.1f} s wall"}
 
 
+def cpu_baseline_c():
+    """Optimised host comparison point (oracle/, the checker): the threaded C
+    restatement of the local stage (wrap + bin + stable partition, exactly the
+    GPU step's work at N=1) on this host's cores, 16M particles of the same
+    layout, best of 3."""
+    from oracle import c_oracle
+
+    avail = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, omp) if omp > 0 else avail
+    n = 1 << 24
+    pos, ids = c_oracle.synth_uniform(SEED, 0, n, 3, 1.0)
+    rec = np.empty((n, 4), dtype=np.float64)
+    rec[:, :3] = pos
+    rec.view(np.int64)[:, 3] = ids
+    out = np.empty_like(rec)
+    secs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        c_oracle.local_partition_omp(pos, rec, [2, 2, 2], [1.0, 1.0, 1.0], threads=threads, out=out)
+        secs.append(time.perf_counter() - t0)
+    return {"value": n / min(secs), "unit": "particles/s", "cores": threads, "kind": "port",
+            "sample": f"{n} uniform particles, f64 (N,3) positions + 32-byte records, 2x2x2, "
+                      f"threaded C restatement (oracle/mgr_oracle.c oracle_local_partition_omp) "
+                      f"of the local stage, best of 3 {[round(x, 3) for x in secs]} s"}
+
+
 def load_traffic(kernel, workload):
     """HBM bytes/launch from a committed rocprofv3 PMC pass (profiles/traffic.json)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -124,6 +151,7 @@ def main():
     # CPU baseline first: its rank processes are spawned before this process
     # touches the GPU
     cpu = cpu_baseline() if (world == 1 and not args.no_cpu_baseline) else None
+    cpu_c = cpu_baseline_c() if (world == 1 and not args.no_cpu_baseline) else None
     torch.cuda.set_device(local)
     dist = None
     multi = world > 1 or args.exchange
@@ -300,6 +328,7 @@ def main():
             "kernels": kernels,
             "xgmi": xgmi,
             "cpu_baseline": cpu,
+            "cpu_baseline_c": cpu_c,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -42,6 +42,9 @@ def lib():
         L.oracle_pymod.restype = ctypes.c_double
         L.oracle_trunc_i64.argtypes = [ctypes.c_double]
         L.oracle_trunc_i64.restype = ctypes.c_int64
+        L.oracle_local_partition_omp.argtypes = [_P, _I64, _I64, ctypes.c_int, _P, _P,
+                                                 ctypes.c_int, _P, _I64, _P, _P, ctypes.c_int]
+        L.oracle_local_partition_omp.restype = _I64
         _lib = L
     return _lib
 
@@ -84,6 +87,26 @@ def partition(data, dest, nbins):
     total = lib().oracle_partition(_ptr(data), n, row_bytes, _ptr(dest), nbins, _ptr(out),
                                    _ptr(offsets))
     return out[:total], offsets
+
+
+def local_partition_omp(position, data, grid_topology, box_length, periodic=True, threads=1,
+                        out=None):
+    """Threaded host restatement of the local stage (wrap + bin of f64
+    positions in place, stable partition of ``data`` rows): the optimised
+    CPU comparison point of bench.py.  Returns (out, offsets)."""
+    assert position.dtype == np.float64 and position.strides[1] == 8
+    topo = np.ascontiguousarray(np.asarray(grid_topology).astype(np.int64))
+    box = np.ascontiguousarray(np.asarray(box_length, dtype=np.float64))
+    data = np.ascontiguousarray(data)
+    n = position.shape[0]
+    row_bytes = data.itemsize * (int(np.prod(data.shape[1:])) if data.ndim > 1 else 1)
+    if out is None:
+        out = np.empty_like(data)
+    offsets = np.zeros(int(np.prod(topo)) + 1, dtype=np.int64)
+    lib().oracle_local_partition_omp(_ptr(position), n, position.strides[0] // 8, len(topo),
+                                     _ptr(box), _ptr(topo), int(bool(periodic)), _ptr(data),
+                                     row_bytes, _ptr(out), _ptr(offsets), int(threads))
+    return out, offsets
 
 
 def synth_uniform(seed, gid0, n, dim=3, box=1.0):

@@ -23,6 +23,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 /* x86 cvttsd2si semantics of numpy astype(int64): NaN/out-of-range -> INT64_MIN (S10). */
 static int64_t trunc_i64(double v) {
@@ -73,39 +76,126 @@ int64_t oracle_trunc_i64(double v) { return trunc_i64(v); }
  *   periodic    : wrap + in-place write-back (redist.py:67-68)
  * Outputs: cell[r] (int64, row-major cell id), idx[r*dim+d] (optional).
  */
+static int64_t bin_one(void* pos, int pos_is_f32, int compute_f32, int64_t r, int64_t row_stride,
+                       int dim, const double* box, const int64_t* topo, const int64_t* offset,
+                       int periodic, int64_t* idx, int fast) {
+    int64_t c = 0;
+    for (int d = 0; d < dim; ++d) {
+        int64_t k;
+        if (pos_is_f32) {
+            float* p = (float*)pos + r * row_stride + d;
+            if (compute_f32) {
+                float L = (float)box[d];
+                if (periodic) *p = pymodf(pymodf(*p, L) + L, L);
+                float q = *p / L;
+                k = trunc_i64((double)q * (double)topo[d]);
+            } else {
+                double L = box[d];
+                if (periodic) *p = (float)pymod(pymod((double)*p, L) + L, L);
+                k = trunc_i64((double)*p / L * (double)topo[d]);
+            }
+        } else {
+            double* p = (double*)pos + r * row_stride + d;
+            double L = box[d];
+            if (periodic) {
+                const double x = *p;
+                if (fast && x >= 0.0 && x < L) {
+                    /* in-box: x % L == x and (x + L) % L == (x + L) - L exactly
+                     * (Sterbenz), 0 when x + L rounds to 2L -- the same value as the
+                     * general path (checked by tests/test_oracle.py) */
+                    const double y = x + L;
+                    *p = (y == L + L) ? 0.0 : y - L;
+                } else {
+                    *p = pymod(pymod(x, L) + L, L);
+                }
+            }
+            k = trunc_i64(*p / L * (double)topo[d]);
+        }
+        if (idx) idx[r * dim + d] = k;
+        if (fast && k >= 0 && k < topo[d])
+            c += offset[d] * k;   /* ((k % n) + n) % n == k: skip the integer divisions */
+        else
+            c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
+    }
+    return c;
+}
+
 void oracle_bin(void* pos, int pos_is_f32, int compute_f32, int64_t n, int64_t row_stride,
                 int dim, const double* box, const int64_t* topo, int periodic,
                 int64_t* cell, int64_t* idx) {
     int64_t offset[64];
     int64_t off = 1;
     for (int d = dim - 1; d >= 0; --d) { offset[d] = off; off *= topo[d]; }
-    for (int64_t r = 0; r < n; ++r) {
-        int64_t c = 0;
-        for (int d = 0; d < dim; ++d) {
-            int64_t k;
-            if (pos_is_f32) {
-                float* p = (float*)pos + r * row_stride + d;
-                if (compute_f32) {
-                    float L = (float)box[d];
-                    if (periodic) *p = pymodf(pymodf(*p, L) + L, L);
-                    float q = *p / L;
-                    k = trunc_i64((double)q * (double)topo[d]);
-                } else {
-                    double L = box[d];
-                    if (periodic) *p = (float)pymod(pymod((double)*p, L) + L, L);
-                    k = trunc_i64((double)*p / L * (double)topo[d]);
-                }
-            } else {
-                double* p = (double*)pos + r * row_stride + d;
-                double L = box[d];
-                if (periodic) *p = pymod(pymod(*p, L) + L, L);
-                k = trunc_i64(*p / L * (double)topo[d]);
-            }
-            if (idx) idx[r * dim + d] = k;
-            c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
+    for (int64_t r = 0; r < n; ++r)
+        cell[r] = bin_one(pos, pos_is_f32, compute_f32, r, row_stride, dim, box, topo, offset,
+                          periodic, idx, 0);
+}
+
+/*
+ * The local stage on the host's cores (bench.py cpu_baseline_c): wrap + bin
+ * of f64 positions and a stable partition of the rows, threaded: every
+ * thread bins a contiguous chunk and counts its bins, the per-(thread, bin)
+ * starts follow in (bin, thread) order, and every thread scatters its own
+ * chunk -- the same result as oracle_bin + oracle_partition.  Returns rows
+ * written; offsets[nbins+1].
+ */
+int64_t oracle_local_partition_omp(double* pos, int64_t n, int64_t row_stride, int dim,
+                                   const double* box, const int64_t* topo, int periodic,
+                                   const void* data, int64_t row_bytes, void* out,
+                                   int64_t* offsets, int nthreads) {
+    int64_t offset[64];
+    int64_t off = 1;
+    for (int d = dim - 1; d >= 0; --d) { offset[d] = off; off *= topo[d]; }
+    const int64_t nbins = off;
+    if (nthreads < 1) nthreads = 1;
+    int32_t* dest = (int32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
+    int64_t* start = (int64_t*)calloc((size_t)nthreads * (size_t)nbins, sizeof(int64_t));
+    const char* src = (const char*)data;
+    char* dst = (char*)out;
+    int fast = 1;   /* the in-box fast wrap needs L > 0 with 2L finite */
+    for (int d = 0; d < dim; ++d)
+        if (!(box[d] > 0.0) || !isfinite(box[d] + box[d])) fast = 0;
+#pragma omp parallel num_threads(nthreads)
+    {
+#ifdef _OPENMP
+        const int t = omp_get_thread_num(), T = omp_get_num_threads();
+#else
+        const int t = 0, T = 1;
+#endif
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        int64_t* h = start + (int64_t)t * nbins;
+        for (int64_t r = lo; r < hi; ++r) {
+            const int64_t c = bin_one(pos, 0, 0, r, row_stride, dim, box, topo, offset, periodic,
+                                      NULL, fast);
+            dest[r] = (int32_t)c;
+            h[c]++;
         }
-        cell[r] = c;
+#pragma omp barrier
+#pragma omp single
+        {
+            int64_t run = 0;
+            for (int64_t b = 0; b < nbins; ++b) {
+                offsets[b] = run;
+                for (int u = 0; u < T; ++u) {
+                    const int64_t c = start[(int64_t)u * nbins + b];
+                    start[(int64_t)u * nbins + b] = run;
+                    run += c;
+                }
+            }
+            offsets[nbins] = run;
+        }
+        if (row_bytes == 32) {   /* the bench layout: fixed-size copies the compiler inlines */
+            for (int64_t r = lo; r < hi; ++r)
+                memcpy(dst + (h[dest[r]]++) * 32, src + r * 32, 32);
+        } else {
+            for (int64_t r = lo; r < hi; ++r)
+                memcpy(dst + (h[dest[r]]++) * row_bytes, src + r * row_bytes, (size_t)row_bytes);
+        }
     }
+    const int64_t total = offsets[nbins];
+    free(start);
+    free(dest);
+    return total;
 }
 
 /*

@@ -186,3 +186,22 @@ def test_oracle_fine_cells_match_reference_binning(case):
         out, off = ro.fine_cell_sort(d, fid, nfine)
         assert G.same_bytes(out, f[f"r{r}_sorted"]), (case, r)
         assert off[-1] == len(d) and np.all(np.diff(off) == np.bincount(fid, minlength=nfine))
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+@pytest.mark.parametrize("topo", [[2, 2, 2], [3, 1, 5], [7]])
+def test_local_partition_omp_matches_serial(threads, topo):
+    """The threaded host restatement (bench cpu_baseline_c) equals the serial
+    C oracle: same wrapped positions, offsets and row order."""
+    rng = np.random.default_rng(threads * 10 + len(topo))
+    n = 20_011
+    dim = len(topo)
+    pos = rng.uniform(-1.5, 2.5, (n, dim))
+    data = rng.integers(0, 256, (n, 20 if threads != 3 else 32), dtype=np.uint8)
+    p1, p2 = pos.copy(), pos.copy()
+    cell = c_oracle.bin_positions(p1, topo, [1.0] * dim)
+    exp, exp_off = c_oracle.partition(data, cell, int(np.prod(topo)))
+    got, off = c_oracle.local_partition_omp(p2, data, topo, [1.0] * dim, threads=threads)
+    assert p1.tobytes() == p2.tobytes()
+    assert np.array_equal(off, exp_off)
+    assert np.array_equal(got, exp)
