@@ -137,6 +137,9 @@ def main():
     ap.add_argument("--config", type=int, choices=(2, 3, 4, 5), default=0,
                     help="BASELINE config (default: 2 at one GPU, 3 for N > 1); 4 = clustered, "
                          "5 = 36-byte records + 8x8x8 fine-cell sort")
+    ap.add_argument("--overload", type=float, default=0.0,
+                    help="N > 1 / --exchange: overload (halo) length per dimension in box units; "
+                         "the step then includes the halo exchange (redist.py:161-166)")
     ap.add_argument("--exchange", action="store_true",
                     help="run the N>1 path (config 3, RCCL exchange) even at one GPU")
     args = ap.parse_args()
@@ -220,8 +223,12 @@ def main():
                 workload = "cfg3_uniform_per_gpu_125M_full_exchange"
                 pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=rank * n)
 
+            ol = [args.overload] * 3 if args.overload > 0 else None
+            if ol:
+                workload += f"_halo{args.overload:g}"
+
             def step():
-                R.redistribute_by_position(rec, pos)
+                R.redistribute_by_position(rec, pos, overload_lengths=ol)
 
     # Fresh input needs the in-place wrap written back (redist.py:68: x + L
     # rounds, so most in-box coordinates change on the first call).  The bin
@@ -244,7 +251,7 @@ def main():
     # exchange inside the timed region: every timed launch adds two event
     # records to the stream (measured ~2-3 us of step time per kernel).  The
     # other kernels are timed in an untimed detail pass after the region.
-    timed = {"report": ["pack", "exchange"], "all": list(_lib.PROFILE_KERNELS),
+    timed = {"report": ["pack", "exchange", "halo"], "all": list(_lib.PROFILE_KERNELS),
              "none": []}[args.prof]
     _lib.profile_select(timed)
     _lib.profile_enable(bool(timed))
@@ -265,7 +272,7 @@ def main():
         elapsed = float(t.item())
 
     kernels = {}
-    for k in ("bin_count", "scan", "pack", "exchange"):
+    for k in ("bin_count", "scan", "pack", "exchange", "halo"):
         ms, cnt = _lib.profile_read(k)
         if cnt:
             kernels[k] = {"avg_ms": ms / cnt, "launches": cnt, "in_timed_region": True}
@@ -295,16 +302,22 @@ def main():
                 "note": "rank 0: bytes sent + received per grouped ncclSend/ncclRecv over its "
                         "avg duration; peak = 7 links x 153 GB/s (link rate taken as "
                         "bidirectional)"}
-    dom = max(("bin_count", "pack"), key=lambda k: kernels.get(k, {"avg_ms": 0})["avg_ms"])
-    assert args.prof == "none" or kernels[dom]["in_timed_region"], \
-        f"dominant kernel {dom} was not timed inside the timed region"
-    avg_s = kernels[dom]["avg_ms"] / 1e3
-    alg_bytes = bytes_pp[dom] * n
-    achieved = alg_bytes / avg_s / 1e9
-    for k in ("bin_count", "pack"):
-        if k in kernels:
-            kernels[k]["alg_GBps"] = bytes_pp[k] * n / (kernels[k]["avg_ms"] / 1e3) / 1e9
-    traffic = load_traffic(dom, workload)
+    roofline = None
+    if args.overload <= 0 and cfg != 5:
+        # one bin and one pack launch per step over all n rows
+        dom = max(("bin_count", "pack"), key=lambda k: kernels.get(k, {"avg_ms": 0})["avg_ms"])
+        assert args.prof == "none" or kernels[dom]["in_timed_region"], \
+            f"dominant kernel {dom} was not timed inside the timed region"
+        alg_bytes = bytes_pp[dom] * n
+        achieved = alg_bytes / (kernels[dom]["avg_ms"] / 1e3) / 1e9
+        for k in ("bin_count", "pack"):
+            if k in kernels:
+                kernels[k]["alg_GBps"] = bytes_pp[k] * n / (kernels[k]["avg_ms"] / 1e3) / 1e9
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": load_traffic(dom, workload), "alg_bytes_per_launch": alg_bytes}
+    # config 5 / halo steps launch the pack several times on different row
+    # counts: per-kernel averages are reported, the roofline is not
 
     total = n * world * args.steps
     value = total / elapsed
@@ -316,15 +329,15 @@ def main():
             "gpu_ms_per_step": gpu_ms / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32" if cfg == 5 else "f64",
-            "data": "synthetic (splitmix64 uniform, generated on device)",
+            "data": {2: "synthetic (splitmix64 uniform, generated on device)",
+                     3: "synthetic (splitmix64 uniform, generated on device)",
+                     4: "synthetic (64 Gaussian halos + 20 % uniform, torch RNG on device)",
+                     5: "synthetic (uniform 36-byte records, torch RNG on device)"}[cfg],
             "config": {"workload": workload, "particles_per_gpu": n,
                        "grid": topo, "payload_bytes": rb, "position": pos_desc,
                        "parallelism": f"{world} rank(s), one GPU per grid cell" if multi
                        else "1 GPU, 8 virtual subdomains"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes},
+            "roofline": roofline,
             "kernels": kernels,
             "xgmi": xgmi,
             "cpu_baseline": cpu,

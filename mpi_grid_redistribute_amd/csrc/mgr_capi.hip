@@ -517,6 +517,8 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
     else if (!strcmp(key, "scan_onepass")) mgr::g_tune.scan_onepass = (int)value;
     else if (!strcmp(key, "pack_img")) mgr::g_tune.pack_img = (int)value;
+    else if (!strcmp(key, "pack_sel")) mgr::g_tune.pack_sel = (int)value;
+    else if (!strcmp(key, "pack_compact")) mgr::g_tune.pack_compact = (int)value;
     else if (!strcmp(key, "scan_max_chunks")) {
         if (value < 1 || value > mgr::kScanFlags) return fail(MGR_EINVAL, "scan_max_chunks %lld", (long long)value);
         mgr::g_tune.scan_max_chunks = (int)value;

@@ -101,6 +101,8 @@ struct Tune {
     int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
     int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
+    int pack_compact = 1;  // selections (2 bins, bin 1 dropped): wave-per-tile compaction
+    int pack_sel = 1;      // selection packs (2 bins, one dropped) load only kept rows
     int pack_img = 1;      // 16-byte-unit image pack for 4-byte-multiple rows (1: 24..60 B, 2: 12..60 B)
     int scan_onepass = 1;  // one-pass decoupled look-back scan (0: reduce + apply + totals)
     int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)

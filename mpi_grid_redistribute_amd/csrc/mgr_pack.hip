@@ -168,7 +168,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kCoopMaxRounds][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -192,9 +192,19 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+        if (sel) {
+            // selection (most rows dropped): load only the units of kept rows
 #pragma unroll
-        for (int k = 0; k < UPR; ++k)
-            if (64 * k + lane < nr[q] * UPR) v[q][k] = ld<NT>(sp + 64 * k + lane);
+            for (int k = 0; k < UPR; ++k) {
+                const int u = 64 * k + lane;
+                const int rb = __shfl((int)b[q], u / UPR, 64);
+                if (u < nr[q] * UPR && rb != drop_bin) v[q][k] = ld<NT>(sp + u);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < UPR; ++k)
+                if (64 * k + lane < nr[q] * UPR) v[q][k] = ld<NT>(sp + 64 * k + lane);
+        }
     }
     // rank inside each round; lane l counts bin l
     unsigned long long peers[RPW];
@@ -237,6 +247,133 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
 }
 
+// Compaction for selections (2 bins, bin 1 dropped: the halo's rows to send,
+// redist.py:271-275): one wave per tile walks its rounds, ballots the kept
+// rows, and each kept row is copied by its own lane to the tile's bin-0
+// segment.  Per row only the destination byte is read unless it is kept, so a
+// sparse selection costs ~1 byte per row plus the kept rows -- the
+// cooperative pack reads every row and pays its per-tile barrier.
+template <int W, int UPR>
+__global__ __launch_bounds__(256) void compact_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
+    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst) {
+    using U = typename Unit<W>::T;
+    constexpr int D = 4;   // rounds per batch (8 measured the same: sparse rows cost whole lines)
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
+    if (tile >= T) return;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    long long base = offsets[tile];          // bin 0 (kept) segment of the tile
+    const U* __restrict__ s_u = (const U*)src + row0 * UPR;
+    U* __restrict__ d_u = (U*)dst;
+    unsigned nb_[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+        const int r = 64 * q + lane;
+        nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
+    }
+    for (int r0 = 0; r0 < rows; r0 += 64 * D) {
+        unsigned long long m[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) m[q] = __ballot(nb_[q] == 0u);
+        // next batch's destination bytes in flight
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const int r = r0 + 64 * (D + q) + lane;
+            nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
+        }
+        // unit-transposed loads of the kept rows only (lane l: units 64k + l);
+        // a dropped row's lanes all read the tile's first unit (one cached
+        // line, no HBM traffic) so every load is unconditional and the
+        // values stay in registers (a predicated load into an array is
+        // demoted to scratch)
+        U v[D][UPR];
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+#pragma unroll
+            for (int k = 0; k < UPR; ++k) {
+                const int u = 64 * k + lane, r = u / UPR;
+                const int64_t idx = ((m[q] >> r) & 1ull) ? (int64_t)(r0 + 64 * q) * UPR + u : 0;
+                v[q][k] = s_u[idx];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+#pragma unroll
+            for (int k = 0; k < UPR; ++k) {
+                const int u = 64 * k + lane, r = u / UPR, part = u - r * UPR;
+                if ((m[q] >> r) & 1ull) {
+                    const long long slot = base + __popcll(m[q] & ((1ull << r) - 1ull));
+                    d_u[slot * UPR + part] = v[q][k];
+                }
+            }
+            base += __popcll(m[q]);
+        }
+    }
+}
+
+// Rows of any width: one lane copies one kept row.
+template <int W>
+__global__ __launch_bounds__(256) void compact_any_kernel(
+    const uint8_t* __restrict__ src, int64_t upr, int64_t n, const uint8_t* __restrict__ dest,
+    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst) {
+    using U = typename Unit<W>::T;
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
+    if (tile >= T) return;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    long long base = offsets[tile];
+    const U* __restrict__ s_u = (const U*)src;
+    U* __restrict__ d_u = (U*)dst;
+    for (int r0 = 0; r0 < rows; r0 += 64) {
+        const bool keep = r0 + lane < rows && dest[row0 + r0 + lane] == 0;
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+            const U* sp = s_u + (row0 + r0 + lane) * upr;
+            U* dp = d_u + (base + rank_in(m)) * upr;
+            for (int64_t k = 0; k < upr; ++k) dp[k] = sp[k];
+        }
+        base += __popcll(m);
+    }
+}
+
+template <int W>
+static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                            int tile_rows, const Workspace& ws, void* dst, hipStream_t s) {
+    const dim3 grid((unsigned)((ws.T + 3) / 4));
+    const int upr = (int)(row_bytes / W);
+#define MGR_CK(U_)                                                                             \
+    case U_:                                                                                   \
+        hipLaunchKernelGGL((compact_kernel<W, U_>), grid, dim3(256), 0, s, (const uint8_t*)src, \
+                           n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows, (uint8_t*)dst); \
+        return hipGetLastError();
+    if (64 * W <= 1024 || upr <= 4) {
+        switch (upr) {
+            MGR_CK(1) MGR_CK(2) MGR_CK(3) MGR_CK(4)
+            default: break;
+        }
+    }
+    if (W <= 8) {
+        switch (upr) {
+            MGR_CK(5) MGR_CK(6) MGR_CK(7) MGR_CK(8)
+            default: break;
+        }
+    }
+    if (W == 4) {
+        switch (upr) {
+            MGR_CK(9) MGR_CK(10) MGR_CK(11) MGR_CK(12) MGR_CK(13) MGR_CK(14) MGR_CK(15) MGR_CK(16)
+            default: break;
+        }
+    }
+#undef MGR_CK
+    hipLaunchKernelGGL(compact_any_kernel<W>, grid, dim3(256), 0, s, (const uint8_t*)src,
+                       row_bytes / W, n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows,
+                       (uint8_t*)dst);
+    return hipGetLastError();
+}
+
 // Image pack for rows of RB bytes, RB a multiple of 4 but not of 16 (e.g.
 // the 36-byte records of config 5), <= 64 bins: the cooperative shape of
 // pack_coop_kernel (one wave per 64-row round, per-bin bases exchanged
@@ -255,7 +392,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel) {
     static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
     constexpr int RBYTES = 64 * RB;                 // one round, a multiple of 16
     constexpr int NU = (RBYTES / 16 + 63) / 64;     // 16-byte units per lane
@@ -285,7 +422,14 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
 #pragma unroll
     for (int k = 0; k < NU; ++k) {
         const int x = 16 * (64 * k + lane);
-        if (x + 16 <= nbytes) {
+        bool need = true;
+        if (sel) {   // selection: skip units whose rows (at most two, RB > 16) are all dropped
+            const int b0 = __shfl((int)b, min(x / RB, 63), 64);
+            const int b1 = __shfl((int)b, min((x + 15) / RB, 63), 64);
+            need = b0 != drop_bin || b1 != drop_bin;
+        }
+        if (!need) {
+        } else if (x + 16 <= nbytes) {
             v[k] = *(const u32x4_t*)(sp + x);
         } else if (x < nbytes) {            // last partial unit of the array
             const uint32_t* q = (const uint32_t*)(sp + x);
@@ -609,7 +753,10 @@ static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int
         hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T), \
                            dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
                            nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack)
+                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel)
+        // selection packs (2 bins, one dropped: the halo's rows to send) skip
+        // the loads of dropped rows; elsewhere loads go out before the bins are known
+        const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
         if (g_tune.pack_nt >= 2) {
             if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
         } else if (g_tune.pack_nt == 1) {
@@ -720,7 +867,8 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s,
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
-                       (uint8_t*)redirect_dst, g_tune.xcd_pack);
+                       (uint8_t*)redirect_dst, g_tune.xcd_pack,
+                       g_tune.pack_sel && nb <= 2 && drop_bin >= 0);
     return hipGetLastError();
 }
 
@@ -784,8 +932,16 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
     uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
     prof_begin(s, K_PACK);
-    hipError_t e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
-                            redirect_bin, redirect_dst, s);
+    hipError_t e = hipErrorNotSupported;
+    if (g_tune.pack_compact && nbins == 2 && drop_bin == 1 && redirect_bin < 0) {
+        if ((a & 15) == 0) e = compact_t<16>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
+        else if ((a & 7) == 0) e = compact_t<8>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
+        else if ((a & 3) == 0) e = compact_t<4>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
+        else e = compact_t<1>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
+    }
+    if (e == hipErrorNotSupported)
+        e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
+                     redirect_dst, s);
     if (e != hipErrorNotSupported) {
         prof_end(s, K_PACK);
         return e;

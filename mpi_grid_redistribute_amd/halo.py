@@ -63,6 +63,9 @@ def thresholds(R, overload_lengths):
     return hi, lo
 
 
+SELECT_TILE_ROWS = 4096
+
+
 class DeviceSelect:
     """Selections on the GPU: flags (mgr_halo_flags), per-mask 2-bin
     partition counts (mgr_select_count + mgr_scan) and stable packs."""
@@ -82,7 +85,9 @@ class DeviceSelect:
     def select(self, flags, n, mask, max_row_bytes):
         """-> (handle, count tensor [1] on the device)."""
         lib = _lib.load()
-        tile_rows = lib.mgr_tile_rows(int(max_row_bytes), 2)
+        # long tiles: the selection pack is a wave-per-tile compaction
+        # (mgr_pack with 2 bins, bin 1 dropped), whose cost is per tile
+        tile_rows = SELECT_TILE_ROWS
         ws = torch.empty(int(lib.mgr_workspace_bytes(int(n), 2, tile_rows)), dtype=torch.uint8,
                          device=self.dev)
         dest = torch.empty(max(n, 1), dtype=torch.uint8, device=self.dev)

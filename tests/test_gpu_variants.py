@@ -21,7 +21,7 @@ from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _li
 DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
             "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
             "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
-            "scan_max_chunks": 1024}
+            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1}
 VARIANTS = [
     {"pack_sorted": 1},
     {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
@@ -50,6 +50,8 @@ VARIANTS = [
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},
     {"pack_img": 0},
+    {"pack_sel": 0},
+    {"pack_compact": 0},
     {"many_super": 4},
     {"scan_max_chunks": 4096},
     {"scan_max_chunks": 8, "scan_chunk": 256},
@@ -158,3 +160,23 @@ def test_image_pack_row_sizes(row_bytes, topo):
         assert np.array_equal(out.cpu().numpy(), exp)
     finally:
         _lib.tune("pack_img", DEFAULTS["pack_img"])
+
+
+@pytest.mark.parametrize("case", ["halo_p8_f64_rec32.npz", "halo_p2_f32_rec36.npz",
+                                  "halo_p27_333_ids.npz"])
+def test_halo_variant(variant, case):
+    """The overload exchange (selection packs: compaction, coop, image) under
+    every variant, against the reference's own outputs."""
+    f = G.load(case)
+    size = int(f["size"])
+    topo, box, ol = f["topology"], f["box"], list(f["overload"])
+    data = [d.copy() for d in G.per_rank(f, "data", size)]
+    pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
+
+    def fn(comm, r):
+        return MPIGridRedistributor(comm if size > 1 else None, topo, box).redistribute_by_position(
+            data[r], pos[r], overload_lengths=ol)
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
