@@ -510,6 +510,11 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "pack_small")) mgr::g_tune.pack_small = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
+    else if (!strcmp(key, "many_rows")) {
+        if (value != 0 && value != 1024 && value != 2048 && value != 4096)
+            return fail(MGR_EINVAL, "many_rows %lld (0, 1024, 2048 or 4096)", (long long)value);
+        mgr::g_tune.many_rows = (int)value;
+    }
     else if (!strcmp(key, "bin_skip_clean")) mgr::g_tune.bin_skip_clean = (int)value;
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;

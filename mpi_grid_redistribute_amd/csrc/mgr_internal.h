@@ -107,6 +107,7 @@ struct Tune {
     int scan_onepass = 1;  // one-pass decoupled look-back scan (0: reduce + apply + totals)
     int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)
     int scan_max_chunks = 1024;  // one-pass scan: at most this many chunks (look-back depth)
+    int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)
     int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)
 };
 extern Tune g_tune;

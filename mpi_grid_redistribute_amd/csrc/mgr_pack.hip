@@ -688,10 +688,19 @@ __global__ __launch_bounds__(1024) void pack_sorted_kernel(
 }
 
 // ============================================================ launchers
-// pack_many_kernel: super-rounds of 64 rounds (4096 rows) up to 512 bins, 32
-// rounds up to 1024 bins -- the uint16 [rounds][nbins] LDS table stays <= 64
-// KiB -- and many_super super-rounds per tile (longer runs per bin).
-static int many_round_rows(int nbins) { return nbins <= 512 ? 4096 : 2048; }
+// pack_many_kernel: super-rounds of 64 * R rows (the uint16 [R][nbins] LDS
+// table stays <= 128 KiB at 4096 rows and 1024 bins), many_super super-rounds
+// per tile (A/B: longer per-bin runs, slower).
+// Up to 512 bins 2048-row super-rounds (8x8x8 cells, 64M 36-byte rows: pack
+// 1.43-1.49 vs 1.55-1.70 ms at 4096 rows and 1.70 at 1024; the bin kernel and
+// the scan pay ~+0.05 ms each for the twice larger histogram; whole sort 2.17-2.24
+// vs 2.19-2.34 ms; 120 cells 1.85 vs 2.03 ms); above 512 bins 4096 rows (1024
+// cells: 2.53 vs 2.84 ms -- there the [bins][tiles] histogram dominates).
+// profiles/round1/fine_many_ab.log, fine_shapes_ab.log.
+static int many_round_rows(int nbins) {
+    if (g_tune.many_rows > 0) return g_tune.many_rows;
+    return nbins <= 512 ? 2048 : 4096;
+}
 static int many_tile_rows(int nbins) { return many_round_rows(nbins) * g_tune.many_super; }
 
 int pack_tile_rows(int64_t row_bytes, int nbins) {
@@ -826,7 +835,9 @@ static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int 
                            redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack);             \
     }
     if (round_rows == 4096) MGR_PMK(4)
-    else MGR_PMK(2)
+    else if (round_rows == 2048) MGR_PMK(2)
+    else if (round_rows == 1024) MGR_PMK(1)
+    else return hipErrorNotSupported;
 #undef MGR_PMK
     return hipGetLastError();
 }

@@ -243,7 +243,8 @@ def test_return_positions():
 
 
 # ----------------------------------------------- 1-GPU partition (Cfg2)
-@pytest.mark.parametrize("nbins_topo", [[1], [2], [7], [2, 2, 2], [3, 3, 3], [4, 4, 4], [5, 6, 10]])
+@pytest.mark.parametrize("nbins_topo", [[1], [2], [7], [2, 2, 2], [3, 3, 3], [4, 4, 4], [5, 6, 10],
+                                        [9, 9, 9], [8, 8, 16]])
 @pytest.mark.parametrize("row_bytes", [1, 3, 8, 12, 24, 32, 36, 100, 1000])
 def test_partition_vs_c_oracle(nbins_topo, row_bytes):
     rng = np.random.default_rng(row_bytes * 131 + len(nbins_topo))
@@ -260,6 +261,29 @@ def test_partition_vs_c_oracle(nbins_topo, row_bytes):
     tpos = torch.from_numpy(pos).cuda()
     out, off = P.partition_by_position(torch.from_numpy(data).cuda(), tpos)
     assert G.same_bytes(tpos.cpu().numpy(), exp_pos)
+    assert np.array_equal(off.cpu().numpy(), exp_off)
+    assert np.array_equal(out.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("topo", [[8, 8, 8], [8, 8, 16]])
+@pytest.mark.parametrize("row_bytes", [8, 36])
+def test_partition_many_bins_skewed(topo, row_bytes):
+    """65..1024 destinations (the many-destination pack) with heavy skew: most
+    rows in one cell (whole tiles of one bin), the rest spread, a ragged tail."""
+    rng = np.random.default_rng(sum(topo) + row_bytes)
+    n = 3 * 4096 * 4 + 777
+    pos = rng.uniform(0.0, 1.0, (n, 3))
+    hot = rng.random(n) < 0.7
+    pos[hot] = 0.51 / np.asarray(topo)   # all inside cell (0, 0, 0) ... + offset
+    pos[hot, 0] += 3.0 / topo[0]
+    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
+    exp_pos = pos.copy()
+    cell = c_oracle.bin_positions(exp_pos, topo, [1.0] * 3)
+    nb = int(np.prod(topo))
+    exp, exp_off = c_oracle.partition(data, cell, nb)
+    P = GridPartitioner(topo, [1.0] * 3)
+    tpos = torch.from_numpy(pos).cuda()
+    out, off = P.partition_by_position(torch.from_numpy(data).cuda(), tpos)
     assert np.array_equal(off.cpu().numpy(), exp_off)
     assert np.array_equal(out.cpu().numpy(), exp)
 

@@ -19,7 +19,7 @@ mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
 DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
-            "pack_small": 1, "pack_nt": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
+            "pack_small": 1, "pack_nt": 0, "many_rows": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
             "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
             "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1}
 VARIANTS = [
@@ -59,6 +59,10 @@ VARIANTS = [
     {"pack_img": 1, "tile_rounds": 16, "pack_rpw": 2},
     {"pack_img": 1, "xcd_pack": 0, "tile_rounds": 1},
     {"scan_chunk": 65536},
+    {"many_rows": 4096},
+    {"many_rows": 2048, "many_super": 2},
+    {"many_rows": 1024},
+    {"many_rows": 1024, "many_super": 4},
 ]
 
 
@@ -75,7 +79,7 @@ def variant(request):
 
 @pytest.mark.parametrize("topo,row_bytes", [([2, 2, 2], 32), ([2, 2, 2], 36), ([7], 8),
                                             ([4, 4, 4], 12), ([3, 3, 3], 64), ([2], 4),
-                                            ([8, 8, 8], 36), ([5, 6, 10], 24)])
+                                            ([8, 8, 8], 36), ([5, 6, 10], 24), ([9, 9, 9], 36)])
 def test_partition_variant_vs_c_oracle(variant, topo, row_bytes):
     rng = np.random.default_rng(row_bytes * 7 + len(topo))
     n = 70_001 + row_bytes
