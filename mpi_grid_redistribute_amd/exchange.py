@@ -32,19 +32,22 @@ class ExchangeLayout:
     redirect_self: bool
 
 
-def exchange(transport, row_bytes, bin_counts, rank, device, pack):
+def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=None):
     """Run steps 1-4.  ``bin_counts``: int64 tensor [size] of rows per
     destination (on ``device``).  ``pack(field, send, redirect_bin,
-    redirect_out)`` packs field ``field``.  Returns (outs, layout); outs are
-    flat uint8 tensors of total_recv * row_bytes[f] bytes (>= 1 byte)."""
+    redirect_out)`` packs field ``field``.  ``extra_rows(total_recv)``: spare
+    rows to allocate after the received ones (the halo appends there).
+    Returns (outs, layout); outs are flat uint8 tensors of (total_recv +
+    extra) * row_bytes[f] bytes (>= 1 byte)."""
     sc, rc = transport.exchange_counts(bin_counts)
     lay = ExchangeLayout(send_counts=sc, recv_counts=rc, send_offsets=excl_cumsum(sc),
                          recv_offsets=excl_cumsum(rc), total_recv=int(rc.sum()),
                          total_send=int(sc.sum()), redirect_self=bool(transport.skips_self))
     size = len(sc)
+    extra = int(extra_rows(lay.total_recv)) if extra_rows is not None else 0
     outs, sends = [], []
     for f, rb in enumerate(row_bytes):
-        out = torch.empty(max(lay.total_recv * rb, 1), dtype=torch.uint8, device=device)
+        out = torch.empty(max((lay.total_recv + extra) * rb, 1), dtype=torch.uint8, device=device)
         n_send = lay.total_send
         if lay.redirect_self and size == 1:
             n_send = 0  # everything is the self segment

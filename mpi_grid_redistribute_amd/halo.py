@@ -66,6 +66,17 @@ def thresholds(R, overload_lengths):
 SELECT_TILE_ROWS = 4096
 
 
+def halo_capacity(R, m, overload_lengths):
+    """Spare rows to reserve after a rank's m redistributed rows for its halo:
+    the uniform-density estimate m * (prod(1 + 2 ol/len) - 1), x1.25, + 4096.
+    A halo that outgrows it still works (exchange_overload then moves to its
+    own store and the caller concatenates)."""
+    cl = np.asarray(R.cell_length, dtype=np.float64)
+    ol = np.maximum(np.asarray(overload_lengths, dtype=np.float64), 0.0)
+    frac = float(np.prod(1.0 + 2.0 * ol / cl) - 1.0)
+    return int(m * frac * 1.25) + 4096
+
+
 class DeviceSelect:
     """Selections on the GPU: flags (mgr_halo_flags), per-mask 2-bin
     partition counts (mgr_select_count + mgr_scan) and stable packs."""
@@ -105,11 +116,16 @@ class DeviceSelect:
 
 
 def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n,
-                      overload_lengths, periodic=True, sel=None):
+                      overload_lengths, periodic=True, sel=None, arena=None):
     """Overload rows of rank R (redist.py:202-309).  ``data_flat``/``pos_flat``:
     flat uint8 tensors of this rank's n rows (payload rows of ``rbd`` bytes;
-    positions (n, ncols) float32/float64 rows, ncols >= dim).  Returns
-    (overload data flat, overload positions flat, rows)."""
+    positions (n, ncols) float32/float64 rows, ncols >= dim).  The overload
+    buffer only grows at its end (concat(buffer, from_a, from_b), :305), so
+    its rows live in an append-only store: ``arena`` = (data store, position
+    store, first row, spare rows), e.g. the free tail of the redistribution's
+    output, is used while the rows fit; beyond it the rows move once to a
+    store of their own with headroom.  Returns (overload data flat, overload
+    positions flat, rows, whether they stayed in the arena)."""
     dim = R.dim
     assert len(overload_lengths) == dim, \
         "Overload lengths must be the same length as the dimensions"  # redist.py:245
@@ -119,13 +135,19 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
     rbp = ncols * isz
     hi, lo = thresholds(R, overload_lengths)
     seg_local = (sel.flags(pos_flat, n, ncols, pos_code, dim, hi, lo), n, data_flat, pos_flat)
-    ov_d = torch.empty(0, dtype=torch.uint8, device=dev)
-    ov_p = torch.empty(0, dtype=torch.uint8, device=dev)
+    if arena is not None:
+        st_d, st_p, base, cap = arena
+    else:
+        st_d = st_p = None
+        base, cap = 0, 0
+    in_arena = arena is not None
     m = 0
     for d in range(dim):
         a, b, keep_a, keep_b = neighbours(R, d, periodic)
         segs = [seg_local]
         if m:
+            ov_d = st_d[base * rbd:(base + m) * rbd]
+            ov_p = st_p[base * rbp:(base + m) * rbp]
             segs.append((sel.flags(ov_p, m, ncols, pos_code, dim, hi, lo), m, ov_d, ov_p))
         sends = []
         for mask, keep in ((1 << (2 * d), keep_a), (1 << (2 * d + 1), keep_b)):
@@ -155,16 +177,24 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
         transport.sendrecv(cs[1:2].view(torch.uint8), b, cr[1:2].view(torch.uint8), a)  # :298-303
         r_from_b, r_from_a = (int(x) for x in cr.cpu().tolist())
         new_m = m + r_from_a + r_from_b
-        nd = torch.empty(max(new_m * rbd, 1), dtype=torch.uint8, device=dev)
-        npb = torch.empty(max(new_m * rbp, 1), dtype=torch.uint8, device=dev)
-        if m:
-            nd[: m * rbd].copy_(ov_d[: m * rbd])
-            npb[: m * rbp].copy_(ov_p[: m * rbp])
-        # concat(buffer, from_a, from_b) (redist.py:305)
+        if st_d is None or new_m > cap:
+            # outgrew the store: a store of its own with headroom, rows so far moved once
+            ncap = max(2 * new_m, 1024)
+            nd = torch.empty(ncap * rbd, dtype=torch.uint8, device=dev)
+            npb = torch.empty(ncap * rbp, dtype=torch.uint8, device=dev)
+            if m:
+                nd[: m * rbd].copy_(st_d[base * rbd:(base + m) * rbd])
+                npb[: m * rbp].copy_(st_p[base * rbp:(base + m) * rbp])
+            st_d, st_p, base, cap, in_arena = nd, npb, 0, ncap, False
+        # concat(buffer, from_a, from_b) (redist.py:305): appended in place
+        od, op = st_d[base * rbd:], st_p[base * rbp:]
         ia, ib = m, m + r_from_a
-        transport.sendrecv(bufs[0][1], a, nd[ib * rbd:(ib + r_from_b) * rbd], b)
-        transport.sendrecv(bufs[0][2], a, npb[ib * rbp:(ib + r_from_b) * rbp], b)
-        transport.sendrecv(bufs[1][1], b, nd[ia * rbd:(ia + r_from_a) * rbd], a)
-        transport.sendrecv(bufs[1][2], b, npb[ia * rbp:(ia + r_from_a) * rbp], a)
-        ov_d, ov_p, m = nd, npb, new_m
-    return ov_d[: m * rbd], ov_p[: m * rbp], m
+        transport.sendrecv(bufs[0][1], a, od[ib * rbd:(ib + r_from_b) * rbd], b)
+        transport.sendrecv(bufs[0][2], a, op[ib * rbp:(ib + r_from_b) * rbp], b)
+        transport.sendrecv(bufs[1][1], b, od[ia * rbd:(ia + r_from_a) * rbd], a)
+        transport.sendrecv(bufs[1][2], b, op[ia * rbp:(ia + r_from_a) * rbp], a)
+        m = new_m
+    if not m:
+        empty = torch.empty(0, dtype=torch.uint8, device=dev)
+        return empty, empty, 0, in_arena
+    return st_d[base * rbd:(base + m) * rbd], st_p[base * rbp:(base + m) * rbp], m, in_arena

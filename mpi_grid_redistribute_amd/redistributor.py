@@ -40,7 +40,7 @@ from . import _lib
 from ._arrays import Positions, Rows, box_dtype_code, device, id_array
 from .comm import SelfComm, as_transport
 from .exchange import exchange
-from .halo import exchange_overload
+from .halo import exchange_overload, halo_capacity
 
 
 class _Plan:
@@ -236,19 +236,30 @@ class MPIGridRedistributor:
         row_bytes_hint = [rows.row_bytes]
         if want_pos:
             row_bytes_hint.append(self._pos_row_bytes(position, pos))
-        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=row_bytes_hint)
+        extra = (lambda m_: halo_capacity(self, m_, overload_lengths)) if halo else None
+        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=row_bytes_hint,
+                            extra_rows=extra)
         if not halo:
             res = rows.wrap(outs[0], m)
             if return_positions:
                 return res, fields[1].wrap(outs[1], m)
             return res
         rbd, rbp = rows.row_bytes, fields[1].row_bytes
-        ov_d, ov_p, mo = exchange_overload(self, self.comm, outs[0][: m * rbd], rbd,
-                                           outs[1][: m * rbp], int(position.shape[1]), pos.code,
-                                           m, list(overload_lengths), periodic=True)
-        res = rows.wrap(torch.cat([outs[0][: m * rbd], ov_d]), m + mo)  # redist.py:166
+        # the halo rows are appended in place after the m received rows while
+        # they fit the spare capacity (no concatenation copies)
+        cap = outs[0].numel() // max(rbd, 1) - m
+        ov_d, ov_p, mo, in_place = exchange_overload(
+            self, self.comm, outs[0][: m * rbd], rbd, outs[1][: m * rbp],
+            int(position.shape[1]), pos.code, m, list(overload_lengths), periodic=True,
+            arena=(outs[0], outs[1], m, cap))
+        if in_place:   # redist.py:166: concatenate(data, overload)
+            res_d, res_p = outs[0][: (m + mo) * rbd], outs[1][: (m + mo) * rbp]
+        else:
+            res_d = torch.cat([outs[0][: m * rbd], ov_d])
+            res_p = torch.cat([outs[1][: m * rbp], ov_p]) if return_positions else None
+        res = rows.wrap(res_d, m + mo)
         if return_positions:
-            return res, fields[1].wrap(torch.cat([outs[1][: m * rbp], ov_p]), m + mo)
+            return res, fields[1].wrap(res_p, m + mo)
         return res
 
     def exchange_overload_by_position(self, data, position, overload_lengths,
@@ -271,9 +282,9 @@ class MPIGridRedistributor:
             raise TypeError(f"position dtype {position.dtype} not supported (float32/float64)")
         if prow.n != rows.n:
             raise ValueError(f"data has {rows.n} rows, position has {prow.n}")
-        ov_d, ov_p, mo = exchange_overload(self, self.comm, rows.flat, rows.row_bytes, prow.flat,
-                                           int(position.shape[1]), code, rows.n,
-                                           list(overload_lengths), periodic=bool(periodic))
+        ov_d, ov_p, mo, _ = exchange_overload(self, self.comm, rows.flat, rows.row_bytes,
+                                              prow.flat, int(position.shape[1]), code, rows.n,
+                                              list(overload_lengths), periodic=bool(periodic))
         res = rows.wrap(ov_d, mo)
         return (res, prow.wrap(ov_p, mo)) if return_positions else res
 
@@ -338,7 +349,7 @@ class MPIGridRedistributor:
         outs, m = self._run([rows], binner, rows.n, drop=True)
         return rows.wrap(outs[0], m)
 
-    def _run(self, fields, binner, n, drop, row_bytes_hint=None):
+    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None):
         """bin -> scan -> count exchange -> pack -> row exchange."""
         P = self.size
         nb = P + 1 if drop else P
@@ -356,7 +367,7 @@ class MPIGridRedistributor:
                       _lib.ptr(redirect_out), stream)
 
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
-                             self._dev, pack)
+                             self._dev, pack, extra_rows=extra_rows)
         return outs, lay.total_recv
 
     # ------------------------------------------------------------ helpers

@@ -120,3 +120,46 @@ def test_halo_rccl_single_rank():
         assert G.same_bytes(pos, f["r0_pos_out"])
     finally:
         comm.close()
+
+
+
+@pytest.mark.parametrize("clustered", [False, True])
+def test_halo_in_place_and_overflow(clustered):
+    """The halo rows are appended in place after the redistributed rows while
+    they fit the spare capacity halo_capacity() reserves (uniform estimate);
+    particles packed against the cell faces outgrow it and take the
+    concatenating path.  Both against the oracle, with return_positions."""
+    from mpi_grid_redistribute_amd.halo import halo_capacity
+    rng = np.random.default_rng(77 + clustered)
+    size, topo, box, ol = 4, [2, 2, 1], [1.0, 1.0, 1.0], [0.1, 0.1, 0.05]
+    pos = []
+    for r in range(size):
+        p = rng.uniform(0.0, 1.0, (30_000 + 1000 * r, 3))
+        if clustered:   # most rows within ol of the x = 0.5 / y = 0.5 faces
+            k = rng.random(len(p)) < 0.85
+            p[k, 0] = 0.5 + rng.uniform(-0.09, 0.09, int(k.sum()))
+            p[k, 1] = 0.5 + rng.uniform(-0.09, 0.09, int(k.sum()))
+        pos.append(p)
+    data = [np.arange(len(p), dtype=np.int64) + 1_000_000 * r for r, p in enumerate(pos)]
+    pos_o = [p.copy() for p in pos]
+    exp = ro.redistribute_by_position_overload_all_ranks(topo, box, size, data, pos_o, ol)
+
+    def fn(comm, r):
+        R = MPIGridRedistributor(comm, topo, box)
+        out = R.redistribute_by_position(data[r], pos[r], overload_lengths=ol,
+                                         return_positions=True)
+        return out, R
+
+    outs = run_ranks(size, fn)
+    fits = []
+    for r in range(size):
+        (got, gpos), R = outs[r]
+        assert G.same_bytes(got, exp[r]), r
+        assert len(gpos) == len(got)
+        src_rank, src_idx = got // 1_000_000, got % 1_000_000
+        want = np.stack([pos_o[s][i] for s, i in zip(src_rank, src_idx)])
+        assert G.same_bytes(gpos, want), r
+        own = sum(int(np.sum(ro.cell_number_from_position(
+            ro.Geometry(topo, box, size, s), pos_o[s].copy()) == r)) for s in range(size))
+        fits.append(len(got) - own <= halo_capacity(R, own, ol))
+    assert all(fits) if not clustered else not any(fits)

@@ -85,16 +85,35 @@ def local_inputs(f, case):
     return local, local_pos, True
 
 
-def run_rank(f, case, transport, r):
+def run_rank(f, case, transport, r, spare=None):
+    """``spare``: None = the overload gets a store of its own; else the local
+    rows sit at the head of a store with ``spare`` free rows after them (the
+    layout redistribute_by_position hands over) and the halo appends there."""
     size = int(f["size"])
     data, pos, periodic = local_inputs(f, case)
     R = GeoRank(f["topology"], f["box"], size, r)
     d, p = data[r], pos[r]
     code = _lib.MGR_F32 if p.dtype == np.float32 else _lib.MGR_F64
     rbd = d.dtype.itemsize * int(np.prod(d.shape[1:], dtype=np.int64))
-    ov_d, ov_p, m = exchange_overload(R, transport, _flat(d), rbd, _flat(p), p.shape[1], code,
-                                      len(d), list(f["overload"]), periodic=periodic,
-                                      sel=CpuSelect())
+    rbp = p.dtype.itemsize * p.shape[1]
+    n = len(d)
+    d_flat, p_flat, arena = _flat(d), _flat(p), None
+    if spare is not None:
+        st_d = torch.full(((n + spare) * rbd,), 0xA5, dtype=torch.uint8)
+        st_p = torch.full(((n + spare) * rbp,), 0x5A, dtype=torch.uint8)
+        st_d[: n * rbd].copy_(d_flat)
+        st_p[: n * rbp].copy_(p_flat)
+        d_flat, p_flat, arena = st_d[: n * rbd], st_p[: n * rbp], (st_d, st_p, n, spare)
+    ov_d, ov_p, m, in_arena = exchange_overload(R, transport, d_flat, rbd, p_flat, p.shape[1],
+                                                code, n, list(f["overload"]), periodic=periodic,
+                                                sel=CpuSelect(), arena=arena)
+    if spare is not None:
+        assert in_arena == (m <= spare), (m, spare, in_arena)
+        assert torch.equal(st_d[: n * rbd], _flat(d)), "the local rows were overwritten"
+        if in_arena and periodic:
+            whole = st_d[: (n + m) * rbd].numpy().view(d.dtype).reshape((n + m,) + d.shape[1:])
+            assert np.array_equal(st_p[n * rbp:(n + m) * rbp].numpy(), ov_p.numpy())
+            return whole
     ov = ov_d.numpy().view(d.dtype).reshape((m,) + d.shape[1:])
     return np.concatenate([d, ov]) if periodic else ov
 
@@ -137,6 +156,20 @@ def test_threaded_halo(case):
                      if size > 1 else run_rank(f, case, _SelfT(), r))
     for r in range(size):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
+
+
+@pytest.mark.parametrize("spare", [0, 3, 40, 10**6])
+@pytest.mark.parametrize("case", ["halo_p8_f64_rec32.npz", "halo_p1_self.npz",
+                                  "halo_direct_p8_nonperiodic.npz"])
+def test_threaded_halo_in_place(case, spare):
+    """The halo rows appended in place after the local rows (the arena that
+    redistribute_by_position passes), fitting or outgrowing the spare rows."""
+    f = G.load(case)
+    size = int(f["size"])
+    outs = run_ranks(size, lambda comm, r: run_rank(f, case, MpiHostComm(comm), r, spare)
+                     if size > 1 else run_rank(f, case, _SelfT(), r, spare))
+    for r in range(size):
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r, spare)
 
 
 class _SelfT:
