@@ -172,6 +172,15 @@ int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride
                    const double* hi, const double* lo, uint16_t* flags, void* stream);
 int mgr_select_count(const uint16_t* flags, int64_t n, int mask, void* dest, int tile_rows,
                      void* workspace, void* stream);
+/* mgr_select_pack2: the selection of mgr_select_count + mgr_scan applied to
+ * two fields of the same n rows in one pass (the payload rows and their
+ * position rows, redist.py:274-275 / :164), = mgr_pack(src1, rb1, ..., 2,
+ * 1, ...) then mgr_pack(src2, rb2, ...).  Fused for 16-byte-aligned rows of
+ * <= 64 bytes with 24-byte (f64) or 12-byte (f32) position rows; other
+ * shapes run the two packs.                                                 */
+int mgr_select_pack2(const void* src1, int64_t row_bytes1, void* dst1, const void* src2,
+                     int64_t row_bytes2, void* dst2, int64_t n, const void* dest, int tile_rows,
+                     const void* workspace, void* stream);
 
 /* ------------------------------------------------------------ exchange --
  * Replaces comm.alltoall(send_buff) + np.concatenate (redist.py:199):

@@ -46,6 +46,7 @@ SIGNATURES = {
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
     "mgr_halo_flags": (_I, [_P, _I, _I64, _I64, _I, _P, _P, _P, _P]),
     "mgr_select_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
+    "mgr_select_pack2": (_I, [_P, _I64, _P, _P, _I64, _P, _I64, _P, _I, _P, _P]),
     "mgr_comm_unique_id": (_I, [_P]),
     "mgr_comm_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
     "mgr_comm_destroy": (_I, [_P]),

@@ -345,6 +345,21 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
 }
 
 // ------------------------------------------------------ halo (f1)
+int mgr_select_pack2(const void* src1, int64_t row_bytes1, void* dst1, const void* src2,
+                     int64_t row_bytes2, void* dst2, int64_t n, const void* dest, int tile_rows,
+                     const void* workspace, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (row_bytes1 < 1 || row_bytes2 < 1)
+        return fail(MGR_EINVAL, "row_bytes %lld / %lld", (long long)row_bytes1, (long long)row_bytes2);
+    if (n > 0 && (!src1 || !src2 || !dst1 || !dst2 || !dest || !workspace))
+        return fail(MGR_EINVAL, "null argument");
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, 2, tile_rows);
+    HIP_OK(mgr::launch_select_pack2(src1, row_bytes1, dst1, src2, row_bytes2, dst2, n, dest,
+                                    tile_rows, ws, (hipStream_t)stream));
+    return MGR_OK;
+}
+
 int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
                    const double* hi, const double* lo, uint16_t* flags, void* stream) {
     if (pos_dtype != MGR_F32 && pos_dtype != MGR_F64)

@@ -80,6 +80,9 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
+hipError_t launch_select_pack2(const void* src1, int64_t rb1, void* dst1, const void* src2,
+                               int64_t rb2, void* dst2, int64_t n, const void* dest,
+                               int tile_rows, const Workspace& ws, hipStream_t s);
 hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
 hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,

@@ -313,6 +313,127 @@ __global__ __launch_bounds__(256) void compact_kernel(
     }
 }
 
+// One batch of D rounds of a compaction for one field: unit-transposed
+// unconditional loads (dropped rows read the tile's first unit), kept units
+// stored to their slots from base.
+template <int W, int UPR, int D>
+__device__ __forceinline__ void compact_batch(const typename Unit<W>::T* __restrict__ s_u,
+                                              typename Unit<W>::T* __restrict__ d_u,
+                                              const unsigned long long (&m)[D], int r0,
+                                              long long base, int lane) {
+    using U = typename Unit<W>::T;
+    U v[D][UPR];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane, r = u / UPR;
+            const int64_t idx = ((m[q] >> r) & 1ull) ? (int64_t)(r0 + 64 * q) * UPR + u : 0;
+            v[q][k] = s_u[idx];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+#pragma unroll
+        for (int k = 0; k < UPR; ++k) {
+            const int u = 64 * k + lane, r = u / UPR, part = u - r * UPR;
+            if ((m[q] >> r) & 1ull) {
+                const long long slot = base + __popcll(m[q] & ((1ull << r) - 1ull));
+                d_u[slot * UPR + part] = v[q][k];
+            }
+        }
+        base += __popcll(m[q]);
+    }
+}
+
+// Two fields under one selection (the halo's payload rows and their position
+// rows, redist.py:271-275 applied to data and position alike): the dest bytes
+// are read and balloted once, both fields' kept rows copied in the same pass.
+template <int W1, int U1, int W2, int U2>
+__global__ __launch_bounds__(256) void compact2_kernel(
+    const uint8_t* __restrict__ src1, uint8_t* __restrict__ dst1,
+    const uint8_t* __restrict__ src2, uint8_t* __restrict__ dst2, int64_t n,
+    const uint8_t* __restrict__ dest, const int64_t* __restrict__ offsets, int64_t T,
+    int tile_rows) {
+    constexpr int D = 4;
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
+    if (tile >= T) return;
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    long long base = offsets[tile];
+    const auto* s1 = (const typename Unit<W1>::T*)src1 + row0 * U1;
+    const auto* s2 = (const typename Unit<W2>::T*)src2 + row0 * U2;
+    auto* d1 = (typename Unit<W1>::T*)dst1;
+    auto* d2 = (typename Unit<W2>::T*)dst2;
+    unsigned nb_[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+        const int r = 64 * q + lane;
+        nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
+    }
+    for (int r0 = 0; r0 < rows; r0 += 64 * D) {
+        unsigned long long m[D];
+        long long kept = 0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            m[q] = __ballot(nb_[q] == 0u);
+            kept += __popcll(m[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const int r = r0 + 64 * (D + q) + lane;
+            nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
+        }
+        if (kept) {
+            compact_batch<W1, U1, D>(s1, d1, m, r0, base, lane);
+            compact_batch<W2, U2, D>(s2, d2, m, r0, base, lane);
+        }
+        base += kept;
+    }
+}
+
+// Unit shape (W bytes, U units per row) of a compaction field; 0 if none of
+// the fused kernel's instantiations fits.
+static int compact2_shape(uintptr_t a, int64_t row_bytes, int* W) {
+    if ((a & 15) == 0 && row_bytes <= 64) { *W = 16; return (int)(row_bytes / 16); }
+    if ((a & 7) == 0 && row_bytes == 24) { *W = 8; return 3; }
+    if ((a & 3) == 0 && row_bytes == 12) { *W = 4; return 3; }
+    return 0;
+}
+
+hipError_t launch_select_pack2(const void* src1, int64_t rb1, void* dst1, const void* src2,
+                               int64_t rb2, void* dst2, int64_t n, const void* dest,
+                               int tile_rows, const Workspace& ws, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int w1 = 0, w2 = 0;
+    const int u1 = compact2_shape((uintptr_t)src1 | (uintptr_t)dst1 | (uintptr_t)rb1, rb1, &w1);
+    const int u2 = compact2_shape((uintptr_t)src2 | (uintptr_t)dst2 | (uintptr_t)rb2, rb2, &w2);
+    const dim3 grid((unsigned)((ws.T + 3) / 4));
+    auto go = [&](auto k) {
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, (const uint8_t*)src1, (uint8_t*)dst1,
+                           (const uint8_t*)src2, (uint8_t*)dst2, n, (const uint8_t*)dest,
+                           ws.offsets, ws.T, tile_rows);
+        return hipGetLastError();
+    };
+    if (g_tune.pack_compact && w1 == 16 && u1 >= 1 && u1 <= 4 && u2 == 3 && (w2 == 8 || w2 == 4)) {
+        prof_begin(s, K_PACK);
+        hipError_t e = hipErrorNotSupported;
+#define MGR_C2(U1_)                                                                  \
+    case U1_:                                                                        \
+        e = w2 == 8 ? go(compact2_kernel<16, U1_, 8, 3>) : go(compact2_kernel<16, U1_, 4, 3>); \
+        break;
+        switch (u1) { MGR_C2(1) MGR_C2(2) MGR_C2(3) MGR_C2(4) default: break; }
+#undef MGR_C2
+        prof_end(s, K_PACK);
+        if (e != hipErrorNotSupported) return e;
+    }
+    // other shapes: one selection pack per field
+    hipError_t e = launch_pack(src1, rb1, n, dest, 2, 1, tile_rows, ws, dst1, -1, nullptr, s);
+    if (e != hipSuccess) return e;
+    return launch_pack(src2, rb2, n, dest, 2, 1, tile_rows, ws, dst2, -1, nullptr, s);
+}
+
 // Rows of any width: one lane copies one kept row.
 template <int W>
 __global__ __launch_bounds__(256) void compact_any_kernel(

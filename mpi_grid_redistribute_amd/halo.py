@@ -114,6 +114,13 @@ class DeviceSelect:
         _lib.call("mgr_pack", _lib.ptr(src_flat), row_bytes, n, _lib.ptr(dest), 2, 1, tile_rows,
                   _lib.ptr(ws), _lib.ptr(dst_flat), -1, None, _lib.stream_handle())
 
+    def pack2(self, handle, src1, rb1, dst1, src2, rb2, dst2):
+        """Both fields of the selection in one pass (mgr_select_pack2)."""
+        n, dest, ws, tile_rows = handle
+        _lib.call("mgr_select_pack2", _lib.ptr(src1), rb1, _lib.ptr(dst1), _lib.ptr(src2), rb2,
+                  _lib.ptr(dst2), n, _lib.ptr(dest), tile_rows, _lib.ptr(ws),
+                  _lib.stream_handle())
+
 
 def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n,
                       overload_lengths, periodic=True, sel=None, arena=None):
@@ -165,6 +172,8 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
             o = 0
             for (h, _, dd, pp), c in zip(picks, cs):
                 if c:
+                    # two selection packs: the fused one (sel.pack2) measured
+                    # no faster (sparse rows cost a line each either way)
                     sel.pack(h, dd, rbd, bd[o * rbd:])
                     sel.pack(h, pp, rbp, bp[o * rbp:])
                 o += c

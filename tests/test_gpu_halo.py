@@ -163,3 +163,39 @@ def test_halo_in_place_and_overflow(clustered):
             ro.Geometry(topo, box, size, s), pos_o[s].copy()) == r)) for s in range(size))
         fits.append(len(got) - own <= halo_capacity(R, own, ol))
     assert all(fits) if not clustered else not any(fits)
+
+
+@pytest.mark.parametrize("compact", [1, 0])
+@pytest.mark.parametrize("rb1,rb2", [(32, 24), (16, 12), (48, 24), (64, 12), (36, 12), (32, 16)])
+@pytest.mark.parametrize("n,frac", [(1, 1.0), (4095, 0.1), (4097, 0.5), (300001, 0.07),
+                                    (1 << 20, 0.0), (1 << 20, 1.0)])
+def test_select_pack2(n, frac, rb1, rb2, compact):
+    """mgr_select_pack2 (fused two-field selection pack, the fused kernel or
+    its two-pack fallback for other row shapes) = data[sel], pos[sel] in
+    order, the selection the halo takes per direction (redist.py:271-275)."""
+    from mpi_grid_redistribute_amd import _lib
+    from mpi_grid_redistribute_amd.halo import DeviceSelect
+    rng = np.random.default_rng(n + rb1 * 7 + rb2)
+    flags = (rng.random(n) < frac).astype(np.uint16) * 4 + rng.integers(0, 2, n).astype(np.uint16)
+    a = rng.integers(0, 256, (n, rb1), dtype=np.uint8)
+    b = rng.integers(0, 256, (n, rb2), dtype=np.uint8)
+    keep = (flags & 4) != 0
+    _lib.tune("pack_compact", compact)
+    try:
+        sel = DeviceSelect(torch.device("cuda"))
+        fl = torch.from_numpy(flags.view(np.int16)).cuda()
+        h, cnt = sel.select(fl, n, 4, max(rb1, rb2))
+        da = torch.from_numpy(a.reshape(-1)).cuda()
+        db = torch.from_numpy(b.reshape(-1)).cuda()
+        k = int(keep.sum())
+        oa = torch.full((max(k, 1) * rb1 + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+        ob = torch.full((max(k, 1) * rb2 + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+        sel.pack2(h, da, rb1, oa, db, rb2, ob)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == k
+        oa, ob = oa.cpu().numpy(), ob.cpu().numpy()
+        np.testing.assert_array_equal(oa[: k * rb1].reshape(k, rb1), a[keep])
+        np.testing.assert_array_equal(ob[: k * rb2].reshape(k, rb2), b[keep])
+        assert (oa[max(k, 1) * rb1:] == 0xAB).all() and (ob[max(k, 1) * rb2:] == 0xCD).all()
+    finally:
+        _lib.tune("pack_compact", 1)

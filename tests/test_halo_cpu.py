@@ -64,6 +64,10 @@ class CpuSelect:
         rows = src_flat.numpy().reshape(-1, row_bytes)[idx].reshape(-1)
         dst_flat[: rows.size].copy_(torch.from_numpy(rows.copy()))
 
+    def pack2(self, handle, src1, rb1, dst1, src2, rb2, dst2):
+        self.pack(handle, src1, rb1, dst1)
+        self.pack(handle, src2, rb2, dst2)
+
 
 def _flat(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy())
