@@ -87,3 +87,18 @@ def test_product_refuses_without_gpu():
         m.MPIGridRedistributor(None, [2], [1.0])
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m.GridPartitioner([2], [1.0])
+
+
+def test_select_pack2_validation(lib):
+    """mgr_select_pack2 argument checks run on the host before any launch."""
+    from mpi_grid_redistribute_amd import _lib
+    fn = lib.mgr_select_pack2
+    tr = _lib.SELECT_TILE_ROWS if hasattr(_lib, "SELECT_TILE_ROWS") else 4096
+    buf = ctypes.create_string_buffer(64)
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    assert fn(p, 0, p, p, 24, p, 1, p, tr, p, None) < 0          # row_bytes < 1
+    assert b"row_bytes" in lib.mgr_last_error()
+    assert fn(None, 32, p, p, 24, p, 5, p, tr, p, None) < 0      # null source with rows
+    assert b"null" in lib.mgr_last_error()
+    assert fn(p, 32, p, p, 24, p, 5, p, 100, p, None) < 0        # tile not a multiple of 64
+    assert fn(None, 32, None, None, 24, None, 0, None, tr, None, None) == 0  # empty: no-op
