@@ -126,7 +126,12 @@ int mgr_cell_number_from_indexes(const mgr_plan* plan, const int64_t* idx, int64
  * reference's send_buff[i] (redist.py:195-198).  Consumes what a count
  * producer (mgr_bin_count / mgr_bin_ids / mgr_select_count) left in the
  * workspace, including the zeroed one-pass scan words: one producer
- * launch precedes every scan on the same stream.                          */
+ * launch precedes every scan on the same stream.
+ * Failure: the scan never hangs the GPU.  If a look-back gives up (a chunk's
+ * predecessor never published, knob "scan_spins"), every bin_counts entry and
+ * bin_starts[nbins] become -1 and a flag in the workspace makes every later
+ * mgr_pack on this workspace write nothing -- the caller sees the failure at
+ * its count read instead of wrong offsets.                                */
 int mgr_scan(int64_t n, int nbins, int tile_rows, void* workspace, int64_t* bin_counts,
              void* stream);
 
@@ -136,7 +141,9 @@ int mgr_scan(int64_t n, int nbins, int tile_rows, void* workspace, int64_t* bin_
  * order kept inside each bin.  Rows of bin drop_bin (or -1: none) are not
  * written.  Rows of redirect_bin (or -1) are written to redirect_dst
  * starting at its row 0 instead (the self segment goes straight into the
- * caller's output).  Call once per field; all fields share dest/workspace. */
+ * caller's output), and the bins after it move up to close its gap in dst
+ * (dst then holds exactly the rows that travel, bin-major).  Call once per
+ * field; all fields share dest/workspace.                                  */
 int mgr_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
              int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
              void* redirect_dst, void* stream);
@@ -206,6 +213,23 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
                       const int64_t* row_bytes, const int64_t* send_counts,
                       const int64_t* send_offsets, const int64_t* recv_counts,
                       const int64_t* recv_offsets, int skip_self, void* stream);
+/* The operation list mgr_exchange_rows issues for rank `rank` of `size`, in
+ * issue order (host only, no GPU or communicator needed: the RCCL schedule
+ * is testable on a CPU).  Peers in ring order from rank+1 (sends to
+ * rank+j, receives from rank-j), fields in order within a peer; then the
+ * self-segment copies when !skip_self.  Writes at most max_ops entries to
+ * ops (may be NULL) and returns the total number of operations, < 0 on error.
+ * Offsets and sizes are in bytes: src_offset into send[field] (SEND, COPY),
+ * dst_offset into recv[field] (RECV, COPY).                                */
+enum { MGR_XOP_SEND = 0, MGR_XOP_RECV = 1, MGR_XOP_COPY = 2 };
+typedef struct {
+    int32_t kind, peer, field, reserved;
+    int64_t src_offset, dst_offset, bytes;
+} mgr_xop;
+int mgr_exchange_schedule(int rank, int size, int nfields, const int64_t* row_bytes,
+                          const int64_t* send_counts, const int64_t* send_offsets,
+                          const int64_t* recv_counts, const int64_t* recv_offsets, int skip_self,
+                          mgr_xop* ops, int max_ops);
 /* One isend/irecv pair of the halo exchange (redist.py:289-303): send
  * send_bytes to rank dest and receive recv_bytes from rank source, grouped
  * (ncclSend + ncclRecv); dest == source == me is a device copy.  Sizes must
@@ -225,21 +249,22 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
 
 /* -------------------------------------------------------------- tuning --
  * Kernel-variant knobs for A/B measurement: "bin_staged", "bin_skip_clean",
- * "bin_depth", "bin_waves", "xcd_bin", "pack_small", "pack_coop",
- * "pack_sorted", "pack_nt", "pack_rpw", "xcd_pack", "tile_rounds",
- * "scan_onepass", "scan_chunk", "scan_max_chunks", "pack_img", "many_super",
- * and "prof_mask" (bit k: time profiler kernel id k, in the
- * order of the names listed under profiling below; default all)
+ * "bin_waves", "xcd_bin", "pack_coop", "pack_nt", "pack_rpw", "xcd_pack",
+ * "tile_rounds", "scan_chunk", "scan_max_chunks", "pack_img", "pack_sel",
+ * "pack_compact", "pack_many", "many_super", "many_rows", "scan_spins" (polls
+ * per look-back word before the scan gives up; -1 gives up at once, for
+ * tests of the failure path) and "prof_mask" (bit k: time profiler kernel id
+ * k, in the order of the names listed under profiling below; default all)
  * (mgr_internal.h Tune); the defaults are the shipped configuration.
- * Process-wide, not thread-safe against concurrent launches.             */
+ * Process-wide: call between launches, not concurrently with them.        */
 int mgr_tune(const char* key, int64_t value);
 
 /* ----------------------------------------------------------- profiling --
  * Per-kernel HIP-event timing of every launch made while enabled, on the
  * launch's own stream.  mgr_profile_read synchronises those events and
  * returns the accumulated device time (ms) and launch count of the named
- * kernel ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack",
- * "cell_ids", "bin_ids", "cellnum_idx", "synth", "halo") or of the RCCL
+ * kernel ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx",
+ * "synth", "halo") or of the RCCL
  * grouped row exchange ("exchange").                                               */
 int mgr_profile_enable(int on);
 int mgr_profile_reset(void);

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mgr_comm_size": (_I, [_P]),
     "mgr_exchange_counts": (_I, [_P, _P, _P, _P]),
     "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
+    "mgr_exchange_schedule": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I]),
     "mgr_sendrecv": (_I, [_P, _P, _I64, _I, _P, _I64, _I, _P]),
     "mgr_comm_allreduce_max_f64": (_I, [_P, _P, _P, _I64, _P]),
     "mgr_synth_uniform": (_I, [ctypes.c_uint64, _I64, _I64, _I, _P, _P, _P, _P]),
@@ -67,6 +68,32 @@ SIGNATURES = {
 
 class MgrError(RuntimeError):
     """A libmgr.so call returned a negative status."""
+
+
+MGR_XOP_SEND, MGR_XOP_RECV, MGR_XOP_COPY = 0, 1, 2
+
+
+class XOp(ctypes.Structure):
+    """mgr_xop: one operation of a row exchange (include/mgr.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("field", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("src_offset", ctypes.c_int64),
+                ("dst_offset", ctypes.c_int64), ("bytes", ctypes.c_int64)]
+
+
+def exchange_schedule(rank, size, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets, skip_self=True):
+    """The RCCL operation list mgr_exchange_rows issues (host only, no GPU):
+    [(kind, peer, field, src_offset, dst_offset, bytes), ...] in issue order."""
+    nf = len(row_bytes)
+    arr = lambda a, k: (ctypes.c_int64 * k)(*[int(x) for x in a])  # noqa: E731
+    args = (int(rank), int(size), nf, arr(row_bytes, nf), arr(send_counts, size),
+            arr(send_offsets, size), arr(recv_counts, size), arr(recv_offsets, size),
+            int(bool(skip_self)))
+    n = load().mgr_exchange_schedule(*args, None, 0)
+    check(min(n, 0), "mgr_exchange_schedule")
+    ops = (XOp * max(n, 1))()
+    check(min(load().mgr_exchange_schedule(*args, ops, n), 0), "mgr_exchange_schedule")
+    return [(o.kind, o.peer, o.field, o.src_offset, o.dst_offset, o.bytes) for o in ops[:n]]
 
 
 _lib = None
@@ -125,8 +152,8 @@ def tune(key, value):
 
 # --------------------------------------------------------------- profiler
 # Profiler kernel names (mgr_internal.h KernelId).
-PROFILE_KERNELS = ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack",
-                   "cell_ids", "bin_ids", "cellnum_idx", "synth", "exchange", "halo")
+PROFILE_KERNELS = ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx", "synth",
+                   "exchange", "halo")
 
 
 def profile_enable(on=True):

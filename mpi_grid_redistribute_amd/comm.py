@@ -40,6 +40,17 @@ def excl_cumsum(counts):
     return out
 
 
+def row_exchange_arrays(size, row_bytes, send_counts, send_offsets, recv_counts, recv_offsets):
+    """The host arrays RcclComm hands to mgr_exchange_rows / mgr_exchange_schedule
+    after the field pointers: (row_bytes[nf], send_counts, send_offsets,
+    recv_counts, recv_offsets, skip_self=1) -- the pack already wrote the self
+    segment into the output (exchange.py)."""
+    I64 = ctypes.c_int64
+    arr = lambda a: (I64 * size)(*[int(x) for x in a])  # noqa: E731
+    return ((I64 * len(row_bytes))(*[int(x) for x in row_bytes]), arr(send_counts),
+            arr(send_offsets), arr(recv_counts), arr(recv_offsets), 1)
+
+
 class Transport:
     """Interface.  ``skips_self`` True means the transport never touches the
     self segment, so the pack may write it straight into the output."""
@@ -152,13 +163,12 @@ class RcclComm(Transport):
                       recv_offsets):
         nf = len(sends)
         P = ctypes.c_void_p * nf
-        I64 = ctypes.c_int64
         sp = P(*[s.data_ptr() for s in sends])
         rp = P(*[o.data_ptr() for o in outs])
-        rb = (I64 * nf)(*row_bytes)
-        arr = lambda a: (I64 * self.size)(*[int(x) for x in a])  # noqa: E731
-        _lib.call("mgr_exchange_rows", self._h, nf, sp, rp, rb, arr(send_counts),
-                  arr(send_offsets), arr(recv_counts), arr(recv_offsets), 1, _lib.stream_handle())
+        _lib.call("mgr_exchange_rows", self._h, nf, sp, rp,
+                  *row_exchange_arrays(self.size, row_bytes, send_counts, send_offsets,
+                                       recv_counts, recv_offsets),
+                  _lib.stream_handle())
 
     def sendrecv(self, send, dest, recv, source):
         _lib.call("mgr_sendrecv", self._h, _lib.ptr(send), send.numel(), int(dest),

@@ -230,10 +230,10 @@ __global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t*
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    // nontemporal slab loads/stores always (every A/B favoured them); one or
-    // two slabs in flight per wave (deeper measured no faster)
-    auto k = g_tune.bin_depth >= 2 ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 2>
-                                   : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>;
+    // nontemporal slab loads/stores always (every A/B favoured them); one
+    // slab in flight per wave (two measured slower with the write-back,
+    // DESIGN.md §3.3)
+    auto k = bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
     int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each

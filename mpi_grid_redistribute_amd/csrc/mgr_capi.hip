@@ -93,8 +93,7 @@ void collect_locked() {
 }  // namespace
 
 const char* kernel_name(int k) {
-    static const char* names[K_NUM_KERNELS] = {"bin_count", "scan", "scan_reduce", "scan_apply",
-                                               "bin_totals", "pack", "cell_ids",
+    static const char* names[K_NUM_KERNELS] = {"bin_count", "scan", "pack", "cell_ids",
                                                "bin_ids", "cellnum_idx", "synth",
                                                "exchange", "halo"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
@@ -422,17 +421,87 @@ int mgr_comm_destroy(mgr_comm* comm) {
 int mgr_comm_rank(const mgr_comm* comm) { return comm ? comm->rank : -1; }
 int mgr_comm_size(const mgr_comm* comm) { return comm ? comm->size : -1; }
 
+// An RCCL group that always closes: the first failing call inside it is
+// remembered and ncclGroupEnd still runs, so a failure never leaves the
+// calling thread inside an open group (later RCCL calls would misbehave).
+namespace {
+struct Group {
+    ncclResult_t first = ncclSuccess;
+    const char* what = nullptr;
+    int line = 0;
+    void run(ncclResult_t r, const char* expr, int ln) {
+        if (r != ncclSuccess && first == ncclSuccess) {
+            first = r;
+            what = expr;
+            line = ln;
+        }
+    }
+    int end() {
+        const ncclResult_t r = ncclGroupEnd();
+        if (first != ncclSuccess)
+            return fail(MGR_ERCCL, "%s: %s (%s:%d)", what, ncclGetErrorString(first), __FILE__, line);
+        if (r != ncclSuccess) return fail(MGR_ERCCL, "ncclGroupEnd: %s", ncclGetErrorString(r));
+        return MGR_OK;
+    }
+};
+}  // namespace
+#define GROUP_CALL(g, expr) (g).run((expr), #expr, __LINE__)
+
 int mgr_exchange_counts(mgr_comm* comm, const int64_t* send_counts, int64_t* recv_counts,
                         void* stream) {
     if (!comm || !send_counts || !recv_counts) return fail(MGR_EINVAL, "null argument");
     hipStream_t s = (hipStream_t)stream;
     NCCL_OK(ncclGroupStart());
+    Group g;
     for (int p = 0; p < comm->size; ++p) {
-        NCCL_OK(ncclSend(send_counts + p, 1, ncclInt64, p, comm->nccl, s));
-        NCCL_OK(ncclRecv(recv_counts + p, 1, ncclInt64, p, comm->nccl, s));
+        GROUP_CALL(g, ncclSend(send_counts + p, 1, ncclInt64, p, comm->nccl, s));
+        GROUP_CALL(g, ncclRecv(recv_counts + p, 1, ncclInt64, p, comm->nccl, s));
     }
-    NCCL_OK(ncclGroupEnd());
-    return MGR_OK;
+    return g.end();
+}
+
+// The operation list of one row exchange (what mgr_exchange_rows issues, in
+// that order).  Peers are visited in ring order starting after me -- to =
+// me + j, from = me - j -- so the first wave of transfers of all ranks uses
+// distinct xGMI links; per peer pair the sends of one side and the receives
+// of the other come in the same field order, as RCCL matches them.
+int mgr_exchange_schedule(int rank, int size, int nfields, const int64_t* row_bytes,
+                          const int64_t* send_counts, const int64_t* send_offsets,
+                          const int64_t* recv_counts, const int64_t* recv_offsets, int skip_self,
+                          mgr_xop* ops, int max_ops) {
+    if (size < 1 || rank < 0 || rank >= size) return fail(MGR_EINVAL, "rank %d of %d", rank, size);
+    if (nfields < 1 || !row_bytes || !send_counts || !send_offsets || !recv_counts || !recv_offsets)
+        return fail(MGR_EINVAL, "null argument");
+    for (int p = 0; p < size; ++p)
+        if (send_counts[p] < 0 || recv_counts[p] < 0 || send_offsets[p] < 0 || recv_offsets[p] < 0)
+            return fail(MGR_EINVAL, "negative count/offset for peer %d", p);
+    for (int f = 0; f < nfields; ++f)
+        if (row_bytes[f] < 1) return fail(MGR_EINVAL, "row_bytes[%d] = %lld", f, (long long)row_bytes[f]);
+    int k = 0;
+    auto put = [&](int kind, int peer, int f, int64_t src, int64_t dst, int64_t bytes) {
+        if (ops && k < max_ops) ops[k] = mgr_xop{kind, peer, f, 0, src, dst, bytes};
+        ++k;
+    };
+    for (int j = 1; j < size; ++j) {
+        const int to = (rank + j) % size;
+        const int from = (rank - j + size) % size;
+        for (int f = 0; f < nfields; ++f) {
+            const int64_t rb = row_bytes[f];
+            if (send_counts[to] > 0)
+                put(MGR_XOP_SEND, to, f, send_offsets[to] * rb, -1, send_counts[to] * rb);
+            if (recv_counts[from] > 0)
+                put(MGR_XOP_RECV, from, f, -1, recv_offsets[from] * rb, recv_counts[from] * rb);
+        }
+    }
+    if (!skip_self && send_counts[rank] > 0) {
+        if (recv_counts[rank] != send_counts[rank])
+            return fail(MGR_EINVAL, "self segment: %lld rows sent, %lld expected",
+                        (long long)send_counts[rank], (long long)recv_counts[rank]);
+        for (int f = 0; f < nfields; ++f)
+            put(MGR_XOP_COPY, rank, f, send_offsets[rank] * row_bytes[f],
+                recv_offsets[rank] * row_bytes[f], send_counts[rank] * row_bytes[f]);
+    }
+    return k;
 }
 
 int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void* const* recv,
@@ -443,39 +512,36 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
         !recv_counts || !recv_offsets)
         return fail(MGR_EINVAL, "null argument");
     hipStream_t s = (hipStream_t)stream;
-    const int me = comm->rank;
-    bool any = false;
-    for (int p = 0; p < comm->size; ++p)
-        if (p != me && (send_counts[p] > 0 || recv_counts[p] > 0)) any = true;
-    if (any) {
+    const int nops = mgr_exchange_schedule(comm->rank, comm->size, nfields, row_bytes, send_counts,
+                                           send_offsets, recv_counts, recv_offsets, skip_self,
+                                           nullptr, 0);
+    if (nops < 0) return nops;
+    std::vector<mgr_xop> ops((size_t)nops);
+    mgr_exchange_schedule(comm->rank, comm->size, nfields, row_bytes, send_counts, send_offsets,
+                          recv_counts, recv_offsets, skip_self, ops.data(), nops);
+    bool p2p = false;
+    for (const mgr_xop& o : ops) p2p |= o.kind != MGR_XOP_COPY;
+    if (p2p) {
         mgr::prof_begin(s, mgr::K_EXCHANGE);
         NCCL_OK(ncclGroupStart());
-        // Peers in ring order starting after me spread the first wave of
-        // transfers over distinct xGMI links.
-        for (int j = 1; j < comm->size; ++j) {
-            const int to = (me + j) % comm->size;
-            const int from = (me - j + comm->size) % comm->size;
-            for (int f = 0; f < nfields; ++f) {
-                const int64_t rb = row_bytes[f];
-                if (send_counts[to] > 0)
-                    NCCL_OK(ncclSend((const char*)send[f] + send_offsets[to] * rb,
-                                     (size_t)(send_counts[to] * rb), ncclUint8, to, comm->nccl, s));
-                if (recv_counts[from] > 0)
-                    NCCL_OK(ncclRecv((char*)recv[f] + recv_offsets[from] * rb,
-                                     (size_t)(recv_counts[from] * rb), ncclUint8, from, comm->nccl, s));
-            }
+        Group g;
+        for (const mgr_xop& o : ops) {
+            if (o.kind == MGR_XOP_SEND)
+                GROUP_CALL(g, ncclSend((const char*)send[o.field] + o.src_offset, (size_t)o.bytes,
+                                       ncclUint8, o.peer, comm->nccl, s));
+            else if (o.kind == MGR_XOP_RECV)
+                GROUP_CALL(g, ncclRecv((char*)recv[o.field] + o.dst_offset, (size_t)o.bytes,
+                                       ncclUint8, o.peer, comm->nccl, s));
         }
-        NCCL_OK(ncclGroupEnd());
+        const int rc = g.end();
         mgr::prof_end(s, mgr::K_EXCHANGE);
+        if (rc) return rc;
     }
-    if (!skip_self && send_counts[me] > 0) {
-        for (int f = 0; f < nfields; ++f) {
-            const int64_t rb = row_bytes[f];
-            HIP_OK(hipMemcpyAsync((char*)recv[f] + recv_offsets[me] * rb,
-                                  (const char*)send[f] + send_offsets[me] * rb,
-                                  (size_t)(send_counts[me] * rb), hipMemcpyDeviceToDevice, s));
-        }
-    }
+    for (const mgr_xop& o : ops)
+        if (o.kind == MGR_XOP_COPY)
+            HIP_OK(hipMemcpyAsync((char*)recv[o.field] + o.dst_offset,
+                                  (const char*)send[o.field] + o.src_offset, (size_t)o.bytes,
+                                  hipMemcpyDeviceToDevice, s));
     return MGR_OK;
 }
 
@@ -494,10 +560,10 @@ int mgr_sendrecv(mgr_comm* comm, const void* send, int64_t send_bytes, int dest,
         return MGR_OK;
     }
     NCCL_OK(ncclGroupStart());
-    if (send_bytes > 0) NCCL_OK(ncclSend(send, (size_t)send_bytes, ncclUint8, dest, comm->nccl, s));
-    if (recv_bytes > 0) NCCL_OK(ncclRecv(recv, (size_t)recv_bytes, ncclUint8, source, comm->nccl, s));
-    NCCL_OK(ncclGroupEnd());
-    return MGR_OK;
+    Group g;
+    if (send_bytes > 0) GROUP_CALL(g, ncclSend(send, (size_t)send_bytes, ncclUint8, dest, comm->nccl, s));
+    if (recv_bytes > 0) GROUP_CALL(g, ncclRecv(recv, (size_t)recv_bytes, ncclUint8, source, comm->nccl, s));
+    return g.end();
 }
 
 int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,
@@ -522,7 +588,6 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
 int mgr_tune(const char* key, int64_t value) {
     if (!key) return fail(MGR_EINVAL, "null key");
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
-    else if (!strcmp(key, "pack_small")) mgr::g_tune.pack_small = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
     else if (!strcmp(key, "many_rows")) {
@@ -533,9 +598,7 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "bin_skip_clean")) mgr::g_tune.bin_skip_clean = (int)value;
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
-    else if (!strcmp(key, "pack_sorted")) mgr::g_tune.pack_sorted = (int)value;
     else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
-    else if (!strcmp(key, "scan_onepass")) mgr::g_tune.scan_onepass = (int)value;
     else if (!strcmp(key, "pack_img")) mgr::g_tune.pack_img = (int)value;
     else if (!strcmp(key, "pack_sel")) mgr::g_tune.pack_sel = (int)value;
     else if (!strcmp(key, "pack_compact")) mgr::g_tune.pack_compact = (int)value;
@@ -555,9 +618,9 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "pack_rpw")) {
         if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
         mgr::g_tune.pack_rpw = (int)value;
-    } else if (!strcmp(key, "bin_depth")) {
-        if (value < 1 || value > 2) return fail(MGR_EINVAL, "bin_depth %lld", (long long)value);
-        mgr::g_tune.bin_depth = (int)value;
+    } else if (!strcmp(key, "scan_spins")) {
+        if (value < -1 || value > (1 << 30)) return fail(MGR_EINVAL, "scan_spins %lld", (long long)value);
+        mgr::g_tune.scan_spins = (int)value;
     } else if (!strcmp(key, "bin_waves")) {
         if (value < 1 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);
         mgr::g_tune.bin_waves = (int)value;

@@ -231,28 +231,63 @@ __device__ __forceinline__ long long block_excl_scan(long long v, long long* tot
 }
 
 // ------------------------------------------------- one-pass scan words
-constexpr uint64_t kScanAgg = 1ull << 62, kScanInc = 2ull << 62, kScanVal = (1ull << 62) - 1;
+// Word layout: bits 62-63 status (0 none, 1 aggregate, 2 inclusive prefix),
+// bit 61 poison (the value rests on a look-back that timed out), bits 0-60
+// the count.  Behind the kScanFlags words the scan keeps its control words
+// (ScanCtl), zeroed with them by every count producer.
+constexpr uint64_t kScanAgg = 1ull << 62, kScanInc = 2ull << 62, kScanPoison = 1ull << 61,
+                   kScanVal = (1ull << 61) - 1;
 
 __device__ __forceinline__ void clear_scan_flags(uint64_t* __restrict__ flags) {
     const int64_t step = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kScanFlags; i += step)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kScanFlags + kScanCtlWords;
+         i += step)
         flags[i] = 0;
+}
+
+__device__ __forceinline__ ScanCtl* scan_ctl(uint64_t* flags) {
+    return (ScanCtl*)(flags + kScanFlags);
 }
 
 __device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Poll until the word's status reaches `need` (bounded: a lost producer
-// would yield a wrong scan, never a hung GPU).
-__device__ __forceinline__ uint64_t flag_poll(uint64_t* p, uint64_t need) {
+// Poll until the word's status reaches `need`, at most `spins` times (a
+// lost producer must not hang the GPU).  On exhaustion the stale word is
+// returned with the poison bit set, so everything computed from it is
+// marked; spins < 0 gives up at once (test knob scan_spins).
+__device__ __forceinline__ uint64_t flag_poll(uint64_t* p, uint64_t need, int spins) {
     uint64_t w = 0;
-    for (int spin = 0; spin < (1 << 24); ++spin) {
-        w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((w >> 62) >= need) break;
+    for (int spin = 0;; ++spin) {
+        if (spins >= 0) w = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (spins >= 0 && (w >> 62) >= need) return w;
+        if (spin >= spins) return (w & ~(3ull << 62)) | (need << 62) | kScanPoison;
         __builtin_amdgcn_s_sleep(1);
     }
-    return w;
+}
+
+// Segment start of bin b's rows of tile `tile` in a pack's output: the
+// scan's offset; the redirect bin's rows go to redirect_dst from its row 0
+// (minus the bin's start), and the bins after it close the gap it leaves
+// (minus its size), so the packed send buffer holds exactly the rows that
+// travel (mgr_pack, include/mgr.h).
+__device__ __forceinline__ long long seg_start(const int64_t* __restrict__ offsets,
+                                               const int64_t* __restrict__ bin_starts, int64_t T,
+                                               int64_t tile, int b, int redirect_bin) {
+    long long o = offsets[(int64_t)b * T + tile];
+    if (redirect_bin >= 0) {
+        if (b == redirect_bin) o -= bin_starts[b];
+        else if (b > redirect_bin) o -= bin_starts[redirect_bin + 1] - bin_starts[redirect_bin];
+    }
+    return o;
+}
+
+// A failed scan (ScanCtl::err, mgr_kernels.hip) leaves offsets that must
+// not be written through: every pack kernel checks it before its first
+// store (the word was written by an earlier kernel, a uniform read).
+__device__ __forceinline__ bool scan_failed(const uint32_t* __restrict__ scan_err) {
+    return scan_err && *scan_err != 0u;
 }
 
 // ------------------------------------------------------ wave-private tiles

@@ -13,8 +13,17 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kMaxTileRows = 65536;      // many-bin pack tiles (super-rounds of 4096 rows)
 constexpr int kCoopMaxRounds = 64;       // cooperative pack tiles <= 4096 rows
 constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
-constexpr int kScanMaxBlocks = 1024;      // two-pass scan (A/B knob scan_onepass = 0)
 constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups) at most
+
+// One-pass scan control words, right behind the kScanFlags chunk words and
+// zeroed with them by every count producer.
+struct ScanCtl {
+    uint32_t ticket;   // chunk ids in dispatch order (atomic ticket)
+    uint32_t done;     // chunks that have written their offsets
+    uint32_t err;      // nonzero: a look-back timed out; packs then write nothing
+    uint32_t pad;
+};
+constexpr int kScanCtlWords = sizeof(ScanCtl) / 8;
 
 // Geometry of one plan, passed to kernels by value (kernarg segment).
 struct Geom {
@@ -44,9 +53,9 @@ struct Workspace {
     int32_t* counts;     // [nbins][T] destination-major tile histogram
     int64_t* offsets;    // [nbins][T] exclusive scan of counts
     int64_t* bin_starts; // [nbins + 1]
-    int64_t* partials;   // [kScanMaxBlocks] (two-pass scan)
-    uint64_t* flags;     // [kScanFlags] one-pass scan chunk words; zeroed by the
-                         // count producers (bin_count, bin_ids, select_count)
+    uint64_t* flags;     // [kScanFlags] one-pass scan chunk words + ScanCtl; zeroed
+                         // by the count producers (bin_count, bin_ids, select_count)
+    const uint32_t* scan_err;  // &ScanCtl::err: packs return at once when set
     int64_t T;
 };
 int64_t num_tiles(int64_t n, int tile_rows);
@@ -56,8 +65,8 @@ int dest_bytes(int nbins);
 int nbits_for(int nbins);
 
 // Kernel ids for the profiler.
-enum KernelId { K_BIN_COUNT, K_SCAN, K_SCAN_REDUCE, K_SCAN_APPLY, K_BIN_TOTALS, K_PACK, K_CELL_IDS,
-                K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH, K_EXCHANGE, K_HALO, K_NUM_KERNELS };
+enum KernelId { K_BIN_COUNT, K_SCAN, K_PACK, K_CELL_IDS, K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH,
+                K_EXCHANGE, K_HALO, K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);
@@ -91,25 +100,23 @@ hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, 
 // Tuning knobs (mgr_tune); defaults are the shipped configuration.
 struct Tune {
     int bin_staged = 1;    // stage 64-row position slabs through LDS
-    int pack_small = 1;    // register-resident pack for <= 64 bins, <= 64-byte rows
     int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
     int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
     int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores (small/coop)
     int bin_skip_clean = 1;  // write a position slab back only if a row changed
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
     int xcd_pack = 1;      // ... in the pack kernels
-    int pack_sorted = 0;   // pack through an LDS image sorted by destination
     int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
-    int bin_depth = 1;     // position slabs in flight per bin wave (1 or 2)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
     int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
     int pack_compact = 1;  // selections (2 bins, bin 1 dropped): wave-per-tile compaction
     int pack_sel = 1;      // selection packs (2 bins, one dropped) load only kept rows
     int pack_img = 1;      // 16-byte-unit image pack for 4-byte-multiple rows (1: 24..60 B, 2: 12..60 B)
-    int scan_onepass = 1;  // one-pass decoupled look-back scan (0: reduce + apply + totals)
     int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)
     int scan_max_chunks = 1024;  // one-pass scan: at most this many chunks (look-back depth)
+    int scan_spins = 1 << 24;    // one-pass scan: polls per look-back word before giving up
+                                 // (-1: give up at once -- tests of the error path)
     int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)
     int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)
 };

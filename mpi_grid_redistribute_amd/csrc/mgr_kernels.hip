@@ -27,61 +27,23 @@ namespace mgr {
 Tune g_tune;
 
 // ------------------------------------------------------------------ scan
-__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const int32_t* __restrict__ counts,
-                                                             int64_t M, int64_t chunk,
-                                                             int64_t* __restrict__ partials) {
-    __shared__ long long s_w[kWaves];
-    const int64_t lo = blockIdx.x * chunk, hi = min(M, lo + chunk);
-    long long acc = 0;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) acc += counts[i];
-    long long tot;
-    block_excl_scan(acc, &tot, s_w);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(kBlock) void scan_apply_kernel(const int32_t* __restrict__ counts,
-                                                            int64_t M, int64_t chunk,
-                                                            const int64_t* __restrict__ partials,
-                                                            int64_t* __restrict__ offsets, int64_t T,
-                                                            int64_t* __restrict__ bin_starts,
-                                                            int nbins) {
-    __shared__ long long s_w[kWaves];
-    long long carry = 0;
-    for (int j = threadIdx.x; j < (int)blockIdx.x; j += kBlock) carry += partials[j];
-    long long tot;
-    block_excl_scan(carry, &tot, s_w);
-    carry = tot;
-    const int64_t lo = blockIdx.x * chunk, hi = min(M, lo + chunk);
-    for (int64_t base = lo; base < hi; base += kBlock) {
-        const int64_t i = base + threadIdx.x;
-        const long long v = (i < hi) ? counts[i] : 0;
-        const long long ex = block_excl_scan(v, &tot, s_w) + carry;
-        if (i < hi) {
-            offsets[i] = ex;
-            if (i % T == 0) bin_starts[i / T] = ex;
-        }
-        carry += tot;
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) bin_starts[nbins] = carry;
-}
-
-__global__ void bin_totals_kernel(const int64_t* __restrict__ bin_starts, int nbins,
-                                  int64_t* __restrict__ bin_counts) {
-    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x)
-        bin_counts[b] = bin_starts[b + 1] - bin_starts[b];
-}
-
 // One-pass scan (decoupled look-back).  Chunks never straddle a bin: chunk
 // j covers counts [b*T + c*chunk, b*T + min(T, (c+1)*chunk)) of bin b = j /
 // cpb, c = j % cpb, one workgroup each.  A chunk publishes its aggregate,
 // then wave 0 looks back 64 predecessors at a time until it meets one that
 // already published its inclusive prefix, publishes its own inclusive
 // prefix, and the workgroup writes the chunk's exclusive offsets.  Status
-// and value share one 64-bit word (bits 62-63: 0 none, 1 aggregate, 2
-// inclusive), stored and polled with agent-scope atomics (sc1, coherent
-// across the XCDs' L2s).  A chunk only waits on lower-numbered chunks, which
-// the in-order dispatch started earlier, so the waits always end; the count
-// producers zero the words (clear_scan_flags) before every scan.
+// and value share one 64-bit word (mgr_device.h), stored and polled with
+// agent-scope atomics (sc1, coherent across the XCDs' L2s).
+// Forward progress: a workgroup takes its chunk id j from an atomic ticket,
+// so chunks 0..j-1 were all taken by workgroups that are already running
+// (no assumption about dispatch order), and a chunk only waits on those.
+// Every poll is bounded; a look-back that gives up marks its words
+// poisoned, sets ScanCtl::err (every pack kernel then writes nothing), and
+// the chunk with the last ticket -- which waits until every other chunk is
+// done -- writes -1 into every bin count: the failure reaches the host at
+// the count read it already does, never as silently wrong offsets.
+// The count producers zero the words and ScanCtl (clear_scan_flags).
 // ITEMS consecutive counts per thread (a TILE of ITEMS * 256 per pass): a
 // chunk that fits one tile is read once, kept in registers, and scanned with
 // one block scan; longer chunks loop over tiles.
@@ -92,11 +54,20 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
                                                               uint64_t* __restrict__ flags,
                                                               int64_t* __restrict__ offsets,
                                                               int64_t* __restrict__ bin_starts,
-                                                              int64_t* __restrict__ bin_counts) {
+                                                              int64_t* __restrict__ bin_counts,
+                                                              int spins) {
     constexpr int TILE = ITEMS * kBlock;
     __shared__ long long s_w[kWaves];
     __shared__ long long s_excl;
-    const int j = blockIdx.x;
+    __shared__ int s_j, s_poison;
+    ScanCtl* ctl = scan_ctl(flags);
+    if (threadIdx.x == 0) {
+        s_j = (int)__hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        s_poison = 0;
+    }
+    __syncthreads();
+    const int j = s_j;
     const int b = j / cpb, c = j - b * cpb;
     const int64_t lo = (int64_t)b * T + (int64_t)c * chunk;
     const int64_t hi = (int64_t)b * T + min(T, (int64_t)(c + 1) * chunk);
@@ -118,25 +89,36 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         long long excl = 0;
+        uint64_t poison = 0;
         if (j == 0) {
             if (lane == 0) flag_store(&flags[0], kScanInc | (uint64_t)agg);
         } else {
             if (lane == 0) flag_store(&flags[j], kScanAgg | (uint64_t)agg);
             for (int base = j - 1;; base -= 64) {
                 const int idx = base - lane;
-                const uint64_t w = idx >= 0 ? flag_poll(&flags[idx], 1) : kScanInc;
+                // after a give-up, no more waiting: one look per word
+                const uint64_t w = idx >= 0 ? flag_poll(&flags[idx], 1, poison ? 0 : spins)
+                                            : kScanInc;
                 const unsigned long long inc = __ballot((w >> 62) >= 2);
                 long long x = (long long)(w & kScanVal);
                 // lanes up to the nearest predecessor with an inclusive prefix
-                if (inc && lane > __ffsll((long long)inc) - 1) x = 0;
+                const bool used = !(inc && lane > __ffsll((long long)inc) - 1);
+                if (!used) x = 0;
+                if (__ballot(used && (w & kScanPoison))) poison = kScanPoison;
 #pragma unroll
                 for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o, 64);
                 excl += x;
                 if (inc) break;
             }
-            if (lane == 0) flag_store(&flags[j], kScanInc | (uint64_t)(excl + agg));
+            if (lane == 0) flag_store(&flags[j], kScanInc | poison | (uint64_t)(excl + agg));
         }
-        if (lane == 0) s_excl = excl;
+        if (lane == 0) {
+            s_excl = excl;
+            if (poison) {
+                s_poison = 1;
+                __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
     __syncthreads();
     long long carry = s_excl;
@@ -167,20 +149,41 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
             carry += tot;
         }
     }
-    if (j == (int)gridDim.x - 1) {
-        // every bin's total from the inclusive prefixes at the bin ends
-        const long long total = s_excl + agg;
-        if (bin_counts) {
-            for (int bb = threadIdx.x; bb < nbins; bb += kBlock) {
-                const long long st = bb == 0 ? 0 : (long long)(flag_poll(&flags[bb * cpb - 1], 2) & kScanVal);
-                const long long en = bb == nbins - 1
-                                         ? total
-                                         : (long long)(flag_poll(&flags[(bb + 1) * cpb - 1], 2) & kScanVal);
-                bin_counts[bb] = en - st;
-            }
-        }
-        if (threadIdx.x == 0) bin_starts[nbins] = total;
+    __syncthreads();
+    if (j != (int)gridDim.x - 1) {
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
+    // The last ticket: wait until every other chunk is done (all of them hold
+    // earlier tickets, so they are running and their polls are bounded), then
+    // every bin's total from the inclusive prefixes at the bin ends -- or -1
+    // everywhere when any look-back gave up.
+    if (threadIdx.x == 0) {
+        const unsigned others = gridDim.x - 1;
+        int spin = 0;
+        while (__hip_atomic_load(&ctl->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < others) {
+            if (spins < 0 || ++spin > (1 << 26)) {   // a lost chunk: fail loudly
+                __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (__hip_atomic_load(&ctl->err, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) s_poison = 1;
+    }
+    __syncthreads();
+    const bool failed = s_poison != 0;
+    const long long total = s_excl + agg;
+    if (bin_counts) {
+        for (int bb = threadIdx.x; bb < nbins; bb += kBlock) {
+            const long long st = bb == 0 ? 0 : (long long)(flag_poll(&flags[bb * cpb - 1], 2, 0) & kScanVal);
+            const long long en = bb == nbins - 1
+                                     ? total
+                                     : (long long)(flag_poll(&flags[(bb + 1) * cpb - 1], 2, 0) & kScanVal);
+            bin_counts[bb] = failed ? -1 : en - st;
+        }
+    }
+    if (threadIdx.x == 0) bin_starts[nbins] = failed ? -1 : total;
 }
 
 // ---------------------------------------------------------- halo (f1)
@@ -307,8 +310,8 @@ static int64_t a256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
     const int64_t T = num_tiles(n, tile_rows);
     const int64_t M = (int64_t)nbins * (T > 0 ? T : 1);
-    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) + a256(kScanMaxBlocks * 8) +
-           a256(kScanFlags * 8);
+    return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) +
+           a256((kScanFlags + kScanCtlWords) * 8);
 }
 
 Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
@@ -319,56 +322,33 @@ Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
     ws.counts = (int32_t*)p;     p += a256(M * 4);
     ws.offsets = (int64_t*)p;    p += a256(M * 8);
     ws.bin_starts = (int64_t*)p; p += a256((nbins + 1) * 8);
-    ws.partials = (int64_t*)p;   p += a256(kScanMaxBlocks * 8);
     ws.flags = (uint64_t*)p;
+    ws.scan_err = &((const ScanCtl*)(ws.flags + kScanFlags))->err;
     return ws;
 }
 
 hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
                        int64_t* bin_counts, hipStream_t s) {
     if (n <= 0 || ws.T == 0) {
+        // no producer ran: clear the control words too (packs read err)
         hipError_t e = hipMemsetAsync(ws.bin_starts, 0, (size_t)(nbins + 1) * 8, s);
+        if (e == hipSuccess) e = hipMemsetAsync(ws.flags + kScanFlags, 0, sizeof(ScanCtl), s);
         if (e == hipSuccess && bin_counts) e = hipMemsetAsync(bin_counts, 0, (size_t)nbins * 8, s);
         return e;
     }
-    if (g_tune.scan_onepass) {
-        const int64_t target = g_tune.scan_chunk;         // counts per chunk (workgroup)
-        int64_t cpb = (ws.T + target - 1) / target;
-        int64_t cap = min((int64_t)g_tune.scan_max_chunks, (int64_t)kScanFlags) / nbins;
-        if (cap < 1) cap = 1;                             // nbins <= MGR_MAX_BINS = kScanFlags
-        if (cpb > cap) cpb = cap;
-        const int64_t chunk = (ws.T + cpb - 1) / cpb;
-        cpb = (ws.T + chunk - 1) / chunk;                 // no empty chunk
-        prof_begin(s, K_SCAN);
-        auto k = chunk <= 8 * kBlock ? scan_onepass_kernel<8> : scan_onepass_kernel<16>;
-        hipLaunchKernelGGL(k, dim3((unsigned)(nbins * cpb)), dim3(kBlock), 0, s,
-                           ws.counts, ws.T, chunk, (int)cpb, nbins, ws.flags, ws.offsets,
-                           ws.bin_starts, bin_counts);
-        prof_end(s, K_SCAN);
-        return hipGetLastError();
-    }
-    const int64_t M = (int64_t)nbins * ws.T;
-    int64_t G = (M + 2047) / 2048;
-    if (G > kScanMaxBlocks) G = kScanMaxBlocks;
-    if (G < 1) G = 1;
-    int64_t chunk = (M + G - 1) / G;
-    G = (M + chunk - 1) / chunk;
-    prof_begin(s, K_SCAN_REDUCE);
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)G), dim3(kBlock), 0, s, ws.counts, M,
-                       chunk, ws.partials);
-    prof_end(s, K_SCAN_REDUCE);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    prof_begin(s, K_SCAN_APPLY);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)G), dim3(kBlock), 0, s, ws.counts, M,
-                       chunk, ws.partials, ws.offsets, ws.T, ws.bin_starts, nbins);
-    prof_end(s, K_SCAN_APPLY);
-    e = hipGetLastError();
-    if (e != hipSuccess || !bin_counts) return e;
-    prof_begin(s, K_BIN_TOTALS);
-    hipLaunchKernelGGL(bin_totals_kernel, dim3((nbins + 255) / 256), dim3(256), 0, s,
-                       ws.bin_starts, nbins, bin_counts);
-    prof_end(s, K_BIN_TOTALS);
+    const int64_t target = g_tune.scan_chunk;         // counts per chunk (workgroup)
+    int64_t cpb = (ws.T + target - 1) / target;
+    int64_t cap = min((int64_t)g_tune.scan_max_chunks, (int64_t)kScanFlags) / nbins;
+    if (cap < 1) cap = 1;                             // nbins <= MGR_MAX_BINS = kScanFlags
+    if (cpb > cap) cpb = cap;
+    const int64_t chunk = (ws.T + cpb - 1) / cpb;
+    cpb = (ws.T + chunk - 1) / chunk;                 // no empty chunk
+    prof_begin(s, K_SCAN);
+    auto k = chunk <= 8 * kBlock ? scan_onepass_kernel<8> : scan_onepass_kernel<16>;
+    hipLaunchKernelGGL(k, dim3((unsigned)(nbins * cpb)), dim3(kBlock), 0, s, ws.counts, ws.T,
+                       chunk, (int)cpb, nbins, ws.flags, ws.offsets, ws.bin_starts, bin_counts,
+                       g_tune.scan_spins);
+    prof_end(s, K_SCAN);
     return hipGetLastError();
 }
 

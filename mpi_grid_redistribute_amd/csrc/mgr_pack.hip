@@ -19,18 +19,16 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
     const DestT* __restrict__ dest, int nb, int nbits, int drop_bin,
     const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts, int64_t T,
     int tile_rows, int per_wave_lds, uint8_t* __restrict__ dst, int redirect_bin,
-    uint8_t* __restrict__ redirect_dst) {
+    uint8_t* __restrict__ redirect_dst, const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
-    if (tile >= T) return;
+    if (tile >= T || scan_failed(scan_err)) return;
     int64_t* goff = (int64_t*)(smem + w * per_wave_lds);
     int32_t* run = (int32_t*)(smem + w * per_wave_lds + align16(nb * 8));
     for (int b = lane; b < nb; b += 64) {
-        int64_t o = offsets[(int64_t)b * T + tile];
-        if (b == redirect_bin) o -= bin_starts[b];
-        goff[b] = o;
+        goff[b] = seg_start(offsets, bin_starts, T, tile, b, redirect_bin);
         run[b] = 0;
     }
     wave_sync();
@@ -76,86 +74,6 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
     }
 }
 
-// Register-resident pack for <= 64 bins and rows of <= 64 bytes (the
-// common case, e.g. 8 grid cells x 32-byte records).  Lane l keeps the next
-// free slot of bin l in a register; a row finds its slot with one
-// cross-lane read (bpermute) of its bin's lane; per-bin round counts come
-// from the same nbits ballots as the rank, so there is no LDS traffic.  The
-// next round's destinations and rows are prefetched while the current
-// round is ranked and stored.
-template <int W, int UPR, bool NT, bool NTS>
-__global__ __launch_bounds__(kBlock) void pack_small_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
-    int nb, int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst) {
-    using U = typename Unit<W>::T;
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
-    if (tile >= T) return;
-    long long next_slot = 0;  // lane l: next free slot of bin l
-    if (lane < nb) {
-        next_slot = offsets[(int64_t)lane * T + tile];
-        if (lane == redirect_bin) next_slot -= bin_starts[lane];
-    }
-    const int64_t row0 = tile * (int64_t)tile_rows;
-    const int rows = (int)min((int64_t)tile_rows, n - row0);
-    // Round = 64 rows = 64*UPR units of W bytes, contiguous in src.  Lane l
-    // moves units 64k + l (k < UPR): every load instruction reads 64*W
-    // contiguous bytes.  The unit's row (compile-time division by UPR) gets
-    // its slot from the lane that ranked it.
-    const U* __restrict__ s_u = (const U*)src + row0 * UPR;
-    U* __restrict__ d_u = (U*)dst;
-    U* __restrict__ r_u = (U*)redirect_dst;
-    unsigned nb_next = 0;
-    U nv[UPR];
-    if (lane < rows) nb_next = dest[row0 + lane];
-#pragma unroll
-    for (int k = 0; k < UPR; ++k)
-        if (64 * k + lane < rows * UPR) nv[k] = ld<NT>(s_u + 64 * k + lane);
-    for (int r0 = 0; r0 < rows; r0 += 64) {
-        const int nr = min(64, rows - r0);
-        const bool valid = lane < nr;
-        const unsigned b = valid ? nb_next : 0u;
-        U v[UPR];
-#pragma unroll
-        for (int k = 0; k < UPR; ++k) v[k] = nv[k];
-        if (r0 + 64 < rows) {  // next round in flight
-            const int nn = min(64, rows - r0 - 64);
-            if (lane < nn) nb_next = dest[row0 + r0 + 64 + lane];
-            const U* sp = s_u + (int64_t)(r0 + 64) * UPR;
-#pragma unroll
-            for (int k = 0; k < UPR; ++k)
-                if (64 * k + lane < nn * UPR) nv[k] = ld<NT>(sp + 64 * k + lane);
-        }
-        // nbits ballots: rank inside the wave + per-bin counts for lane == bin
-        unsigned long long peers = __ballot(valid);
-        unsigned long long mine = peers;  // lanes whose bin == this lane's index
-        for (int i = 0; i < nbits; ++i) {
-            const unsigned long long m = __ballot((b >> i) & 1u);
-            peers &= ((b >> i) & 1u) ? m : ~m;
-            mine &= ((lane >> i) & 1) ? m : ~m;
-        }
-        if (!valid) peers = 0;
-        const long long base = __shfl(next_slot, (int)b, 64);
-        next_slot += __popcll(mine);
-        // per-row target: slot, or -1 (dropped / past the end); bit 62 = redirect
-        long long tgt = -1;
-        if (valid && (int)b != drop_bin)
-            tgt = (base + rank_in(peers)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
-#pragma unroll
-        for (int k = 0; k < UPR; ++k) {
-            const int u = 64 * k + lane;
-            const int r = u / UPR, part = u - r * UPR;
-            const long long t = __shfl(tgt, r, 64);
-            if (u < nr * UPR && t >= 0) {
-                U* o = (t >> 62) ? r_u : d_u;
-                st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[k]);
-            }
-        }
-    }
-}
-
 // Block-cooperative pack for <= 64 bins and rows of <= 64 bytes: one
 // workgroup per tile of R rounds, wave w ranks and moves round w (64 rows)
 // in one shot -- the short-lived, fully parallel shape that streams best.
@@ -168,7 +86,8 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
+    const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kCoopMaxRounds][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -185,10 +104,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
         b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
     }
     long long tbase = 0;
-    if (lane < nb) {
-        tbase = offsets[(int64_t)lane * T + tile];
-        if (lane == redirect_bin) tbase -= bin_starts[lane];
-    }
+    if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
@@ -224,6 +140,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
         s_cnt[w * RPW + q][lane] = cnt[q];
     }
     __syncthreads();
+    if (scan_failed(scan_err)) return;
     for (int j = 0; j < w * RPW; ++j) tbase += s_cnt[j][lane];
     U* __restrict__ d_u = (U*)dst;
     U* __restrict__ r_u = (U*)redirect_dst;
@@ -256,12 +173,13 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
 template <int W, int UPR>
 __global__ __launch_bounds__(256) void compact_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
-    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst) {
+    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     constexpr int D = 4;   // rounds per batch (8 measured the same: sparse rows cost whole lines)
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = (int64_t)blockIdx.x * 4 + w;
-    if (tile >= T) return;
+    if (tile >= T || scan_failed(scan_err)) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     long long base = offsets[tile];          // bin 0 (kept) segment of the tile
@@ -354,11 +272,11 @@ __global__ __launch_bounds__(256) void compact2_kernel(
     const uint8_t* __restrict__ src1, uint8_t* __restrict__ dst1,
     const uint8_t* __restrict__ src2, uint8_t* __restrict__ dst2, int64_t n,
     const uint8_t* __restrict__ dest, const int64_t* __restrict__ offsets, int64_t T,
-    int tile_rows) {
+    int tile_rows, const uint32_t* __restrict__ scan_err) {
     constexpr int D = 4;
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = (int64_t)blockIdx.x * 4 + w;
-    if (tile >= T) return;
+    if (tile >= T || scan_failed(scan_err)) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     long long base = offsets[tile];
@@ -413,7 +331,7 @@ hipError_t launch_select_pack2(const void* src1, int64_t rb1, void* dst1, const 
     auto go = [&](auto k) {
         hipLaunchKernelGGL(k, grid, dim3(256), 0, s, (const uint8_t*)src1, (uint8_t*)dst1,
                            (const uint8_t*)src2, (uint8_t*)dst2, n, (const uint8_t*)dest,
-                           ws.offsets, ws.T, tile_rows);
+                           ws.offsets, ws.T, tile_rows, ws.scan_err);
         return hipGetLastError();
     };
     if (g_tune.pack_compact && w1 == 16 && u1 >= 1 && u1 <= 4 && u2 == 3 && (w2 == 8 || w2 == 4)) {
@@ -438,11 +356,12 @@ hipError_t launch_select_pack2(const void* src1, int64_t rb1, void* dst1, const 
 template <int W>
 __global__ __launch_bounds__(256) void compact_any_kernel(
     const uint8_t* __restrict__ src, int64_t upr, int64_t n, const uint8_t* __restrict__ dest,
-    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst) {
+    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = (int64_t)blockIdx.x * 4 + w;
-    if (tile >= T) return;
+    if (tile >= T || scan_failed(scan_err)) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     long long base = offsets[tile];
@@ -468,7 +387,8 @@ static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const
 #define MGR_CK(U_)                                                                             \
     case U_:                                                                                   \
         hipLaunchKernelGGL((compact_kernel<W, U_>), grid, dim3(256), 0, s, (const uint8_t*)src, \
-                           n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows, (uint8_t*)dst); \
+                           n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows, (uint8_t*)dst, \
+                           ws.scan_err);                                                          \
         return hipGetLastError();
     if (64 * W <= 1024 || upr <= 4) {
         switch (upr) {
@@ -491,7 +411,7 @@ static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const
 #undef MGR_CK
     hipLaunchKernelGGL(compact_any_kernel<W>, grid, dim3(256), 0, s, (const uint8_t*)src,
                        row_bytes / W, n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows,
-                       (uint8_t*)dst);
+                       (uint8_t*)dst, ws.scan_err);
     return hipGetLastError();
 }
 
@@ -513,7 +433,8 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
+    const uint32_t* __restrict__ scan_err) {
     static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
     constexpr int RBYTES = 64 * RB;                 // one round, a multiple of 16
     constexpr int NU = (RBYTES / 16 + 63) / 64;     // 16-byte units per lane
@@ -534,10 +455,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     const bool valid = lane < nr;
     const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
     long long tbase = 0;
-    if (lane < nb) {
-        tbase = offsets[(int64_t)lane * T + tile];
-        if (lane == redirect_bin) tbase -= bin_starts[lane];
-    }
+    if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
     const uint8_t* __restrict__ sp = src + row0 * RB;
     u32x4_t v[NU];
 #pragma unroll
@@ -573,6 +491,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
         if (x < nbytes) *(u32x4_t*)(img + x) = v[k];
     }
     __syncthreads();
+    if (scan_failed(scan_err)) return;
     for (int j = 0; j < w; ++j) tbase += s_cnt[j * 64 + lane];
     // round image order: exclusive prefix of the round's bin counts
     int incl = cnt;
@@ -637,7 +556,8 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     const uint8_t* __restrict__ src, int64_t n, const DestT* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
+    const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     constexpr int R = 16 * RPW;                                // rounds per super-round
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -645,11 +565,9 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     uint16_t* tab = (uint16_t*)(smem + align16(nb * 8));       // [R][nb]
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
-    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x) {
-        long long o = offsets[(int64_t)bb * T + tile];
-        if (bb == redirect_bin) o -= bin_starts[bb];
-        s_off[bb] = o;
-    }
+    if (scan_failed(scan_err)) return;
+    for (int bb = threadIdx.x; bb < nb; bb += blockDim.x)
+        s_off[bb] = seg_start(offsets, bin_starts, T, tile, bb, redirect_bin);
     U* __restrict__ d_u = (U*)dst;
     U* __restrict__ r_u = (U*)redirect_dst;
     // the tile's super-rounds of 64 * R rows, in order: a bin's rows of
@@ -718,96 +636,6 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     }
 }
 
-// Destination-sorted pack for <= 64 bins and rows of <= 64 bytes.  As
-// pack_coop_kernel, one workgroup per tile and wave w ranks round w; but the
-// rows are first written into an LDS image of the tile SORTED by destination
-// (bin, then original order), and the image is then streamed out in order:
-// each store instruction writes 64*W contiguous bytes of one or two
-// destination runs instead of ~nbins short runs.  LDS: the image
-// (tile_rows * row bytes), the [rounds][64] count table and one bin byte per
-// sorted row.
-template <int W, int UPR, bool NT>
-__global__ __launch_bounds__(1024) void pack_sorted_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
-    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd) {
-    using U = typename Unit<W>::T;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int R = tile_rows >> 6;
-    U* img = (U*)smem;
-    int* s_cnt = (int*)(smem + (size_t)tile_rows * UPR * W);
-    uint8_t* s_bin = (uint8_t*)(s_cnt + R * 64);
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
-    const int64_t trow0 = tile * (int64_t)tile_rows;
-    const int64_t row0 = trow0 + 64 * w;
-    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
-    const int trows = (int)min((int64_t)tile_rows, n - trow0);
-    const bool valid = lane < nr;
-    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
-    long long tbase = 0;
-    if (lane < nb) {
-        tbase = offsets[(int64_t)lane * T + tile];
-        if (lane == redirect_bin) tbase -= bin_starts[lane];
-    }
-    const U* __restrict__ sp = (const U*)src + row0 * UPR;
-    U v[UPR];
-#pragma unroll
-    for (int k = 0; k < UPR; ++k)
-        if (64 * k + lane < nr * UPR) v[k] = ld<NT>(sp + 64 * k + lane);
-    unsigned long long peers = __ballot(valid);
-    unsigned long long mine = peers;
-    for (int i = 0; i < nbits; ++i) {
-        const unsigned long long m = __ballot((b >> i) & 1u);
-        peers &= ((b >> i) & 1u) ? m : ~m;
-        mine &= ((lane >> i) & 1) ? m : ~m;
-    }
-    if (!valid) peers = 0;
-    s_cnt[w * 64 + lane] = __popcll(mine);
-    __syncthreads();
-    // lane = bin: rows of this bin in earlier rounds, and in the whole tile
-    int before = 0, tot = 0;
-    for (int j = 0; j < R; ++j) {
-        const int c = s_cnt[j * 64 + lane];
-        before += (j < w) ? c : 0;
-        tot += c;
-    }
-    // exclusive scan of the per-bin tile totals over the lanes: local bin start
-    int lstart = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(lstart, o, 64);
-        if (lane >= o) lstart += y;
-    }
-    lstart -= tot;
-    const int lpos = __shfl(lstart + before, (int)b, 64) + rank_in(peers);
-#pragma unroll
-    for (int k = 0; k < UPR; ++k) {
-        const int u = 64 * k + lane;
-        const int r = u / UPR, part = u - r * UPR;
-        const int t = __shfl(lpos, r, 64);
-        if (u < nr * UPR) img[t * UPR + part] = v[k];
-    }
-    if (valid) s_bin[lpos] = (uint8_t)b;
-    __syncthreads();
-    // stream the sorted image out: wave w writes sorted units [w*64*UPR, ...)
-    const long long delta = tbase - lstart;   // lane = bin: global slot - local position
-    U* __restrict__ d_u = (U*)dst;
-    U* __restrict__ r_u = (U*)redirect_dst;
-#pragma unroll
-    for (int k = 0; k < UPR; ++k) {
-        const int u = w * 64 * UPR + 64 * k + lane;
-        const int p = u / UPR, part = u - p * UPR;
-        const int bb = p < trows ? (int)s_bin[p] : 0;
-        const long long dl = __shfl(delta, bb, 64);
-        if (p < trows && bb != drop_bin) {
-            U* o = bb == redirect_bin ? r_u : d_u;
-            o[(p + dl) * UPR + part] = img[u];
-        }
-    }
-}
-
 // ============================================================ launchers
 // pack_many_kernel: super-rounds of 64 * R rows (the uint16 [R][nbins] LDS
 // table stays <= 128 KiB at 4096 rows and 1024 bins), many_super super-rounds
@@ -852,71 +680,45 @@ static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const vo
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s,
                        (const uint8_t*)src, row_bytes / W, n, (const DestT*)dest, nb,
                        nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,
-                       per_wave, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst);
+                       per_wave, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, ws.scan_err);
     return hipGetLastError();
 }
 
 template <int W, int UPR>
-static hipError_t pack_small_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
-                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
-                               void* redirect_dst, hipStream_t s) {
-    if (g_tune.pack_sorted && tile_rows <= 1024) {
-        const int threads = tile_rows;   // one wave per 64-row round of the tile
-        const int lds = tile_rows * UPR * W + (tile_rows / 64) * 64 * 4 + tile_rows;
-#define MGR_PSS(NT_)                                                                          \
-        {                                                                                     \
-        ensure_lds(pack_sorted_kernel<W, UPR, NT_>, lds);                                      \
-        hipLaunchKernelGGL((pack_sorted_kernel<W, UPR, NT_>), dim3((unsigned)ws.T), dim3(threads), \
-                           (size_t)lds, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb,   \
-                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack); }
-        if (g_tune.pack_nt) MGR_PSS(true)
-        else MGR_PSS(false)
-#undef MGR_PSS
-        return hipGetLastError();
-    }
-    if (g_tune.pack_coop && tile_rows <= 2048) {
-        // one wave per RPW 64-row rounds of the tile (<= 16 waves)
-        const int rpw = tile_rows > 1024 ? 2 : 1;
-        const int threads = tile_rows / rpw;
+static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                              int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
+                              void* redirect_dst, hipStream_t s) {
+    if (!g_tune.pack_coop || tile_rows > 2048) return hipErrorNotSupported;
+    // one wave per RPW 64-row rounds of the tile (<= 16 waves)
+    const int rpw = tile_rows > 1024 ? 2 : 1;
+    const int threads = tile_rows / rpw;
 #define MGR_PCK(NT_, RPW_, NTS_)                                                              \
-        hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T), \
-                           dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
-                           nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, \
-                           (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel)
-        // selection packs (2 bins, one dropped: the halo's rows to send) skip
-        // the loads of dropped rows; elsewhere loads go out before the bins are known
-        const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
-        if (g_tune.pack_nt >= 2) {
-            if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
-        } else if (g_tune.pack_nt == 1) {
-            if (rpw == 2) MGR_PCK(true, 2, false); else MGR_PCK(true, 1, false);
-        } else {
-            if (rpw == 2) MGR_PCK(false, 2, false); else MGR_PCK(false, 1, false);
-        }
-#undef MGR_PCK
-        return hipGetLastError();
+    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T),     \
+                       dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
+                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,   \
+                       (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack,  \
+                       sel, ws.scan_err)
+    // selection packs (2 bins, one dropped: the halo's rows to send) skip
+    // the loads of dropped rows; elsewhere loads go out before the bins are known
+    const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
+    if (g_tune.pack_nt >= 2) {
+        if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
+    } else if (g_tune.pack_nt == 1) {
+        if (rpw == 2) MGR_PCK(true, 2, false); else MGR_PCK(true, 1, false);
+    } else {
+        if (rpw == 2) MGR_PCK(false, 2, false); else MGR_PCK(false, 1, false);
     }
-    const int64_t grid = (ws.T + kWaves - 1) / kWaves;
-#define MGR_PSK(NT_, NTS_)                                                                  \
-    hipLaunchKernelGGL((pack_small_kernel<W, UPR, NT_, NTS_>), dim3((unsigned)grid), dim3(kBlock), \
-                       0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),    \
-                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,     \
-                       redirect_bin, (uint8_t*)redirect_dst)
-    if (g_tune.pack_nt >= 2) MGR_PSK(true, true);
-    else if (g_tune.pack_nt == 1) MGR_PSK(true, false);
-    else MGR_PSK(false, false);
-#undef MGR_PSK
+#undef MGR_PCK
     return hipGetLastError();
 }
 
 // Compile-time units per row for rows of <= 64 bytes in 16/8/4-byte units
 // (registers, no scratch); returns hipErrorNotSupported for other shapes.
 template <int W>
-static hipError_t pack_small_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+static hipError_t pack_coop_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                                int nb, int drop_bin, int tile_rows, const Workspace& ws,
                                void* dst, int redirect_bin, void* redirect_dst, hipStream_t s) {
-#define MGR_PS(U_) case U_: return pack_small_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+#define MGR_PS(U_) case U_: return pack_coop_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
     if (W >= 4) {
         switch ((int)(row_bytes / W)) {
             MGR_PS(1) MGR_PS(2) MGR_PS(3) MGR_PS(4)
@@ -953,7 +755,7 @@ static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int 
         hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,                \
                            (const uint8_t*)src, n, (const DestT*)dest, nb, nbits_for(nb),      \
                            drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, \
-                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack);             \
+                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err); \
     }
     if (round_rows == 4096) MGR_PMK(4)
     else if (round_rows == 2048) MGR_PMK(2)
@@ -1000,7 +802,7 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
                        (uint8_t*)redirect_dst, g_tune.xcd_pack,
-                       g_tune.pack_sel && nb <= 2 && drop_bin >= 0);
+                       g_tune.pack_sel && nb <= 2 && drop_bin >= 0, ws.scan_err);
     return hipGetLastError();
 }
 
@@ -1043,8 +845,8 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
             if (e != hipErrorNotSupported) return e;
         }
     }
-    if (g_tune.pack_small && nb <= 64 && row_bytes <= 64 && W >= 4) {
-        const hipError_t e = pack_small_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
+    if (nb <= 64 && row_bytes <= 64 && W >= 4) {
+        const hipError_t e = pack_coop_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
                                              ws, dst, redirect_bin, redirect_dst, s);
         if (e != hipErrorNotSupported) return e;
     }

@@ -3,8 +3,9 @@
 After the local stage has produced the per-destination row counts, one
 redistribution does:
   1. count exchange    -> how many rows arrive from each source (host copy);
-  2. layout            -> send offsets (bin-major packed buffer) and receive
-                          offsets in source-rank order (S7), output size;
+  2. layout            -> send offsets (bin-major packed buffer without the
+                          self segment) and receive offsets in source-rank
+                          order (S7), output size;
   3. pack (callback)   -> fills the send buffers; when the transport leaves
                           the self segment alone it is written straight into
                           the output at its source-ordered slot;
@@ -18,6 +19,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from ._lib import MgrError
 from .comm import excl_cumsum
 
 
@@ -32,26 +34,50 @@ class ExchangeLayout:
     redirect_self: bool
 
 
-def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=None):
+def check_counts(send_counts, recv_counts):
+    """A failed device scan reports -1 counts (mgr_kernels.hip scan_onepass_kernel);
+    a peer's failure arrives here as a -1 receive count, so every rank raises
+    together instead of one rank leaving the others inside the exchange."""
+    if (np.asarray(send_counts) < 0).any() or (np.asarray(recv_counts) < 0).any():
+        raise MgrError("device scan failed (a look-back timed out on this rank or a peer): "
+                       f"send counts {list(send_counts)}, receive counts {list(recv_counts)}")
+
+
+def plan_layout(send_counts, recv_counts, rank, redirect_self):
+    """Send/receive offsets in rows.  Receives in source-rank order (S7).
+    With ``redirect_self`` the self segment never enters the send buffer
+    (mgr_pack writes it straight into the output and closes the gap), so
+    the send offsets skip it and the buffer holds only the rows that travel."""
+    sc = np.asarray(send_counts, dtype=np.int64)
+    rc = np.asarray(recv_counts, dtype=np.int64)
+    travel = sc.copy()
+    if redirect_self:
+        travel[rank] = 0
+    return ExchangeLayout(send_counts=sc, recv_counts=rc, send_offsets=excl_cumsum(travel),
+                          recv_offsets=excl_cumsum(rc), total_recv=int(rc.sum()),
+                          total_send=int(travel.sum()), redirect_self=bool(redirect_self))
+
+
+def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=None,
+             scratch=None):
     """Run steps 1-4.  ``bin_counts``: int64 tensor [size] of rows per
     destination (on ``device``).  ``pack(field, send, redirect_bin,
     redirect_out)`` packs field ``field``.  ``extra_rows(total_recv)``: spare
     rows to allocate after the received ones (the halo appends there).
-    Returns (outs, layout); outs are flat uint8 tensors of (total_recv +
-    extra) * row_bytes[f] bytes (>= 1 byte)."""
+    ``scratch(name, nbytes)``: a reusable device buffer (the send buffers),
+    else fresh allocations.  Returns (outs, layout); outs are new flat uint8
+    tensors of (total_recv + extra) * row_bytes[f] bytes (>= 1 byte)."""
     sc, rc = transport.exchange_counts(bin_counts)
-    lay = ExchangeLayout(send_counts=sc, recv_counts=rc, send_offsets=excl_cumsum(sc),
-                         recv_offsets=excl_cumsum(rc), total_recv=int(rc.sum()),
-                         total_send=int(sc.sum()), redirect_self=bool(transport.skips_self))
-    size = len(sc)
+    check_counts(sc, rc)
+    lay = plan_layout(sc, rc, rank, transport.skips_self)
     extra = int(extra_rows(lay.total_recv)) if extra_rows is not None else 0
     outs, sends = [], []
     for f, rb in enumerate(row_bytes):
+        # the output is returned to the caller: always a new array (redist.py:199)
         out = torch.empty(max((lay.total_recv + extra) * rb, 1), dtype=torch.uint8, device=device)
-        n_send = lay.total_send
-        if lay.redirect_self and size == 1:
-            n_send = 0  # everything is the self segment
-        snd = torch.empty(max(n_send * rb, 1), dtype=torch.uint8, device=device)
+        nbytes = max(lay.total_send * rb, 1)
+        snd = (scratch(f"send{f}", nbytes) if scratch is not None
+               else torch.empty(nbytes, dtype=torch.uint8, device=device))
         if lay.redirect_self:
             pack(f, snd, rank, out[int(lay.recv_offsets[rank]) * rb:])
         else:

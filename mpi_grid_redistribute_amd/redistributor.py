@@ -39,7 +39,7 @@ import torch
 from . import _lib
 from ._arrays import Positions, Rows, box_dtype_code, device, id_array
 from .comm import SelfComm, as_transport
-from .exchange import exchange
+from .exchange import check_counts, exchange
 from .halo import exchange_overload, halo_capacity
 
 
@@ -96,21 +96,53 @@ def _fine_sort(plan, dim, dev, data, position, return_positions):
         outs.append(f.wrap(o, n))
     offsets = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
     offsets[1:] = torch.cumsum(counts, 0)
-    if isinstance(data, torch.Tensor):
-        offsets = offsets if data.is_cuda else offsets.cpu()
-    else:
-        offsets = offsets.cpu().numpy()
+    if not (isinstance(data, torch.Tensor) and data.is_cuda):
+        # device results stay asynchronous (a failed scan shows as -1 counts);
+        # host results are checked at the copy
+        check_counts(counts.cpu().numpy(), [])
+        offsets = offsets.cpu() if isinstance(data, torch.Tensor) else offsets.cpu().numpy()
     return tuple(outs) + (offsets,)
 
 
-def _scratch(n, nbins, max_row_bytes, dev):
+class Scratch:
+    """Reusable device buffers of one redistributor (workspace, destination
+    bytes, send buffers): grown geometrically, never shrunk, so repeated
+    calls with varying sizes (skewed counts) stop allocating after the first
+    few.  Stream-ordered reuse: calls on one stream run in order."""
+
+    GROWTH = 1.25
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.bufs = {}
+
+    def get(self, name, nbytes):
+        nbytes = max(int(nbytes), 1)
+        b = self.bufs.get(name)
+        if b is None or b.numel() < nbytes:
+            if b is not None:
+                nbytes = max(nbytes, int(b.numel() * self.GROWTH))
+            del b
+            self.bufs.pop(name, None)
+            b = self.bufs[name] = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        return b
+
+    def release(self):
+        self.bufs.clear()
+
+
+def _scratch(n, nbins, max_row_bytes, dev, cache=None):
+    """(tile_rows, workspace, dest) for n rows and nbins bins; from ``cache``
+    (a Scratch) when given, else fresh."""
     tile_rows = _lib.load().mgr_tile_rows(int(max_row_bytes), int(nbins))
     wsb = _lib.load().mgr_workspace_bytes(int(n), int(nbins), int(tile_rows))
     if wsb < 0:
         raise _lib.MgrError("mgr_workspace_bytes: bad arguments")
+    db = max(int(n), 1) * _lib.load().mgr_dest_bytes(int(nbins))
+    if cache is not None:
+        return tile_rows, cache.get("ws", wsb), cache.get("dest", db)
     ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
-    dest = torch.empty(max(int(n), 1) * _lib.load().mgr_dest_bytes(int(nbins)), dtype=torch.uint8,
-                       device=dev)
+    dest = torch.empty(db, dtype=torch.uint8, device=dev)
     return tile_rows, ws, dest
 
 
@@ -149,6 +181,7 @@ class MPIGridRedistributor:
         self._plan = _Plan(self.grid_topology, self.box_length, self.size)
         self._fine_plans = {}
         self._dev = device()
+        self._scratch = Scratch(self._dev)
 
     # ------------------------------------------------------ binning (L1)
     def get_cell_indexes_from_position(self, position, periodic=True):
@@ -354,7 +387,7 @@ class MPIGridRedistributor:
         P = self.size
         nb = P + 1 if drop else P
         hint = row_bytes_hint or [f.row_bytes for f in fields]
-        tile_rows, ws, dest = _scratch(n, nb, max(max(hint), 1), self._dev)
+        tile_rows, ws, dest = _scratch(n, nb, max(max(hint), 1), self._dev, self._scratch)
         binner(dest, tile_rows, ws)
         stream = _lib.stream_handle()
         bin_counts = torch.empty(nb, dtype=torch.int64, device=self._dev)
@@ -367,7 +400,7 @@ class MPIGridRedistributor:
                       _lib.ptr(redirect_out), stream)
 
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
-                             self._dev, pack, extra_rows=extra_rows)
+                             self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get)
         return outs, lay.total_recv
 
     # ------------------------------------------------------------ helpers
@@ -456,9 +489,13 @@ class GridPartitioner:
                   tile_rows, _lib.ptr(ws), _lib.ptr(out), -1, None, stream)
         offsets = torch.zeros(self.nbins + 1, dtype=torch.int64, device=self._dev)
         offsets[1:] = torch.cumsum(counts, 0)
+        if isinstance(data, torch.Tensor) and data.is_cuda:
+            # device results stay asynchronous: a failed scan shows as -1 counts
+            return rows.wrap(out, n), offsets
+        check_counts(counts.cpu().numpy(), [])   # a failed scan reports -1 counts
         res = rows.wrap(out, n)
         if isinstance(data, torch.Tensor):
-            return res, offsets if data.is_cuda else offsets.cpu()
+            return res, offsets.cpu()
         return res, offsets.cpu().numpy()
 
 

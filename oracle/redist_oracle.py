@@ -177,6 +177,33 @@ def redistribute_by_cell_number_all_ranks(size, data_list, ids_list):
     return alltoall_concat([stable_split(d, i, size) for d, i in zip(data_list, ids_list)])
 
 
+# ------------------------------------------------------- position helpers
+def stack_position(columns):
+    """``stack_position`` (redist.py:311-312): d columns of N -> (N, d),
+    ``np.vstack(columns).T``."""
+    return np.vstack(columns).T
+
+
+def unstack_position(position, dim):
+    """Intended behaviour of ``unstack_position`` (redist.py:314-318), whose
+    text is broken (``for d in self.dim``, ``reusult``): the dim columns."""
+    return [position[:, d] for d in range(dim)]
+
+
+def mpi_grid_redistribute_all_ranks(data_list, pos_list, grid_topology, box_lengths, size,
+                                    overload_lengths=None, periodic=True):
+    """Intended behaviour of the module function ``mpi_grid_redistribute``
+    (redist.py:11-13): a redistributor per rank, then
+    ``redistribute_by_position(data, pos, overload_lengths, periodic)``
+    (the reference calls a misspelled method and raises, S13)."""
+    if overload_lengths is None:
+        return redistribute_by_position_all_ranks(grid_topology, box_lengths, size, data_list,
+                                                  pos_list, periodic=periodic)
+    return redistribute_by_position_overload_all_ranks(grid_topology, box_lengths, size,
+                                                       data_list, pos_list, overload_lengths,
+                                                       periodic=periodic)
+
+
 # ------------------------------------------------------- overload / halo
 def _send_rows(field_local, pos_local, field_ov, pos_ov, d, thr, right, keep):
     """One side of ``exchange_overload_by_position``'s selection
@@ -246,15 +273,15 @@ def exchange_overload_all_ranks(grid_topology, box_length, size, data_list, pos_
 
 
 def redistribute_by_position_overload_all_ranks(grid_topology, box_length, size, data_list,
-                                                pos_list, overload_lengths):
+                                                pos_list, overload_lengths, periodic=True):
     """``redistribute_by_position`` with ``overload_lengths`` (redist.py:157-166):
-    redistribute data and positions with the same destinations, exchange the
-    overload (periodic=True: the flag is not forwarded from :165), and return
-    concat(local, overload) per rank."""
+    bin with ``periodic`` (:157), redistribute data and positions with the same
+    destinations, exchange the overload (periodic=True: the flag is not
+    forwarded from :165), and return concat(local, overload) per rank."""
     dest = []
     for r in range(size):
         geo = Geometry(grid_topology, box_length, size, r)
-        dest.append(cell_number_from_position(geo, pos_list[r], periodic=True))
+        dest.append(cell_number_from_position(geo, pos_list[r], periodic=periodic))
     local = redistribute_by_cell_number_all_ranks(size, data_list, dest)
     local_pos = redistribute_by_cell_number_all_ranks(size, pos_list, dest)
     ovd = exchange_overload_all_ranks(grid_topology, box_length, size, local, local_pos,

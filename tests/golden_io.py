@@ -17,6 +17,48 @@ def redist_cases():
     return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "redist_*.npz")))
 
 
+def halo_cases():
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "halo_p*.npz")))
+
+
+def halo_direct_cases():
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "halo_direct_*.npz")))
+
+
+def fixture_inputs(f, case, size, as_torch):
+    """Per-rank (data, position) inputs of a redist_* fixture: numpy copies, or
+    GPU torch tensors with the same aliasing (position = data, or a view of
+    the records' pos field)."""
+    pos = [p.copy() for p in per_rank(f, "pos_in", size)]
+    if bool(f["alias"]):
+        data = pos
+    elif "view" in case:
+        data = [d.copy() for d in per_rank(f, "data", size)]
+        pos = [d["pos"] for d in data]
+    else:
+        data = [d.copy() for d in per_rank(f, "data", size)]
+    if not as_torch:
+        return data, pos
+    import torch
+    tdata, tpos = [], []
+    for r in range(size):
+        if bool(f["alias"]):
+            t = torch.from_numpy(pos[r]).cuda()
+            tdata.append(t)
+            tpos.append(t)
+        elif "view" in case:
+            raw = torch.from_numpy(data[r].view(np.uint8).reshape(len(data[r]), -1)).cuda()
+            tdata.append(raw)
+            tpos.append(raw.view(torch.float32)[:, :3])
+        else:
+            d = data[r]
+            if d.dtype.names:
+                d = d.view(np.uint8).reshape(len(d), -1)
+            tdata.append(torch.from_numpy(np.ascontiguousarray(d)).cuda())
+            tpos.append(torch.from_numpy(pos[r]).cuda())
+    return tdata, tpos
+
+
 def bin_edge_keys(f):
     return sorted({k[: k.rindex("_pos_in")] for k in f.keys() if k.endswith("_pos_in")})
 

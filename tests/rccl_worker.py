@@ -1,0 +1,225 @@
+"""One rank of the multi-process RCCL parity run (tests/test_gpu_multi.py).
+
+Runs the product transport -- RcclComm, i.e. libmgr.so's mgr_exchange_counts,
+mgr_exchange_rows (grouped ncclSend/ncclRecv, receives in place at
+source-ordered offsets) and mgr_sendrecv (the halo's isend/irecv pairs) --
+between distinct ranks, and checks every rank's result bit-exact against the
+reference's own outputs (tests/golden/*.npz) and the oracle.  Replaces
+``comm.alltoall`` (redist.py:199) and the isend/irecv pairs (redist.py:289-303).
+
+Environment: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT (torch.distributed
+gloo rendezvous; it only carries the RCCL unique id), MGR_TEST_OUT (result
+file), MGR_TEST_SHARED_GPU=1 when the ranks share GPU 0: each rank then
+presents its own NCCL_HOSTID, so RCCL treats them as separate hosts and
+connects them with its socket transport over loopback (correctness of the
+exchange logic, not xGMI speed); otherwise rank r uses GPU r (xGMI).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RANK = int(os.environ["RANK"])
+WORLD = int(os.environ["WORLD_SIZE"])
+SHARED = os.environ.get("MGR_TEST_SHARED_GPU") == "1"
+if SHARED:   # before anything loads RCCL
+    os.environ["NCCL_HOSTID"] = f"mgr-test-rank-{RANK}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from oracle import redist_oracle as ro  # noqa: E402  (checker)
+from tests import golden_io as G  # noqa: E402
+
+TOPO = {1: [1, 1, 1], 2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}
+BOX = [1.0, 1.0, 1.0]
+
+
+def log(msg):
+    print(f"[rank {RANK}/{WORLD} {time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+def as_bytes(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().contiguous().numpy().view(np.uint8).reshape(-1)
+    return np.ascontiguousarray(x).view(np.uint8).reshape(-1)
+
+
+def records(n, r, rng):
+    rec = np.zeros(n, dtype=[("x", "f8"), ("y", "f8"), ("z", "f8"), ("id", "i8")])
+    rec["id"] = np.arange(n) + 1_000_000 * r
+    return rec
+
+
+def case_redist_golden(mgr, comm, name, as_torch):
+    f = G.load(name)
+    data, pos = G.fixture_inputs(f, name, WORLD, as_torch)
+    R = mgr.MPIGridRedistributor(comm, f["topology"], f["box"])
+    out = R.redistribute_by_position(data[RANK], pos[RANK], periodic=bool(f["periodic"]))
+    torch.cuda.synchronize()
+    assert np.array_equal(as_bytes(pos[RANK]), as_bytes(f[f"r{RANK}_pos_out"])), "positions"
+    exp = f[f"r{RANK}_out"]
+    if as_torch:
+        assert np.array_equal(as_bytes(out), as_bytes(exp)), "output bytes"
+    else:
+        assert G.same_bytes(out, exp), "output"
+
+
+def case_halo_golden(mgr, comm, name, as_torch):
+    f = G.load(name)
+    data = f[f"r{RANK}_data"].copy()
+    pos = f[f"r{RANK}_pos_in"].copy()
+    if as_torch:
+        data = torch.from_numpy(data.view(np.uint8).reshape(len(data), -1) if data.dtype.names
+                                else data).cuda()
+        pos = torch.from_numpy(pos).cuda()
+    R = mgr.MPIGridRedistributor(comm, f["topology"], f["box"])
+    out = R.redistribute_by_position(data, pos, overload_lengths=list(f["overload"]))
+    torch.cuda.synchronize()
+    assert np.array_equal(as_bytes(out), as_bytes(f[f"r{RANK}_out"])), "halo output"
+    assert np.array_equal(as_bytes(pos), as_bytes(f[f"r{RANK}_pos_out"])), "positions"
+
+
+def case_halo_direct_golden(mgr, comm, name):
+    f = G.load(name)
+    R = mgr.MPIGridRedistributor(comm, f["topology"], f["box"])
+    out = R.exchange_overload_by_position(f[f"r{RANK}_data"], f[f"r{RANK}_pos"],
+                                          list(f["overload"]), periodic=False)
+    assert G.same_bytes(out, f[f"r{RANK}_out"]), "halo (direct, non-periodic)"
+
+
+def rank_inputs(seed, sizes, lo=-0.5, hi=1.5, hot=None):
+    """Every rank's input (each rank builds all of them: the oracle needs all)."""
+    pos, data = [], []
+    for r, n in enumerate(sizes):
+        rng = np.random.default_rng(seed + r)
+        p = rng.uniform(lo, hi, (n, 3))
+        if hot is not None and n:   # skew: most rows into one rank's cell
+            k = rng.random(n) < 0.8
+            p[k] = rng.uniform(0.0, 0.5, (int(k.sum()), 3)) + np.asarray(hot)
+        pos.append(p)
+        data.append(records(n, r, rng))
+    return pos, data
+
+
+def case_random(mgr, comm, sizes, seed, as_torch, hot=None, return_positions=False):
+    topo = TOPO[WORLD]
+    pos, data = rank_inputs(seed, sizes, hot=hot)
+    pos_o = [p.copy() for p in pos]
+    exp = ro.redistribute_by_position_all_ranks(topo, BOX, WORLD, data, pos_o)[RANK]
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    d, p = data[RANK], pos[RANK]
+    if as_torch:
+        d = torch.from_numpy(d.view(np.uint8).reshape(len(d), 32)).cuda()
+        p = torch.from_numpy(p).cuda()
+    out = R.redistribute_by_position(d, p, return_positions=return_positions)
+    torch.cuda.synchronize()
+    if return_positions:
+        out, opos = out
+        want = np.stack([pos_o[s][i] for s, i in
+                         zip(as_bytes(out).view(exp.dtype)["id"] // 1_000_000,
+                             as_bytes(out).view(exp.dtype)["id"] % 1_000_000)]) \
+            if len(exp) else np.zeros((0, 3))
+        assert np.array_equal(as_bytes(opos), as_bytes(want)), "returned positions"
+    assert np.array_equal(as_bytes(out), as_bytes(exp)), "output"
+    assert np.array_equal(as_bytes(p), as_bytes(pos_o[RANK])), "wrapped positions"
+    return len(exp)
+
+
+def case_cell_number(mgr, comm):
+    rng = np.random.default_rng(99)
+    data = [rng.integers(0, 255, (int(rng.integers(0, 5000)), 7)).astype(np.uint8)
+            for _ in range(WORLD)]
+    ids = [np.random.default_rng(500 + r).integers(-2, WORLD + 2, len(d)) for r, d in
+           enumerate(data)]
+    exp = ro.redistribute_by_cell_number_all_ranks(WORLD, data, ids)[RANK]
+    R = mgr.MPIGridRedistributor(comm, [WORLD], [1.0])
+    out = R.redistribute_by_cell_number(torch.from_numpy(data[RANK]).cuda(),
+                                        torch.from_numpy(ids[RANK]).cuda())
+    assert np.array_equal(out.cpu().numpy(), exp), "redistribute_by_cell_number"
+
+
+def case_scan_failure(mgr, comm):
+    """Every rank's scan gives up at once (knob scan_spins = -1): all ranks
+    raise together at the count exchange, nobody hangs in the row exchange."""
+    from mpi_grid_redistribute_amd import _lib
+    topo = TOPO[WORLD]
+    pos, data = rank_inputs(7, [200_000] * WORLD)
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    _lib.tune("scan_spins", -1)
+    try:
+        R.redistribute_by_position(data[RANK], pos[RANK])
+    except _lib.MgrError as e:
+        assert "scan failed" in str(e), str(e)
+    else:
+        raise AssertionError("a failed scan did not raise")
+    finally:
+        _lib.tune("scan_spins", 1 << 24)
+    # the communicator still works afterwards
+    assert case_random(mgr, comm, [1000] * WORLD, 8, False) >= 0
+
+
+def main():
+    out_path = os.environ["MGR_TEST_OUT"]
+    results = {}
+    dev = 0 if SHARED else RANK
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=RANK, world_size=WORLD)
+    import mpi_grid_redistribute_amd as mgr
+    comm = mgr.RcclComm.from_torch_distributed()
+    log(f"RcclComm up (device {dev}, shared={SHARED})")
+    cases = []
+    for name in G.redist_cases():
+        if int(G.load(name)["size"]) == WORLD:
+            for as_torch in (False, True):
+                cases.append((f"{name}[torch={as_torch}]",
+                              lambda n=name, t=as_torch: case_redist_golden(mgr, comm, n, t)))
+    for name in G.halo_cases():
+        if int(G.load(name)["size"]) == WORLD:
+            for as_torch in (False, True):
+                cases.append((f"{name}[torch={as_torch}]",
+                              lambda n=name, t=as_torch: case_halo_golden(mgr, comm, n, t)))
+    for name in G.halo_direct_cases():
+        if int(G.load(name)["size"]) == WORLD:
+            cases.append((name, lambda n=name: case_halo_direct_golden(mgr, comm, n)))
+    if WORLD in TOPO:
+        sizes = [int(np.random.default_rng(r).integers(1000, 30_000)) for r in range(WORLD)]
+        sizes[WORLD - 1] = 0   # an empty rank (the reference raises ValueError, S5)
+        cases += [
+            ("random_empty_rank", lambda: case_random(mgr, comm, sizes, 11, False)),
+            ("random_torch", lambda: case_random(mgr, comm, sizes[::-1], 12, True)),
+            ("skewed_hot_cell", lambda: case_random(mgr, comm, [40_000] * WORLD, 13, True,
+                                                    hot=[0.5, 0.0, 0.0])),
+            ("return_positions", lambda: case_random(mgr, comm, sizes, 14, False,
+                                                     return_positions=True)),
+            ("large_300k", lambda: case_random(mgr, comm, [300_000] * WORLD, 15, True)),
+            ("scan_failure", lambda: case_scan_failure(mgr, comm)),
+        ]
+    cases.append(("cell_number_dropped_ids", lambda: case_cell_number(mgr, comm)))
+    for name, fn in cases:
+        t0 = time.perf_counter()
+        try:
+            fn()
+            results[name] = "ok"
+        except Exception as e:   # record and go on: every rank runs every case
+            results[name] = f"FAIL: {e!r}\n{traceback.format_exc()}"
+        log(f"{name}: {results[name].splitlines()[0]} ({time.perf_counter() - t0:.2f} s)")
+        # keep the ranks in step between cases (a failed case must not skew
+        # the next collective's pairing)
+        dist.barrier()
+    comm.close()
+    dist.destroy_process_group()
+    with open(out_path, "w") as fh:
+        json.dump(results, fh)
+    return 0 if all(v == "ok" for v in results.values()) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

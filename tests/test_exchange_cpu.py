@@ -42,12 +42,17 @@ def oracle_pack(data, dest, size, rb):
     raw = part.view(np.uint8).reshape(-1)
 
     def pack(f, snd, redirect_bin, redirect_out):
+        # mgr_pack semantics: the redirect bin goes to redirect_out from row 0,
+        # the bins after it close its gap in the send buffer
         for b in range(size):
             seg = torch.from_numpy(raw[off[b] * rb: off[b + 1] * rb].copy())
             if b == redirect_bin:
                 redirect_out[: seg.numel()].copy_(seg)
             elif seg.numel():
-                snd[off[b] * rb: off[b + 1] * rb].copy_(seg)
+                o = off[b]
+                if 0 <= redirect_bin < b:
+                    o -= off[redirect_bin + 1] - off[redirect_bin]
+                snd[o * rb: o * rb + seg.numel()].copy_(seg)
 
     counts = torch.from_numpy(np.diff(off).astype(np.int64))
     return pack, counts
@@ -118,3 +123,148 @@ def test_threaded_mpi_host_comm_redirect():
     outs = run_ranks(size, fn)
     for r in range(size):
         assert outs[r].tobytes() == expect[r].tobytes(), r
+
+
+# ------------------------------------------------ the RCCL schedule (host)
+class _SimWorld:
+    """Shared state of the simulated RCCL group: per (src, dst) FIFO of the
+    bytes each send carried, in issue order (RCCL matches a pair's sends and
+    receives inside one group in order)."""
+
+    def __init__(self, size):
+        import threading
+        self.size = size
+        self.barrier = threading.Barrier(size)
+        self.slots = [None] * size
+        self.mail = {}
+        self.lock = threading.Lock()
+
+
+class SimRcclComm:
+    """RcclComm's host side (counts all-to-all, the arrays it hands to
+    mgr_exchange_rows: comm.row_exchange_arrays) with the device transfers
+    replaced by executing mgr_exchange_schedule's operation list on host
+    buffers.  Lets the CPU suite run exchange() exactly as the GPU path does,
+    skip_self included."""
+
+    skips_self = True
+
+    def __init__(self, world, rank):
+        self.world, self.rank, self.size = world, rank, world.size
+
+    def Get_rank(self):
+        return self.rank
+
+    def Get_size(self):
+        return self.size
+
+    def exchange_counts(self, send_counts):
+        w = self.world
+        s = send_counts.detach().cpu().numpy().astype(np.int64)
+        w.slots[self.rank] = s.copy()
+        w.barrier.wait()
+        r = np.array([w.slots[src][self.rank] for src in range(self.size)], dtype=np.int64)
+        w.barrier.wait()
+        return s, r
+
+    def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
+                      recv_offsets):
+        from mpi_grid_redistribute_amd import _lib
+        from mpi_grid_redistribute_amd.comm import row_exchange_arrays
+        rb, sc, so, rc, ro_, skip = row_exchange_arrays(self.size, row_bytes, send_counts,
+                                                        send_offsets, recv_counts, recv_offsets)
+        lib = _lib.load()
+        n = lib.mgr_exchange_schedule(self.rank, self.size, len(sends), rb, sc, so, rc, ro_, skip,
+                                      None, 0)
+        assert n >= 0, lib.mgr_last_error()
+        ops = (_lib.XOp * max(n, 1))()
+        lib.mgr_exchange_schedule(self.rank, self.size, len(sends), rb, sc, so, rc, ro_, skip,
+                                  ops, n)
+        ops = ops[:n]
+        assert all(o.kind != _lib.MGR_XOP_COPY for o in ops)      # skip_self: no self copy
+        assert all(o.peer != self.rank for o in ops)
+        w = self.world
+        with w.lock:
+            for o in ops:
+                if o.kind == _lib.MGR_XOP_SEND:
+                    buf = sends[o.field].numpy()
+                    assert o.src_offset + o.bytes <= buf.size            # inside the send buffer
+                    w.mail.setdefault((self.rank, o.peer), []).append(
+                        (o.field, buf[o.src_offset:o.src_offset + o.bytes].copy()))
+        w.barrier.wait()
+        for o in ops:
+            if o.kind == _lib.MGR_XOP_RECV:
+                with w.lock:
+                    field, data = w.mail[(o.peer, self.rank)].pop(0)
+                assert field == o.field and data.size == o.bytes
+                out = outs[o.field].numpy()
+                assert o.dst_offset + o.bytes <= out.size
+                out[o.dst_offset:o.dst_offset + o.bytes] = data
+        w.barrier.wait()
+        with w.lock:   # every send was received
+            assert all(not v for v in w.mail.values()), "unmatched send"
+
+
+@pytest.mark.parametrize("size,empty_rank,drop", [(2, None, False), (4, 2, False), (8, 0, False),
+                                                  (8, None, True), (3, 1, True)])
+def test_rccl_schedule_exchange(size, empty_rank, drop):
+    """exchange() over the exact RCCL operation list (mgr_exchange_schedule, the
+    list mgr_exchange_rows issues) with RcclComm's arrays and the self-segment
+    redirect, two fields, against the oracle: every send matches a receive of
+    the same size in order, every receive lands at its source-ordered offset."""
+    topo = {2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}[size]
+    pos, data = make_rank_inputs(size, seed=size * 10 + 3, empty_rank=empty_rank)
+    rb = data[0].dtype.itemsize
+    if drop:
+        ids = [np.random.default_rng(200 + r).integers(-1, size + 1, len(data[r]))
+               for r in range(size)]
+        expect = ro.redistribute_by_cell_number_all_ranks(size, data, ids)
+    else:
+        expect = ro.redistribute_by_position_all_ranks(topo, BOX, size, data,
+                                                       [p.copy() for p in pos])
+    world = _SimWorld(size)
+
+    def fn(comm, r):
+        if drop:
+            dest = ids[r]
+        else:
+            dest = ro.cell_number_from_position(ro.Geometry(topo, BOX, size, r), pos[r].copy())
+        pack0, counts = oracle_pack(data[r], dest, size, rb)
+        ids2 = (np.arange(len(data[r]), dtype=np.int32) + 7 * r).view(np.uint8).reshape(-1, 4)
+        pack1, _ = oracle_pack(ids2, dest, size, 4)
+
+        def pack(f, snd, redirect_bin, redirect_out):
+            (pack0 if f == 0 else pack1)(f, snd, redirect_bin, redirect_out)
+
+        t = SimRcclComm(world, r)
+        outs, lay = exchange(t, [rb, 4], counts, r, "cpu", pack)
+        assert lay.total_send == int(counts.sum()) - int(counts[r])   # no self rows in the buffer
+        return outs[0][: lay.total_recv * rb].numpy().copy(), outs[1][: lay.total_recv * 4].numpy()
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert outs[r][0].tobytes() == expect[r].tobytes(), r
+        # the second field followed the same rows
+        assert len(outs[r][1]) // 4 == len(expect[r])
+
+
+def test_rccl_schedule_order_and_self_copy():
+    """Ring order (to = rank+j, from = rank-j), fields inside a peer, and the
+    self-segment copy when the transport does not skip it."""
+    from mpi_grid_redistribute_amd import _lib
+    sc, rc = [3, 0, 5, 1], [2, 4, 0, 6]
+    so, ro_ = [0, 3, 3, 8], [0, 2, 6, 6]
+    ops = _lib.exchange_schedule(1, 4, [32, 24], sc, so, rc, ro_, skip_self=False)
+    S, R, C = _lib.MGR_XOP_SEND, _lib.MGR_XOP_RECV, _lib.MGR_XOP_COPY
+    assert ops == [
+        (S, 2, 0, 3 * 32, -1, 5 * 32), (R, 0, 0, -1, 0, 2 * 32),
+        (S, 2, 1, 3 * 24, -1, 5 * 24), (R, 0, 1, -1, 0, 2 * 24),
+        (S, 3, 0, 8 * 32, -1, 1 * 32), (R, 3, 0, -1, 6 * 32, 6 * 32),
+        (S, 3, 1, 8 * 24, -1, 1 * 24), (R, 3, 1, -1, 6 * 24, 6 * 24),
+        (S, 0, 0, 0, -1, 3 * 32),
+        (S, 0, 1, 0, -1, 3 * 24),
+    ]   # rank 1: no self rows (sc[1] == 0) -> no copy; nothing from rank 2
+    ops = _lib.exchange_schedule(0, 2, [8], [2, 3], [0, 2], [2, 1], [0, 2], skip_self=False)
+    assert ops[-1] == (C, 0, 0, 0, 0, 16)
+    with pytest.raises(_lib.MgrError):
+        _lib.exchange_schedule(0, 2, [8], [-1, 3], [0, 0], [0, 1], [0, 0])

@@ -1,0 +1,161 @@
+"""The rest of the drop-in boundary on the GPU: the module function
+``mpi_grid_redistribute`` (redist.py:11-13, intended behaviour -- the
+reference's raises AttributeError, S13), ``stack_position`` (:311-312) and the
+intended ``unstack_position`` (:314-318), the scan's failure path (a look-back
+that gives up must surface as an error, never as wrong offsets), and scratch
+reuse across calls (no per-call device allocation after warm-up)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import redist_oracle as ro
+from tests import golden_io as G
+from tests.fake_mpi import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+mgr = pytest.importorskip("mpi_grid_redistribute_amd")
+from mpi_grid_redistribute_amd import (GridPartitioner, MPIGridRedistributor,  # noqa: E402
+                                       mpi_grid_redistribute)
+from mpi_grid_redistribute_amd import _lib  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+@pytest.mark.parametrize("case", ["redist_p8_f64_rec32.npz", "redist_p4_2d_alias.npz",
+                                  "redist_p8_nonperiodic_rec32.npz"])
+def test_module_function_golden(case):
+    """mpi_grid_redistribute(data, pos, grid_topology, box_lengths, comm) on
+    threaded ranks = the reference's redistribute_by_position outputs."""
+    f = G.load(case)
+    size = int(f["size"])
+    data, pos = G.fixture_inputs(f, case, size, as_torch=False)
+
+    def fn(comm, r):
+        return mpi_grid_redistribute(data[r], pos[r], f["topology"], f["box"], comm,
+                                     periodic=bool(f["periodic"]))
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], f[f"r{r}_out"]), r
+        assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), r
+
+
+def test_module_function_overload_vs_oracle():
+    """... with overload_lengths (the halo rows follow, redist.py:161-166) and
+    periodic=False binning, against the oracle's intended-behaviour restatement."""
+    rng = np.random.default_rng(41)
+    size, topo, box, ol = 4, [2, 2, 1], [1.0, 1.0, 1.0], [0.1, 0.05, 0.2]
+    pos = [rng.uniform(-0.3, 1.3, (int(rng.integers(2000, 6000)), 3)) for _ in range(size)]
+    data = [np.arange(len(p), dtype=np.int64) * 10 + r for r, p in enumerate(pos)]
+    pos_o = [p.copy() for p in pos]
+    exp = ro.mpi_grid_redistribute_all_ranks(data, pos_o, topo, box, size,
+                                             overload_lengths=ol, periodic=False)
+
+    def fn(comm, r):
+        return mpi_grid_redistribute(data[r], pos[r], topo, box, comm, overload_lengths=ol,
+                                     periodic=False)
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], exp[r]), r
+        assert G.same_bytes(pos[r], pos_o[r]), r
+
+
+def test_module_function_single_rank_torch():
+    rng = np.random.default_rng(3)
+    pos = rng.uniform(-1, 2, (50_000, 3))
+    data = np.arange(50_000, dtype=np.float64)
+    pos_o = pos.copy()
+    exp = ro.mpi_grid_redistribute_all_ranks([data], [pos_o], [1, 1, 1], [1.0] * 3, 1)[0]
+    tpos = torch.from_numpy(pos).cuda()
+    out = mpi_grid_redistribute(torch.from_numpy(data).cuda(), tpos, [1, 1, 1], [1.0] * 3, None)
+    assert out.is_cuda
+    assert G.same_bytes(out.cpu().numpy(), exp)
+    assert G.same_bytes(tpos.cpu().numpy(), pos_o)
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+def test_stack_unstack_position(dim):
+    rng = np.random.default_rng(dim)
+    cols = [rng.uniform(0, 1, 1000) for _ in range(dim)]
+    R = MPIGridRedistributor(None, [1] * dim, [1.0] * dim)
+    got = R.stack_position(cols)
+    exp = ro.stack_position(cols)
+    assert G.same_bytes(got, exp)
+    tcols = [torch.from_numpy(c).cuda() for c in cols]
+    tgot = R.stack_position(tcols)
+    assert tgot.is_cuda and G.same_bytes(tgot.cpu().numpy(), exp)
+    back = R.unstack_position(got)
+    ref = ro.unstack_position(exp, dim)
+    assert len(back) == dim and all(G.same_bytes(a, b) for a, b in zip(back, ref))
+    tback = R.unstack_position(tgot)
+    assert all(G.same_bytes(a.cpu().numpy(), b) for a, b in zip(tback, ref))
+    # the stacked array feeds redistribute_by_position like any (N, d) position
+    p2 = got.copy()
+    out = R.redistribute_by_position(np.arange(1000), p2)
+    assert np.array_equal(out, np.arange(1000))
+
+
+def test_scan_failure_is_loud():
+    """A look-back that gives up (knob scan_spins = -1) must not yield wrong
+    offsets: the counts come back -1, the pack writes nothing, and the API
+    raises at its count read."""
+    n = 1 << 20
+    pos, rec = mgr.synth_uniform(n, seed=5)
+    P = GridPartitioner([2, 2, 2], [1.0] * 3)
+    _lib.tune("scan_spins", -1)
+    try:
+        out, counts = P.partition_device(rec.reshape(-1), 32, pos)
+        out.fill_(0xAB)
+        out, counts = P.partition_device(rec.reshape(-1), 32, pos)
+        torch.cuda.synchronize()
+        assert (counts.cpu().numpy() == -1).all()
+        assert bool((out == 0xAB).all())                  # nothing was written
+        with pytest.raises(_lib.MgrError, match="scan failed"):
+            P.partition_by_position(rec.cpu().numpy(), pos.cpu().numpy())
+    finally:
+        _lib.tune("scan_spins", 1 << 24)
+    out, counts = P.partition_device(rec.reshape(-1), 32, pos)
+    assert (counts.cpu().numpy() > 0).all()
+
+
+def test_single_rank_scan_failure_raises():
+    pos, rec = mgr.synth_uniform(1 << 20, seed=6)
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    _lib.tune("scan_spins", -1)
+    try:
+        with pytest.raises(_lib.MgrError, match="scan failed"):
+            R.redistribute_by_cell_number(rec, torch.zeros(1 << 20, dtype=torch.int64,
+                                                           device="cuda"))
+    finally:
+        _lib.tune("scan_spins", 1 << 24)
+
+
+def test_no_device_allocation_after_warmup():
+    """Skewed inputs of changing size on repeated calls: after warm-up the
+    redistributor reuses its scratch (workspace, destination bytes, send
+    buffers) and the caching allocator serves the fresh outputs -- no new
+    device segment (hipMalloc) per call."""
+    from mpi_grid_redistribute_amd.redistributor import Scratch
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    assert isinstance(R._scratch, Scratch)
+    base = 1 << 22
+    inputs = []
+    for k in range(6):
+        n = base - 10_000 * k
+        pos, rec = mgr.synth_clustered(n, seed=k)
+        inputs.append((pos, rec))
+    for pos, rec in inputs[:2]:
+        R.redistribute_by_position(rec, pos)
+    torch.cuda.synchronize()
+    seg0 = torch.cuda.memory_stats()["segment.all.allocated"]
+    for pos, rec in inputs[2:]:
+        out = R.redistribute_by_position(rec, pos)
+        del out
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_stats()["segment.all.allocated"] == seg0

@@ -103,36 +103,6 @@ def test_cell_number_from_indexes():
 
 
 # ------------------------------------------------- multi-rank (threads)
-def _fixture_inputs(f, case, size, as_torch):
-    pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
-    if bool(f["alias"]):
-        data = pos
-    elif "view" in case:
-        data = [d.copy() for d in G.per_rank(f, "data", size)]
-        pos = [d["pos"] for d in data]
-    else:
-        data = [d.copy() for d in G.per_rank(f, "data", size)]
-    if not as_torch:
-        return data, pos
-    tdata, tpos = [], []
-    for r in range(size):
-        if bool(f["alias"]):
-            t = torch.from_numpy(pos[r]).cuda()
-            tdata.append(t)
-            tpos.append(t)
-        elif "view" in case:
-            raw = torch.from_numpy(data[r].view(np.uint8).reshape(len(data[r]), -1)).cuda()
-            tdata.append(raw)
-            tpos.append(raw.view(torch.float32)[:, :3])
-        else:
-            d = data[r]
-            if d.dtype.names:
-                d = d.view(np.uint8).reshape(len(d), -1)
-            tdata.append(torch.from_numpy(np.ascontiguousarray(d)).cuda())
-            tpos.append(torch.from_numpy(pos[r]).cuda())
-    return tdata, tpos
-
-
 def _as_bytes(x):
     if isinstance(x, torch.Tensor):
         return x.cpu().contiguous().numpy().view(np.uint8).reshape(-1)
@@ -145,7 +115,7 @@ def test_redistribute_golden_threads(case, as_torch):
     f = G.load(case)
     size = int(f["size"])
     topo, box, periodic = f["topology"], f["box"], bool(f["periodic"])
-    data, pos = _fixture_inputs(f, case, size, as_torch)
+    data, pos = G.fixture_inputs(f, case, size, as_torch)
 
     def fn(comm, r):
         R = MPIGridRedistributor(comm, topo, box)

@@ -1,8 +1,8 @@
 """GPU parity of every kernel variant the tuning knobs select (mgr_tune).
 
 The shipped defaults are covered by test_gpu_parity.py; here each non-default
-variant (destination-sorted LDS pack, XCD-contiguous tile order, unconditional
-position write-back) must give the same bytes on the same inputs: the C
+variant (XCD-contiguous tile order, unconditional position write-back, tile
+shapes, scan chunking, the generic pack) must give the same bytes on the same inputs: the C
 oracle on seeded inputs, and the reference's own golden fixtures.
 """
 import numpy as np
@@ -18,34 +18,26 @@ pytestmark = pytest.mark.gpu
 mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
-DEFAULTS = {"pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_coop": 1,
-            "pack_small": 1, "pack_nt": 0, "many_rows": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1, "pack_many": 1,
-            "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
+DEFAULTS = {"xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "pack_coop": 1,
+            "pack_nt": 0, "many_rows": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1,
+            "pack_many": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
             "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1}
 VARIANTS = [
-    {"pack_sorted": 1},
-    {"pack_sorted": 1, "xcd_pack": 1, "xcd_bin": 1},
     {"xcd_pack": 1, "xcd_bin": 1},
     {"bin_skip_clean": 0},
-    {"pack_sorted": 1, "tile_rounds": 8},
-    {"pack_sorted": 1, "pack_nt": 1},
+    {"tile_rounds": 8},
     {"bin_waves": 16, "xcd_pack": 1},
     {"bin_waves": 8, "bin_skip_clean": 0},
-    {"bin_depth": 2, "bin_waves": 2},
-    {"bin_depth": 2, "bin_skip_clean": 0, "bin_staged": 0},
-    {"bin_depth": 2, "bin_waves": 1, "xcd_bin": 1},
-    {"bin_depth": 1, "xcd_pack": 0},
-    {"bin_depth": 2, "bin_waves": 2},
-    {"bin_depth": 1, "bin_waves": 4},
+    {"bin_waves": 2},
+    {"bin_skip_clean": 0, "bin_staged": 0},
+    {"bin_waves": 1, "xcd_bin": 1},
+    {"xcd_pack": 0},
     {"pack_rpw": 2},
     {"pack_nt": 2},
-    {"pack_rpw": 2, "pack_nt": 1, "bin_depth": 1},
+    {"pack_rpw": 2, "pack_nt": 1},
     {"pack_coop": 0},
     {"pack_coop": 0, "pack_nt": 2},
-    {"pack_small": 0},
     {"pack_many": 0},
-    {"scan_onepass": 0},
-    {"scan_onepass": 0, "tile_rounds": 1},
     {"tile_rounds": 1},
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},
