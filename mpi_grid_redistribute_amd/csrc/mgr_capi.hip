@@ -322,7 +322,7 @@ int mgr_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest, in
     if (row_bytes < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes);
     if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
     if (n > 0 && (!src || !dest || !workspace)) return fail(MGR_EINVAL, "null argument");
-    if (redirect_bin >= 0 && !redirect_dst) return fail(MGR_EINVAL, "redirect without buffer");
+    if (n > 0 && redirect_bin >= 0 && !redirect_dst) return fail(MGR_EINVAL, "redirect without buffer");
     if (redirect_bin >= nbins) return fail(MGR_EINVAL, "redirect_bin out of range");
     const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
     HIP_OK(mgr::launch_pack(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
@@ -599,6 +599,7 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
+    else if (!strcmp(key, "pack_fine")) mgr::g_tune.pack_fine = (int)value;
     else if (!strcmp(key, "pack_img")) mgr::g_tune.pack_img = (int)value;
     else if (!strcmp(key, "pack_sel")) mgr::g_tune.pack_sel = (int)value;
     else if (!strcmp(key, "pack_compact")) mgr::g_tune.pack_compact = (int)value;

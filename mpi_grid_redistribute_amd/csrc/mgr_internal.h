@@ -19,9 +19,8 @@ constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups)
 // zeroed with them by every count producer.
 struct ScanCtl {
     uint32_t ticket;   // chunk ids in dispatch order (atomic ticket)
-    uint32_t done;     // chunks that have written their offsets
     uint32_t err;      // nonzero: a look-back timed out; packs then write nothing
-    uint32_t pad;
+    uint64_t done;     // chunks that wrote their offsets (bits 0-31), failed ones (32-63)
 };
 constexpr int kScanCtlWords = sizeof(ScanCtl) / 8;
 
@@ -106,6 +105,7 @@ struct Tune {
     int bin_skip_clean = 1;  // write a position slab back only if a row changed
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
     int xcd_pack = 1;      // ... in the pack kernels
+    int pack_fine = 1;     // sorted-image pack for 65..1024 bins (4-byte-multiple rows)
     int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)

@@ -150,9 +150,14 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
         }
     }
     __syncthreads();
+    // one word counts the finished chunks (bits 0-31) and the failed ones
+    // (bits 32-63): relaxed atomics on ONE location are seen in order, so no
+    // fences (a release here costs an L2 write-back per workgroup)
+    constexpr uint64_t kDoneMask = 0xFFFFFFFFull;
     if (j != (int)gridDim.x - 1) {
         if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(&ctl->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ctl->done, 1ull + (s_poison ? (1ull << 32) : 0ull),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     // The last ticket: wait until every other chunk is done (all of them hold
@@ -160,16 +165,19 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
     // every bin's total from the inclusive prefixes at the bin ends -- or -1
     // everywhere when any look-back gave up.
     if (threadIdx.x == 0) {
-        const unsigned others = gridDim.x - 1;
+        const uint64_t others = gridDim.x - 1;
         int spin = 0;
-        while (__hip_atomic_load(&ctl->done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < others) {
+        uint64_t v;
+        while (((v = __hip_atomic_load(&ctl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
+                kDoneMask) < others) {
             if (spins < 0 || ++spin > (1 << 26)) {   // a lost chunk: fail loudly
+                v |= 1ull << 32;
                 __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
         }
-        if (__hip_atomic_load(&ctl->err, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) s_poison = 1;
+        if (v >> 32) s_poison = 1;
     }
     __syncthreads();
     const bool failed = s_poison != 0;

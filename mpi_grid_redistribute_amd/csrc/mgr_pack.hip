@@ -428,6 +428,13 @@ static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const
 // store instructions per round instead of ~RB/16.
 typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+// Store through an address held as an integer: a global-address-space
+// pointer, so the compiler emits global_store (a plain pointer would be flat).
+template <typename T>
+__device__ __forceinline__ void gstore(unsigned long long a, const T& v) {
+    *(__attribute__((address_space(1))) T*)a = v;
+}
+
 template <int RB>
 __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
@@ -528,14 +535,14 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
             const int last = min(x + 15, nbytes - 1);
             if (x + 16 <= nbytes && ibin[last / RB] == bf) {
                 const unsigned long long a = gaddr[bf];
-                if (a) *(u32x4_a4*)(a + x) = q;
+                if (a) gstore<u32x4_a4>(a + x, q);
             } else {
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
                     const int xd = x + 4 * d;
                     if (xd < nbytes) {
                         const unsigned long long a = gaddr[ibin[xd / RB]];
-                        if (a) *(uint32_t*)(a + xd) = q[d];
+                        if (a) gstore<uint32_t>(a + xd, q[d]);
                     }
                 }
             }
@@ -636,6 +643,215 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     }
 }
 
+// Sorted-image pack for many destinations (65..1024 bins: the 512 fine cells
+// of config 5) and rows of RB bytes (a 4-byte multiple <= 64).
+//
+// Why: with hundreds of bins a round's 64 rows go to ~60 places, so a pack
+// that stores each round straight to its slots (pack_many_kernel) issues
+// store instructions whose 64 lanes touch ~60 different cache lines -- the
+// address pipeline, not HBM, bounds it, and runs of ~4 rows leave
+// half-written lines behind.  Here a workgroup sorts its whole tile by bin
+// in LDS first (stable: wave-private running counts per bin, a prefix over
+// the waves, a scan over the bins) and then streams the sorted image out in
+// 16-byte units, so one store instruction writes 1 KiB of a few contiguous
+// runs.  Persistent: one 1024-thread workgroup per CU (the image fills most
+// of the LDS) walks its XCD's tiles, the 32 workgroups of an XCD on 32
+// adjacent tiles at a time (the lines their runs share meet in one L2), and
+// the next tile's rows are loaded into registers while the current image is
+// stored.
+//
+// LDS: image [TR * RB] | bin of every image row u16 [TR] | wave-private
+// counts u16 [16][nb] | per-bin output base (u64) [nb] | tile bin start [nb].
+typedef unsigned int u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
+typedef unsigned int u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+
+template <int NDW>
+__device__ __forceinline__ void load_row_dw(const uint8_t* __restrict__ p, uint32_t (&v)[NDW]) {
+    int i = 0;
+#pragma unroll
+    for (; i + 4 <= NDW; i += 4) {
+        const u32x4_a4 x = *(const u32x4_a4*)(p + 4 * i);
+        v[i] = x[0]; v[i + 1] = x[1]; v[i + 2] = x[2]; v[i + 3] = x[3];
+    }
+    if constexpr (NDW % 4 == 3) {
+        const u32x3_a4 x = *(const u32x3_a4*)(p + 4 * i);
+        v[i] = x[0]; v[i + 1] = x[1]; v[i + 2] = x[2];
+    } else if constexpr (NDW % 4 == 2) {
+        const u32x2_a4 x = *(const u32x2_a4*)(p + 4 * i);
+        v[i] = x[0]; v[i + 1] = x[1];
+    } else if constexpr (NDW % 4 == 1) {
+        v[i] = *(const uint32_t*)(p + 4 * i);
+    }
+}
+
+constexpr int kFineTR = 2048;      // rows per tile (32 rounds)
+constexpr int kFineWaves = 16;     // 1024 threads, 2 rounds per wave
+static int fine_tile_rows() { return kFineTR; }
+
+__host__ __device__ inline int fine_lds_bytes(int rb, int nb) {
+    return align16(kFineTR * rb) + align16(kFineTR * 2) + align16(kFineWaves * nb * 2) + nb * 8 +
+           nb * 4;
+}
+
+template <int RB, typename DestT>
+__global__ __launch_bounds__(1024) void pack_fine_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const DestT* __restrict__ dest, int nb,
+    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ bin_starts, int64_t T, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, const uint32_t* __restrict__ scan_err) {
+    static_assert(RB % 4 == 0 && RB <= 64, "fine pack row size");
+    constexpr int TR = kFineTR, NW = kFineWaves, RPW = TR / 64 / NW;
+    constexpr int NDW = RB / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* img = (uint32_t*)smem;
+    uint8_t* p = smem + align16(TR * RB);
+    uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
+    uint16_t* wtab = (uint16_t*)p;                 p += align16(NW * nb * 2);
+    unsigned long long* gaddr = (unsigned long long*)p;  p += nb * 8;
+    int* lstart = (int*)p;
+    __shared__ int s_wsum[NW];
+    if (scan_failed(scan_err)) return;
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    // this workgroup's tiles: XCD x = blockIdx % 8 owns tiles [x*per, (x+1)*per);
+    // its G/8 workgroups take them G/8 at a time, adjacent ones together
+    const int64_t per = (T + 7) >> 3;
+    const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3);
+    const int64_t first = (int64_t)(blockIdx.x & 7) * per, last = min(T, first + per);
+    // thread tid < nb owns bin tid: its base correction for the redirect
+    // (tile-independent, seg_start) and its output buffer
+    const int mb = min(tid, nb - 1);
+    long long adj = 0;
+    if (redirect_bin >= 0) {
+        if (mb == redirect_bin) adj = bin_starts[mb];
+        else if (mb > redirect_bin) adj = bin_starts[redirect_bin + 1] - bin_starts[redirect_bin];
+    }
+    uint8_t* const obase = mb == redirect_bin ? redirect_dst : dst;
+    for (int i = tid; i < NW * nb; i += 1024) wtab[i] = 0;
+
+    // Everything a tile needs from HBM -- its rows, their bins, the tile's
+    // segment start of bin tid -- in one register set; two sets, so the next
+    // tile's loads are in flight a whole tile ahead.  The loads are
+    // unconditional (row index clamped to the last row, tile to the last
+    // tile): no loaded register is merged across a branch, which would make
+    // the compiler wait for it (and every older store) on the spot.
+    struct Set {
+        uint32_t v[RPW][NDW];
+        unsigned b[RPW];
+        long long seg;
+    };
+    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        t = min(t, last - 1);
+        S.seg = offsets[(int64_t)mb * T + t];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
+            S.b[q] = (unsigned)dest[row];
+            load_row_dw<NDW>(src + row * RB, S.v[q]);
+        }
+    };
+    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        const int tr = (int)min((int64_t)TR, n - t * TR);   // rows of this tile
+        // 1. wave-private running counts (wtab zeroed at the end of the last
+        //    tile): a row's rank among its wave's rows of its bin
+        int lr[RPW];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const bool valid = (w * RPW + q) * 64 + lane < tr;
+            const unsigned long long peers = match_bin(S.b[q], valid, nbits);
+            const int rk = rank_in(peers);
+            const int before = valid ? (int)wtab[w * nb + S.b[q]] : 0;
+            wave_sync();
+            if (valid && rk == 0) wtab[w * nb + S.b[q]] = (uint16_t)(before + __popcll(peers));
+            wave_sync();
+            lr[q] = before + rk;
+        }
+        __syncthreads();
+        // 2. per bin: exclusive prefix over the waves (the 16 counts read
+        //    first: independent LDS reads), then the bins' starts in the tile
+        int total = 0;
+        if (tid < nb) {
+#pragma unroll
+            for (int w0 = 0; w0 < NW; w0 += 4) {
+                int c[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) c[k] = wtab[(w0 + k) * nb + tid];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    wtab[(w0 + k) * nb + tid] = (uint16_t)total;
+                    total += c[k];
+                }
+            }
+        }
+        int incl = total;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_wsum[w] = incl;
+        __syncthreads();
+        int wpre = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) wpre += ww < w ? s_wsum[ww] : 0;
+        if (tid < nb) {
+            const int ls = wpre + incl - total;
+            lstart[tid] = ls;
+            gaddr[tid] = tid == drop_bin
+                             ? 0ull
+                             : (unsigned long long)(obase + (S.seg - adj - ls) * (long long)RB);
+        }
+        __syncthreads();
+        // 3. rows into the sorted image
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            if ((w * RPW + q) * 64 + lane < tr) {
+                const int lpos = lstart[S.b[q]] + wtab[w * nb + S.b[q]] + lr[q];
+#pragma unroll
+                for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
+                ibin[lpos] = (uint16_t)S.b[q];
+            }
+        }
+        __syncthreads();
+        // 4. stream the image out in 16-byte units; zero the counts for the
+        //    next tile on the way
+        for (int i = tid; i < NW * nb; i += 1024) wtab[i] = 0;
+        const int nbytes = tr * RB;
+        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
+            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
+            const int bf = ibin[x / RB];
+            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+                const unsigned long long a = gaddr[bf];
+                if (a) gstore<u32x4_a4>(a + x, q);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) {
+                        const unsigned long long a = gaddr[ibin[xd / RB]];
+                        if (a) gstore<uint32_t>(a + xd, q[d]);
+                    }
+                }
+            }
+        }
+        __syncthreads();   // the image, ibin and gaddr are reused by the next tile
+    };
+    Set A, B;
+    int64_t t = first + kx;
+    if (t >= last) return;
+    load(A, t);
+    __syncthreads();   // wtab zeroed
+    for (;;) {
+        load(B, t + gx);
+        process(A, t);
+        t += gx;
+        if (t >= last) break;
+        load(A, t + gx);
+        process(B, t);
+        t += gx;
+        if (t >= last) break;
+    }
+}
+
 // ============================================================ launchers
 // pack_many_kernel: super-rounds of 64 * R rows (the uint16 [R][nbins] LDS
 // table stays <= 128 KiB at 4096 rows and 1024 bins), many_super super-rounds
@@ -661,6 +877,9 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // histogram small next to the payload.
     if (nbins <= 16) return 512 * g_tune.pack_rpw;
     if (nbins <= 64) return 1024 * g_tune.pack_rpw;
+    // sorted-image pack: 2048-row tiles (its LDS image), rows of 4-byte multiples
+    if (g_tune.pack_fine && nbins <= 1024 && row_bytes <= 64 && row_bytes % 4 == 0)
+        return fine_tile_rows();
     if (g_tune.pack_many && nbins <= 1024 && row_bytes <= 64) return many_tile_rows(nbins);
     int r = 16;
     while (r < 4096 / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
@@ -806,6 +1025,62 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
     return hipGetLastError();
 }
 
+static int g_cus = 0;   // compute units of the current device (persistent grids)
+static int device_cus() {
+    if (g_cus <= 0) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+            g_cus = c;
+        if (g_cus <= 0) g_cus = 256;
+    }
+    return g_cus;
+}
+
+template <int RB, typename DestT>
+static hipError_t pack_fine_t(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
+                              const Workspace& ws, void* dst, int redirect_bin, void* redirect_dst,
+                              hipStream_t s) {
+    auto k = pack_fine_kernel<RB, DestT>;
+    const int lds = fine_lds_bytes(RB, nb);
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    ensure_lds(k, lds);
+    // one workgroup per CU (the LDS holds one image), a multiple of 8 (XCDs)
+    int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
+    const int64_t need = (ws.T + 7) / 8 * 8;
+    if (grid > need) grid = need;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s, (const uint8_t*)src, n,
+                       (const DestT*)dest, nb, nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts,
+                       ws.T, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, ws.scan_err);
+    return hipGetLastError();
+}
+
+// 65..1024 bins, rows of 4-byte multiples <= 64 bytes, every base 4-byte
+// aligned: the sorted-image pack.
+static hipError_t pack_fine(const void* src, int64_t row_bytes, int64_t n, const void* dest,
+                            int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
+                            int redirect_bin, void* redirect_dst, hipStream_t s) {
+    uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
+    if (redirect_dst) a |= (uintptr_t)redirect_dst;
+    if (!g_tune.pack_fine || nb <= 64 || nb > 1024 || (a & 3) || row_bytes > 64 ||
+        tile_rows != kFineTR)
+        return hipErrorNotSupported;
+    const bool d8 = dest_bytes(nb) == 1;
+#define MGR_PF(RB_)                                                                              \
+    case RB_:                                                                                    \
+        return d8 ? pack_fine_t<RB_, uint8_t>(src, n, dest, nb, drop_bin, ws, dst, redirect_bin, \
+                                              redirect_dst, s)                                   \
+                  : pack_fine_t<RB_, uint16_t>(src, n, dest, nb, drop_bin, ws, dst, redirect_bin, \
+                                               redirect_dst, s);
+    switch ((int)row_bytes) {
+        MGR_PF(4) MGR_PF(8) MGR_PF(12) MGR_PF(16) MGR_PF(20) MGR_PF(24) MGR_PF(28) MGR_PF(32)
+        MGR_PF(36) MGR_PF(40) MGR_PF(44) MGR_PF(48) MGR_PF(52) MGR_PF(56) MGR_PF(60) MGR_PF(64)
+        default: break;
+    }
+#undef MGR_PF
+    return hipErrorNotSupported;
+}
+
 // Rows of 24..60 (pack_img 2: 12..60) bytes, 4-byte multiples but not 16-byte ones: the
 // image pack (16-byte global accesses) when the source is 16-byte aligned,
 // the outputs 4-byte aligned, <= 64 bins and <= 16 waves per tile.
@@ -873,6 +1148,9 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
         else if ((a & 3) == 0) e = compact_t<4>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
         else e = compact_t<1>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
     }
+    if (e == hipErrorNotSupported)
+        e = pack_fine(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
+                      redirect_dst, s);
     if (e == hipErrorNotSupported)
         e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
                      redirect_dst, s);

@@ -61,8 +61,9 @@ def plan_layout(send_counts, recv_counts, rank, redirect_self):
 def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=None,
              scratch=None):
     """Run steps 1-4.  ``bin_counts``: int64 tensor [size] of rows per
-    destination (on ``device``).  ``pack(field, send, redirect_bin,
-    redirect_out)`` packs field ``field``.  ``extra_rows(total_recv)``: spare
+    destination (on ``device``).  ``pack(field, send, redirect_bin, out,
+    out_offset)`` packs field ``field`` (the redirect bin's rows into ``out``
+    from byte ``out_offset``).  ``extra_rows(total_recv)``: spare
     rows to allocate after the received ones (the halo appends there).
     ``scratch(name, nbytes)``: a reusable device buffer (the send buffers),
     else fresh allocations.  Returns (outs, layout); outs are new flat uint8
@@ -79,9 +80,9 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
         snd = (scratch(f"send{f}", nbytes) if scratch is not None
                else torch.empty(nbytes, dtype=torch.uint8, device=device))
         if lay.redirect_self:
-            pack(f, snd, rank, out[int(lay.recv_offsets[rank]) * rb:])
+            pack(f, snd, rank, out, int(lay.recv_offsets[rank]) * rb)
         else:
-            pack(f, snd, -1, None)
+            pack(f, snd, -1, None, 0)
         outs.append(out)
         sends.append(snd)
     transport.exchange_rows(sends, outs, list(row_bytes), sc, lay.send_offsets, rc,

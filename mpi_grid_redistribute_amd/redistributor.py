@@ -393,11 +393,13 @@ class MPIGridRedistributor:
         bin_counts = torch.empty(nb, dtype=torch.int64, device=self._dev)
         _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(bin_counts), stream)
 
-        def pack(f, snd, redirect_bin, redirect_out):
+        def pack(f, snd, redirect_bin, out, out_offset):
             fld = fields[f]
+            # address arithmetic, not a slice: an empty tail slice has no data pointer
+            red = ctypes.c_void_p(out.data_ptr() + out_offset if out is not None else 0)
             _lib.call("mgr_pack", _lib.ptr(fld.flat), fld.row_bytes, n, _lib.ptr(dest), nb,
                       P if drop else -1, tile_rows, _lib.ptr(ws), _lib.ptr(snd), redirect_bin,
-                      _lib.ptr(redirect_out), stream)
+                      red, stream)
 
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
                              self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get)

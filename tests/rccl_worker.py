@@ -29,6 +29,7 @@ SHARED = os.environ.get("MGR_TEST_SHARED_GPU") == "1"
 if SHARED:   # before anything loads RCCL
     os.environ["NCCL_HOSTID"] = f"mgr-test-rank-{RANK}"
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_DEBUG", "WARN")
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
@@ -171,8 +172,10 @@ def main():
     results = {}
     dev = 0 if SHARED else RANK
     torch.cuda.set_device(dev)
+    log("init gloo")
     dist.init_process_group("gloo", rank=RANK, world_size=WORLD)
     import mpi_grid_redistribute_amd as mgr
+    log("creating RcclComm")
     comm = mgr.RcclComm.from_torch_distributed()
     log(f"RcclComm up (device {dev}, shared={SHARED})")
     cases = []

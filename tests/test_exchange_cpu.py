@@ -41,7 +41,8 @@ def oracle_pack(data, dest, size, rb):
     part, off = c_oracle.partition(data, dest, size)
     raw = part.view(np.uint8).reshape(-1)
 
-    def pack(f, snd, redirect_bin, redirect_out):
+    def pack(f, snd, redirect_bin, out, out_offset):
+        redirect_out = out[out_offset:] if out is not None else None
         # mgr_pack semantics: the redirect bin goes to redirect_out from row 0,
         # the bins after it close its gap in the send buffer
         for b in range(size):
@@ -233,8 +234,8 @@ def test_rccl_schedule_exchange(size, empty_rank, drop):
         ids2 = (np.arange(len(data[r]), dtype=np.int32) + 7 * r).view(np.uint8).reshape(-1, 4)
         pack1, _ = oracle_pack(ids2, dest, size, 4)
 
-        def pack(f, snd, redirect_bin, redirect_out):
-            (pack0 if f == 0 else pack1)(f, snd, redirect_bin, redirect_out)
+        def pack(f, snd, redirect_bin, out, out_offset):
+            (pack0 if f == 0 else pack1)(f, snd, redirect_bin, out, out_offset)
 
         t = SimRcclComm(world, r)
         outs, lay = exchange(t, [rb, 4], counts, r, "cpu", pack)

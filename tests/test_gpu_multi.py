@@ -24,7 +24,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TIMEOUT_S = 300
+TIMEOUT_S = int(os.environ.get("MGR_MULTI_TIMEOUT", "300"))
 
 
 def _free_port():
@@ -41,15 +41,20 @@ def test_rccl_multi_rank(world, tmp_path):
         pytest.skip("needs a GPU")
     shared = torch.cuda.device_count() < world
     port = _free_port()
-    procs = []
+    # worker logs go to files (gpurun_out/ on the GPU box: progress stays visible)
+    logdir = os.path.join(ROOT, "gpurun_out") if os.environ.get("GRAFT_REPO_ROOT") else str(tmp_path)
+    os.makedirs(logdir, exist_ok=True)
+    procs, logs = [], []
     for r in range(world):
         env = dict(os.environ)
         env.update(RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    MGR_TEST_OUT=str(tmp_path / f"rank{r}.json"),
                    MGR_TEST_SHARED_GPU="1" if shared else "0")
+        logs.append(open(os.path.join(logdir, f"multi_w{world}_rank{r}.log"), "w"))
         procs.append(subprocess.Popen([sys.executable, "-u", "-m", "tests.rccl_worker"], cwd=ROOT,
-                                      env=env, start_new_session=True))
+                                      env=env, start_new_session=True, stdout=logs[-1],
+                                      stderr=subprocess.STDOUT))
     codes = []
     try:
         for p in procs:
@@ -61,6 +66,9 @@ def test_rccl_multi_rank(world, tmp_path):
         for p in procs:
             p.wait()
         pytest.fail(f"world {world}: ranks did not finish within {TIMEOUT_S} s")
+    finally:
+        for fh in logs:
+            fh.close()
     failures = {}
     for r in range(world):
         path = tmp_path / f"rank{r}.json"

@@ -45,7 +45,7 @@ def main():
     _lib.profile_enable(False)
     out = {"n": N, "fine": FINE, "variant": json.loads(os.environ.get("FB_VARIANT", "{}")),
            "ms_per_sort": a.elapsed_time(b) / ITERS}
-    for k in ("bin_count", "scan", "scan_reduce", "scan_apply", "bin_totals", "pack"):
+    for k in ("bin_count", "scan", "pack"):
         ms, cnt = _lib.profile_read(k)
         if cnt:
             out[k] = round(ms / cnt, 4)
