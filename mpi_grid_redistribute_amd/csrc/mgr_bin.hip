@@ -20,14 +20,19 @@ constexpr int kStageMaxRowBytes = 64;
 // One workgroup per tile: its waves split the tile's 64-row rounds into
 // contiguous runs (wave w: rows [w*rows_per_wave, ...)), bin them, and add
 // their wave-aggregated counts into one LDS histogram for the tile.
-template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT, int DEPTH>
+// kF: also write every row's fine cell (FineGeom, u16) to fine_out -- the
+// destination-side fine sort of config 5 then needs no second binning pass.
+template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT, int DEPTH,
+          bool kF>
 __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
                                                            int32_t* __restrict__ counts,
                                                            int64_t T, int tile_rows,
                                                            int per_wave_lds, int skip_clean,
-                                                           int xcd, uint64_t* __restrict__ scan_flags) {
+                                                           int xcd, uint64_t* __restrict__ scan_flags,
+                                                           FineGeom fg,
+                                                           uint16_t* __restrict__ fine_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     clear_scan_flags(scan_flags);
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -99,8 +104,12 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             wave_sync();
             unsigned b = 0;
             bool dirty = false;
-            if (valid)
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM>((PosT*)(stage + lane * rb), g, nullptr, &dirty);
+            if (valid) {
+                long long fc = 0;
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM, kF>((PosT*)(stage + lane * rb), g,
+                                                                nullptr, &dirty, &fg, &fc);
+                if (kF) fine_out[row0 + r0 + lane] = (uint16_t)fc;
+            }
             // write the slab back only if a row of it changed (skip_clean)
             if (kPeriodic && (!skip_clean || __ballot(dirty) != 0ull)) {
                 wave_sync();
@@ -141,9 +150,12 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             const bool valid = r0 + lane < rows;
             unsigned b = 0;
             bool dirty = false;
-            if (valid)
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM>(pos + (row0 + r0 + lane) * stride, g,
-                                                             nullptr, &dirty);
+            if (valid) {
+                long long fc = 0;
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM, kF>(pos + (row0 + r0 + lane) * stride,
+                                                                g, nullptr, &dirty, &fg, &fc);
+                if (kF) fine_out[row0 + r0 + lane] = (uint16_t)fc;
+            }
             account(b, valid, r0);
             wave_sync();
         }
@@ -229,11 +241,15 @@ __global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t*
 // ============================================================ launchers
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
-                              int tile_rows, const Workspace& ws, hipStream_t s) {
+                              int tile_rows, const Workspace& ws, hipStream_t s,
+                              const FineGeom* fg, uint16_t* fine_out) {
     // nontemporal slab loads/stores always (every A/B favoured them); one
     // slab in flight per wave (two measured slower with the write-back,
     // DESIGN.md §3.3)
-    auto k = bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1>;
+    auto k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, true>
+                : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, false>;
+    FineGeom f{};
+    if (fg) f = *fg;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
     int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each
@@ -242,60 +258,216 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nwaves), (size_t)lds, s, (PosT*)pos, n,
                        stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave,
-                       g_tune.bin_skip_clean, g_tune.xcd_bin, ws.flags);
+                       g_tune.bin_skip_clean, g_tune.xcd_bin || g.nbins > 64, ws.flags, f,
+                       fine_out);
     return hipGetLastError();
 }
 
 template <typename PosT, bool kP, typename DestT, int NU>
 static hipError_t bin_count_dim(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
-                                int tile_rows, const Workspace& ws, hipStream_t s) {
+                                int tile_rows, const Workspace& ws, hipStream_t s,
+                                const FineGeom* fg, uint16_t* fo) {
     switch (g.dim) {
-        case 1: return bin_count_t<PosT, kP, DestT, NU, 1>(g, pos, n, stride, dest, tile_rows, ws, s);
-        case 2: return bin_count_t<PosT, kP, DestT, NU, 2>(g, pos, n, stride, dest, tile_rows, ws, s);
-        case 3: return bin_count_t<PosT, kP, DestT, NU, 3>(g, pos, n, stride, dest, tile_rows, ws, s);
-        default: return bin_count_t<PosT, kP, DestT, NU, 0>(g, pos, n, stride, dest, tile_rows, ws, s);
+        case 1: return bin_count_t<PosT, kP, DestT, NU, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+        case 2: return bin_count_t<PosT, kP, DestT, NU, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+        case 3: return bin_count_t<PosT, kP, DestT, NU, 3>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+        default: return bin_count_t<PosT, kP, DestT, NU, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
     }
 }
 
 template <typename PosT, bool kP, typename DestT>
 static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
-                              int tile_rows, const Workspace& ws, hipStream_t s) {
+                              int tile_rows, const Workspace& ws, hipStream_t s,
+                              const FineGeom* fg, uint16_t* fo) {
     const int64_t rb = stride * (int64_t)sizeof(PosT);
     if (g_tune.bin_staged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0) {
         switch ((int)((rb + 15) / 16)) {   // 16-byte units per lane per 64-row slab
-            case 1: return bin_count_dim<PosT, kP, DestT, 1>(g, pos, n, stride, dest, tile_rows, ws, s);
-            case 2: return bin_count_dim<PosT, kP, DestT, 2>(g, pos, n, stride, dest, tile_rows, ws, s);
-            case 3: return bin_count_dim<PosT, kP, DestT, 3>(g, pos, n, stride, dest, tile_rows, ws, s);
-            default: return bin_count_dim<PosT, kP, DestT, 4>(g, pos, n, stride, dest, tile_rows, ws, s);
+            case 1: return bin_count_dim<PosT, kP, DestT, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+            case 2: return bin_count_dim<PosT, kP, DestT, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+            case 3: return bin_count_dim<PosT, kP, DestT, 3>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+            default: return bin_count_dim<PosT, kP, DestT, 4>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
         }
     }
-    return bin_count_dim<PosT, kP, DestT, 0>(g, pos, n, stride, dest, tile_rows, ws, s);
+    return bin_count_dim<PosT, kP, DestT, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
 }
 
 template <typename PosT, typename DestT>
 static hipError_t bin_count_p(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
-                              void* dest, int tile_rows, const Workspace& ws, hipStream_t s) {
-    return periodic ? bin_count_w<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s)
-                    : bin_count_w<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s);
+                              void* dest, int tile_rows, const Workspace& ws, hipStream_t s,
+                              const FineGeom* fg, uint16_t* fo) {
+    return periodic ? bin_count_w<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo)
+                    : bin_count_w<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
 }
 
 template <typename PosT>
 static hipError_t bin_count_d(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
-                              void* dest, int tile_rows, const Workspace& ws, hipStream_t s) {
+                              void* dest, int tile_rows, const Workspace& ws, hipStream_t s,
+                              const FineGeom* fg, uint16_t* fo) {
     if (dest_bytes(g.nbins) == 1)
-        return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
-    return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
+        return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fo);
+    return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fo);
 }
 
 hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
-                            hipStream_t s) {
+                            hipStream_t s, const FineGeom* fg, uint16_t* fine_out) {
     if (n <= 0) return hipSuccess;
-    prof_begin(s, K_BIN_COUNT);
-    hipError_t e = pos_f32 ? bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s)
-                           : bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s);
-    prof_end(s, K_BIN_COUNT);
+    const int kid = fg ? K_BIN_FINE : K_BIN_COUNT;
+    prof_begin(s, kid);
+    hipError_t e = pos_f32 ? bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fine_out)
+                           : bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fine_out);
+    prof_end(s, kid);
     return e;
+}
+
+// Tile histogram of u16 bin ids (the fine cells that arrived with the rows,
+// config 5): one workgroup per tile, LDS atomics (counts only, order free),
+// destination-major counts[b * T + tile] for mgr_scan; the ids themselves
+// are the pack's destination array (<= 256 bins: copied to the 1-byte
+// destination array dest8 the pack then reads).
+__global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __restrict__ ids,
+                                                           int64_t n, int nbins,
+                                                           int32_t* __restrict__ counts, int64_t T,
+                                                           int tile_rows,
+                                                           uint64_t* __restrict__ scan_flags,
+                                                           uint8_t* __restrict__ dest8) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    int32_t* hist = (int32_t*)smem;
+    clear_scan_flags(scan_flags);
+    // XCD-contiguous tiles: neighbouring tiles' counts share lines
+    // (counts[b * T + tile]) and merge in one L2 instead of leaving it half-written
+    const int64_t tile = xcd_tile(blockIdx.x, T);
+    for (int b = threadIdx.x; b < nbins; b += kBlock) hist[b] = 0;
+    __syncthreads();
+    const int64_t row0 = tile * (int64_t)tile_rows;
+    const int rows = (int)min((int64_t)tile_rows, n - row0);
+    for (int i = threadIdx.x; i < rows; i += kBlock) {
+        const unsigned v = ids[row0 + i];
+        atomicAdd(&hist[v], 1);
+        if (dest8) dest8[row0 + i] = (uint8_t)v;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbins; b += kBlock) counts[(int64_t)b * T + tile] = hist[b];
+}
+
+// Stable ranks of u16 bin ids (the fine cells at the destination, config 5)
+// for mgr_pack_ranked: one 256-thread workgroup per tile of TR rows (4 waves
+// x RPW rounds, in order).  Per row: its rank among the tile's rows of its
+// bin (ballot match + wave-private running counts + a prefix over the
+// waves); per tile: every bin's start inside the tile (tile_starts[t][b],
+// tile-major, contiguous) and its count (counts[b * T + t], for mgr_scan).
+// The ranking work leaves the pack, which then only places rows.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
+    const uint16_t* __restrict__ ids, int64_t n, int nbins, int nbits,
+    int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ ranks,
+    uint16_t* __restrict__ tile_starts, uint8_t* __restrict__ dest8,
+    uint64_t* __restrict__ scan_flags) {
+    constexpr int NT = NW * 64, RPW_MAX = 4096 / 64 / NW;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint16_t* wt = (uint16_t*)smem;   // [NW][nbins]
+    __shared__ int s_wsum[NW];
+    clear_scan_flags(scan_flags);
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const int64_t tile = xcd_tile(blockIdx.x, T);
+    const int rpw = tile_rows / 64 / NW;
+    for (int i = tid; i < NW * nbins; i += NT) wt[i] = 0;
+    unsigned b[RPW_MAX];
+#pragma unroll
+    for (int q = 0; q < RPW_MAX; ++q) {
+        if (q >= rpw) break;
+        const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
+        b[q] = row < n ? (unsigned)ids[row] : 0u;
+    }
+    __syncthreads();
+    int rk[RPW_MAX];
+#pragma unroll
+    for (int q = 0; q < RPW_MAX; ++q) {
+        if (q >= rpw) break;
+        const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
+        const bool valid = row < n;
+        if (dest8 && valid) dest8[row] = (uint8_t)b[q];
+        const unsigned long long peers = match_bin(b[q], valid, nbits);
+        const int r = rank_in(peers);
+        const int before = valid ? (int)wt[w * nbins + b[q]] : 0;
+        wave_sync();
+        if (valid && r == 0) wt[w * nbins + b[q]] = (uint16_t)(before + __popcll(peers));
+        wave_sync();
+        rk[q] = before + r;
+    }
+    __syncthreads();
+    // per bin (bin k*NT + tid): prefix over the waves (in place), the tile
+    // count; then the bins' starts in the tile (block scan over the bins)
+    int carry = 0;
+    for (int k = 0; k * NT < nbins; ++k) {
+        const int bb = k * NT + tid;
+        int run = 0;
+        if (bb < nbins) {
+            int c[NW];
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) c[ww] = wt[ww * nbins + bb];
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                wt[ww * nbins + bb] = (uint16_t)run;
+                run += c[ww];
+            }
+            counts[(int64_t)bb * T + tile] = run;
+        }
+        int incl = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) s_wsum[w] = incl;
+        __syncthreads();
+        int wpre = 0, wall = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) {
+            const int x = s_wsum[ww];
+            wpre += ww < w ? x : 0;
+            wall += x;
+        }
+        if (bb < nbins) tile_starts[tile * nbins + bb] = (uint16_t)(carry + wpre + incl - run);
+        carry += wall;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < RPW_MAX; ++q) {
+        if (q >= rpw) break;
+        const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
+        if (row < n) ranks[row] = (uint16_t)(wt[w * nbins + b[q]] + rk[q]);
+    }
+}
+
+hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
+                           const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
+                           uint8_t* dest8, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_COUNT_IDS);
+    // 16 waves (2 rounds each at 2048 rows) when the tile allows, else 4
+    const bool wide = tile_rows % (64 * 16) == 0;
+    const int nw = wide ? 16 : kWaves;
+    const int lds = align16(nw * nbins * 2);
+    auto k = wide ? rank_ids_kernel<16> : rank_ids_kernel<kWaves>;
+    ensure_lds(k, lds);
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s, ids, n, nbins,
+                       nbits_for(nbins), ws.counts, ws.T, tile_rows, ranks, tile_starts, dest8,
+                       ws.flags);
+    prof_end(s, K_COUNT_IDS);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
+                            const Workspace& ws, uint8_t* dest8, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_COUNT_IDS);
+    const int lds = align16(nbins * 4);
+    ensure_lds(count_ids_kernel, lds);
+    hipLaunchKernelGGL(count_ids_kernel, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lds, s, ids, n,
+                       nbins, ws.counts, ws.T, tile_rows, ws.flags, dest8);
+    prof_end(s, K_COUNT_IDS);
+    return hipGetLastError();
 }
 
 template <typename PosT>

@@ -95,7 +95,8 @@ void collect_locked() {
 const char* kernel_name(int k) {
     static const char* names[K_NUM_KERNELS] = {"bin_count", "scan", "pack", "cell_ids",
                                                "bin_ids", "cellnum_idx", "synth",
-                                               "exchange", "halo"};
+                                               "exchange", "halo", "bin_fine", "count_ids",
+                                               "pack_fine", "pack_narrow"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -263,6 +264,88 @@ int mgr_bin_count(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int
     return MGR_OK;
 }
 
+int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* pos, int pos_dtype,
+                       int64_t n, int64_t row_stride, int periodic, void* dest,
+                       uint16_t* fine_ids, int tile_rows, void* workspace, void* stream) {
+    int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
+    if (rc) return rc;
+    if ((rc = check_tile(tile_rows))) return rc;
+    if (!fine_plan || !fine_plan->g.fine) return fail(MGR_EINVAL, "fine_plan is not a fine-cell plan");
+    if (fine_plan->g.dim != plan->g.dim) return fail(MGR_EINVAL, "plans of different dimensions");
+    for (int d = 0; d < plan->g.dim; ++d)
+        if (memcmp(&fine_plan->g.L[d], &plan->g.L[d], sizeof(double)) ||
+            fine_plan->g.n[d] != plan->g.n[d] * fine_plan->g.fmod[d] ||
+            fine_plan->g.compute_f32 != plan->g.compute_f32)
+            return fail(MGR_EINVAL, "fine_plan is not over this plan's box and topology (dim %d)", d);
+    if (n > 0 && (!dest || !workspace || !fine_ids)) return fail(MGR_EINVAL, "null dest/fine_ids/workspace");
+    mgr::Geom g = plan->g;
+    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    mgr::FineGeom fg;
+    memset(&fg, 0, sizeof fg);
+    for (int d = 0; d < g.dim; ++d) {
+        fg.nd[d] = fine_plan->g.nd[d];
+        fg.n[d] = fine_plan->g.n[d];
+        fg.fmod[d] = fine_plan->g.fmod[d];
+        fg.off[d] = fine_plan->g.off[d];
+    }
+    fg.nbins = fine_plan->g.nbins;
+    const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
+    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
+                                 tile_rows, ws, (hipStream_t)stream, &fg, fine_ids));
+    return MGR_OK;
+}
+
+int mgr_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, void* dest,
+                  void* workspace, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    if (n > 0 && (!ids || !workspace)) return fail(MGR_EINVAL, "null argument");
+    if (n > 0 && mgr::dest_bytes(nbins) == 1 && !dest)
+        return fail(MGR_EINVAL, "%d bins: the 1-byte destination array is required", nbins);
+    const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
+    HIP_OK(mgr::launch_count_ids(ids, n, nbins, tile_rows, ws,
+                                 mgr::dest_bytes(nbins) == 1 ? (uint8_t*)dest : nullptr,
+                                 (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint16_t* ranks,
+                 uint16_t* tile_starts, void* workspace, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (tile_rows % (64 * mgr::kWaves) || tile_rows > 4096)
+        return fail(MGR_EINVAL, "tile_rows %d: a multiple of 256 <= 4096", tile_rows);
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    if (n > 0 && (!ids || !ranks || !tile_starts || !workspace)) return fail(MGR_EINVAL, "null argument");
+    const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
+    HIP_OK(mgr::launch_rank_ids(ids, n, nbins, tile_rows, ws, ranks, tile_starts, nullptr,
+                                (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
+                    const uint16_t* ranks, const uint16_t* tile_starts, int nbins, int tile_rows,
+                    const void* workspace, void* dst, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (row_bytes < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes);
+    if (n > 0 && (!src || !ids || !ranks || !tile_starts || !workspace || !dst))
+        return fail(MGR_EINVAL, "null argument");
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
+    const hipError_t e = mgr::launch_pack_ranked(src, row_bytes, n, ids, ranks, tile_starts, nbins,
+                                                 tile_rows, ws, dst, (hipStream_t)stream);
+    if (e == hipErrorNotSupported)
+        return fail(MGR_EUNSUPPORTED, "ranked pack: rows of %lld bytes, tile_rows %d (needs 4-byte "
+                    "multiples <= 64, tile_rows = mgr_tile_rows, 4-byte aligned buffers)",
+                    (long long)row_bytes, tile_rows);
+    HIP_OK(e);
+    return MGR_OK;
+}
+
 int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
                  int periodic, int64_t* cell_out, int64_t* idx_out, void* stream) {
     int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
@@ -327,6 +410,25 @@ int mgr_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest, in
     const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
     HIP_OK(mgr::launch_pack(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
                             redirect_bin, redirect_dst, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_pack_ids(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
+                 int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
+                 void* redirect_dst, const uint16_t* ids_src, uint16_t* ids_dst,
+                 uint16_t* ids_redirect_dst, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (row_bytes < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes);
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (n > 0 && (!src || !dest || !workspace || !ids_src)) return fail(MGR_EINVAL, "null argument");
+    if (n > 0 && redirect_bin >= 0 && (!redirect_dst || !ids_redirect_dst))
+        return fail(MGR_EINVAL, "redirect without buffer");
+    if (redirect_bin >= nbins) return fail(MGR_EINVAL, "redirect_bin out of range");
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
+    HIP_OK(mgr::launch_pack(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
+                            redirect_bin, redirect_dst, (hipStream_t)stream, ids_src, ids_dst,
+                            ids_redirect_dst));
     return MGR_OK;
 }
 

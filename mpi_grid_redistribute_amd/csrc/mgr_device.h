@@ -140,10 +140,13 @@ __device__ __forceinline__ bool same_bits(PosT a, PosT b) {
 // The wrapped value is stored only when its bits differ from the input
 // (the in-place mutation of redist.py:68 / :328-329 is then complete: an
 // in-box coordinate wraps to itself) and *dirty records that a store happened.
-template <typename PosT, bool kPeriodic>
+// kF: also the coordinate's fine index (FineGeom) from the same quotient t/L
+// -- exactly what the fine plan computes from the stored position later.
+template <typename PosT, bool kPeriodic, bool kF = false>
 __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw,
-                                               bool* dirty) {
-    long long k;
+                                               bool* dirty, const FineGeom* fg = nullptr,
+                                               long long* kfine = nullptr) {
+    long long k, kf = 0;
     const PosT in = *p;
     if (sizeof(PosT) == 4 && g.compute_f32) {
         float x = (float)in;
@@ -153,6 +156,7 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
         }
         const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];  // f32 / f32 -> f32
         k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
+        if (kF) kf = trunc_i64((double)q * fg->nd[d]);
     } else {
         double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)in) : (double)in;
         if (kPeriodic) {
@@ -161,28 +165,45 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
             if (!same_bits(w, in)) { *p = w; *dirty = true; }
             x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)w) : (double)w;  // bin reads it (S2)
         }
-        k = trunc_i64((g.pow2[d] ? x * g.invL[d] : x / g.L[d]) * g.nd[d]);
+        const double q = g.pow2[d] ? x * g.invL[d] : x / g.L[d];
+        k = trunc_i64(q * g.nd[d]);
+        if (kF) kf = trunc_i64(q * fg->nd[d]);
     }
     if (raw) *raw = k;
     const long long n = g.n[d];
     if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
     if (g.fine) k %= g.fmod[d];   // fine-cell plan: index inside the rank's cell
+    if (kF) {
+        const long long nf = fg->n[d];
+        if (!(kf >= 0 && kf < nf)) kf = floormod_i64(floormod_i64(kf, nf) + nf, nf);
+        // kf % f without a 64-bit division: kf - f*k when the coarse index k
+        // is kf's cell (always, up to rounding at a cell face), else the
+        // remainder itself
+        const long long f = fg->fmod[d];
+        long long m = kf - f * k;
+        if (!(m >= 0 && m < f)) m = kf % f;
+        *kfine = m;
+    }
     return k;
 }
 
 // DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
-template <typename PosT, bool kPeriodic, int DIM = 0>
+// kF: *fine gets the row's fine cell (row-major over fg->fmod).
+template <typename PosT, bool kPeriodic, int DIM = 0, bool kF = false>
 __device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx,
-                                             bool* dirty) {
-    long long cell = 0;
-    if (DIM > 0) {
+                                             bool* dirty, const FineGeom* fg = nullptr,
+                                             long long* fine = nullptr) {
+    long long cell = 0, fc = 0;
+    const int nd = DIM > 0 ? DIM : g.dim;
 #pragma unroll
-        for (int d = 0; d < DIM; ++d)
-            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr, dirty);
-    } else {
-        for (int d = 0; d < g.dim; ++d)
-            cell += g.off[d] * bin_coord<PosT, kPeriodic>(row + d, g, d, idx ? idx + d : nullptr, dirty);
+    for (int d = 0; d < (DIM > 0 ? DIM : MGR_MAX_DIM); ++d) {
+        if (DIM == 0 && d >= nd) break;
+        long long kf = 0;
+        cell += g.off[d] * bin_coord<PosT, kPeriodic, kF>(row + d, g, d, idx ? idx + d : nullptr,
+                                                          dirty, fg, &kf);
+        if (kF) fc += (long long)((int)fg->off[d] * (int)kf);   // < 4096 fine cells
     }
+    if (kF) *fine = fc;
     return cell;
 }
 

@@ -47,6 +47,18 @@ struct Geom {
     int64_t fmod[MGR_MAX_DIM];           // fine cells per rank cell and dimension
 };
 
+// The fine cells a row falls in, inside its destination's cell (SURVEY f4,
+// config 5): the reference's binning over the global grid topology * fine
+// (n, nd), reduced to k % fmod per dimension, numbered row-major (off).
+// Same box as the plan it travels with; taken from a mgr_plan_create_fine plan.
+struct FineGeom {
+    double nd[MGR_MAX_DIM];
+    int64_t n[MGR_MAX_DIM];
+    int64_t fmod[MGR_MAX_DIM];
+    int64_t off[MGR_MAX_DIM];
+    int nbins;
+};
+
 // Workspace carve for (n, nbins, tile_rows).
 struct Workspace {
     int32_t* counts;     // [nbins][T] destination-major tile histogram
@@ -65,7 +77,8 @@ int nbits_for(int nbins);
 
 // Kernel ids for the profiler.
 enum KernelId { K_BIN_COUNT, K_SCAN, K_PACK, K_CELL_IDS, K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH,
-                K_EXCHANGE, K_HALO, K_NUM_KERNELS };
+                K_EXCHANGE, K_HALO, K_BIN_FINE, K_COUNT_IDS, K_PACK_FINE, K_PACK_NARROW,
+                K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);
@@ -73,7 +86,16 @@ void prof_end(hipStream_t s, int k);
 // Launchers (return hipError_t of the launch; validate arguments before calling).
 hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
-                            hipStream_t s);
+                            hipStream_t s, const FineGeom* fg = nullptr,
+                            uint16_t* fine_out = nullptr);
+hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
+                            const Workspace& ws, uint8_t* dest8, hipStream_t s);
+hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
+                           const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
+                           uint8_t* dest8, hipStream_t s);
+hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
+                              const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
+                              int tile_rows, const Workspace& ws, void* dst, hipStream_t s);
 hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
                            int periodic, int64_t* cell, int64_t* idx, hipStream_t s);
 hipError_t launch_bin_ids(const void* ids, int ids_dtype, int64_t n, int nbins, void* dest,
@@ -84,7 +106,9 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
                        int64_t* bin_counts, hipStream_t s);
 hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                        int nbins, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                       int redirect_bin, void* redirect_dst, hipStream_t s);
+                       int redirect_bin, void* redirect_dst, hipStream_t s,
+                       const uint16_t* ids_src = nullptr, uint16_t* ids_dst = nullptr,
+                       uint16_t* ids_red = nullptr);
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);

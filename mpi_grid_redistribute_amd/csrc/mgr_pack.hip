@@ -87,7 +87,8 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
     int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
-    const uint32_t* __restrict__ scan_err) {
+    const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
+    uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kCoopMaxRounds][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -98,10 +99,12 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     int nr[RPW];
     unsigned b[RPW];
     U v[RPW][UPR];
+    unsigned idv[RPW];   // side field: every row's 2-byte id (fine cell), moved alike
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
         b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+        idv[q] = id_src && lane < nr[q] ? (unsigned)id_src[row0 + 64 * q + lane] : 0u;
     }
     long long tbase = 0;
     if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
@@ -151,6 +154,8 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
         if (lane < nr[q] && (int)b[q] != drop_bin)
             tgt = (base + rank_in(peers[q])) | ((int)b[q] == redirect_bin ? (1ll << 62) : 0ll);
         tbase += cnt[q];
+        if (id_src && tgt >= 0)
+            ((tgt >> 62) ? id_red : id_dst)[tgt & ((1ll << 62) - 1)] = (uint16_t)idv[q];
 #pragma unroll
         for (int k = 0; k < UPR; ++k) {
             const int u = 64 * k + lane;
@@ -441,7 +446,8 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
     int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
-    const uint32_t* __restrict__ scan_err) {
+    const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
+    uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
     constexpr int RBYTES = 64 * RB;                 // one round, a multiple of 16
     constexpr int NU = (RBYTES / 16 + 63) / 64;     // 16-byte units per lane
@@ -461,6 +467,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     const int nbytes = nr * RB;
     const bool valid = lane < nr;
     const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
+    const unsigned idv = id_src && valid ? (unsigned)id_src[row0 + lane] : 0u;   // side field
     long long tbase = 0;
     if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
     const uint8_t* __restrict__ sp = src + row0 * RB;
@@ -513,6 +520,10 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
         uint8_t* base = lane == redirect_bin ? redirect_dst : dst;
         gaddr[lane] = lane == drop_bin ? 0ull
                                        : (unsigned long long)(base + (tbase - excl) * (long long)RB);
+    }
+    if (id_src) {   // the row's output row: its bin's (tile base - round start) + image slot
+        const long long gr = __shfl(tbase - excl, (int)b, 64) + slot;
+        if (valid && (int)b != drop_bin) ((int)b == redirect_bin ? id_red : id_dst)[gr] = (uint16_t)idv;
     }
     uint32_t row[DW];
     if (valid) {
@@ -853,6 +864,19 @@ __global__ __launch_bounds__(1024) void pack_fine_kernel(
 }
 
 // ============================================================ launchers
+// The 2-byte side field of the pack in progress (mgr_pack_ids: the fine
+// cells travelling with config-5 rows).  launch_pack sets it for the
+// duration of one call on the calling thread; the coop and image launchers
+// take it into their kernel and mark it consumed, other paths leave it to a
+// second (2-byte-row) pack.
+struct SideField {
+    const uint16_t* src = nullptr;
+    uint16_t* dst = nullptr;
+    uint16_t* red = nullptr;
+    bool used = false;
+};
+static thread_local SideField t_side;
+
 // pack_many_kernel: super-rounds of 64 * R rows (the uint16 [R][nbins] LDS
 // table stays <= 128 KiB at 4096 rows and 1024 bins), many_super super-rounds
 // per tile (A/B: longer per-bin runs, slower).
@@ -916,10 +940,11 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
                        dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
                        nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,   \
                        (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack,  \
-                       sel, ws.scan_err)
+                       sel, ws.scan_err, t_side.src, t_side.dst, t_side.red)
     // selection packs (2 bins, one dropped: the halo's rows to send) skip
     // the loads of dropped rows; elsewhere loads go out before the bins are known
     const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
+    t_side.used = t_side.src != nullptr;
     if (g_tune.pack_nt >= 2) {
         if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
     } else if (g_tune.pack_nt == 1) {
@@ -1021,7 +1046,9 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
                        (uint8_t*)redirect_dst, g_tune.xcd_pack,
-                       g_tune.pack_sel && nb <= 2 && drop_bin >= 0, ws.scan_err);
+                       g_tune.pack_sel && nb <= 2 && drop_bin >= 0, ws.scan_err, t_side.src,
+                       t_side.dst, t_side.red);
+    t_side.used = t_side.src != nullptr;
     return hipGetLastError();
 }
 
@@ -1057,6 +1084,134 @@ static hipError_t pack_fine_t(const void* src, int64_t n, const void* dest, int 
 
 // 65..1024 bins, rows of 4-byte multiples <= 64 bytes, every base 4-byte
 // aligned: the sorted-image pack.
+// Ranked sorted-image pack (mgr_pack_ranked): pack_fine_kernel without its
+// ranking -- every row's rank inside (tile, bin) and every tile's bin starts
+// come from mgr_rank_ids -- so a tile is: load (a tile ahead), rows into the
+// LDS image at tile_start[bin] + rank, stream the image out.  No ballots, no
+// per-tile count table, three barriers per tile.
+template <int RB>
+__global__ __launch_bounds__(1024) void pack_ranked_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
+    const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
+    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err) {
+    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
+    constexpr int TR = kFineTR, NW = kFineWaves, RPW = TR / 64 / NW;
+    constexpr int NDW = RB / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* img = (uint32_t*)smem;
+    uint8_t* p = smem + align16(TR * RB);
+    uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
+    unsigned long long* gaddr = (unsigned long long*)p;  p += nb * 8;
+    uint16_t* lstart = (uint16_t*)p;
+    if (scan_failed(scan_err)) return;
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const int64_t per = (T + 7) >> 3;
+    const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3);
+    const int64_t first = (int64_t)(blockIdx.x & 7) * per, last = min(T, first + per);
+    const int mb = min(tid, nb - 1);
+    struct Set {
+        uint32_t v[RPW][NDW];
+        unsigned b[RPW];
+        unsigned rk[RPW];
+        long long seg;
+        unsigned ls;
+    };
+    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        t = min(t, last - 1);
+        S.seg = offsets[(int64_t)mb * T + t];
+        S.ls = tile_starts[t * nb + mb];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
+            S.b[q] = ids[row];
+            S.rk[q] = ranks[row];
+            load_row_dw<NDW>(src + row * RB, S.v[q]);
+        }
+    };
+    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        const int tr = (int)min((int64_t)TR, n - t * TR);
+        if (tid < nb) {
+            lstart[tid] = (uint16_t)S.ls;
+            gaddr[tid] = (unsigned long long)(dst + (S.seg - (long long)S.ls) * (long long)RB);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            if ((w * RPW + q) * 64 + lane < tr) {
+                const int lpos = lstart[S.b[q]] + S.rk[q];
+#pragma unroll
+                for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
+                ibin[lpos] = (uint16_t)S.b[q];
+            }
+        }
+        __syncthreads();
+        const int nbytes = tr * RB;
+        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
+            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
+            const int bf = ibin[x / RB];
+            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+                gstore<u32x4_a4>(gaddr[bf] + x, q);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
+                }
+            }
+        }
+        __syncthreads();   // the image, ibin, lstart and gaddr are reused by the next tile
+    };
+    Set A, B;
+    int64_t t = first + kx;
+    if (t >= last) return;
+    load(A, t);
+    for (;;) {
+        load(B, t + gx);
+        process(A, t);
+        t += gx;
+        if (t >= last) break;
+        load(A, t + gx);
+        process(B, t);
+        t += gx;
+        if (t >= last) break;
+    }
+}
+
+hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
+                              const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
+                              int tile_rows, const Workspace& ws, void* dst, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (tile_rows != kFineTR || row_bytes % 4 || row_bytes > 64 || ((uintptr_t)src & 3) ||
+        ((uintptr_t)dst & 3))
+        return hipErrorNotSupported;
+    const int lds = align16(kFineTR * (int)row_bytes) + align16(kFineTR * 2) + nbins * 8 + nbins * 2;
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
+    const int64_t need = (ws.T + 7) / 8 * 8;
+    if (grid > need) grid = need;
+    prof_begin(s, K_PACK_FINE);
+    hipError_t e = hipErrorNotSupported;
+#define MGR_PR(RB_)                                                                           \
+    case RB_: {                                                                               \
+        auto k = pack_ranked_kernel<RB_>;                                                     \
+        ensure_lds(k, lds);                                                                   \
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,               \
+                           (const uint8_t*)src, n, ids, ranks, tile_starts, nbins, ws.offsets, \
+                           ws.T, (uint8_t*)dst, ws.scan_err);                                  \
+        e = hipGetLastError();                                                                \
+        break;                                                                                \
+    }
+    switch ((int)row_bytes) {
+        MGR_PR(4) MGR_PR(8) MGR_PR(12) MGR_PR(16) MGR_PR(20) MGR_PR(24) MGR_PR(28) MGR_PR(32)
+        MGR_PR(36) MGR_PR(40) MGR_PR(44) MGR_PR(48) MGR_PR(52) MGR_PR(56) MGR_PR(60) MGR_PR(64)
+        default: break;
+    }
+#undef MGR_PR
+    prof_end(s, K_PACK_FINE);
+    return e;
+}
+
 static hipError_t pack_fine(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                             int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                             int redirect_bin, void* redirect_dst, hipStream_t s) {
@@ -1120,6 +1275,13 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
             if (e != hipErrorNotSupported) return e;
         }
     }
+    if constexpr (W == 2) {   // 2-byte rows (the fine cells travelling with config-5 rows)
+        if (nb <= 64 && row_bytes == 2) {
+            const hipError_t e = pack_coop_u<2, 1>(src, n, dest, nb, drop_bin, tile_rows, ws, dst,
+                                                   redirect_bin, redirect_dst, s);
+            if (e != hipErrorNotSupported) return e;
+        }
+    }
     if (nb <= 64 && row_bytes <= 64 && W >= 4) {
         const hipError_t e = pack_coop_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
                                              ws, dst, redirect_bin, redirect_dst, s);
@@ -1133,14 +1295,39 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
                 : pack_t<W, uint16_t, false>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
 }
 
+static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n,
+                                   const void* dest, int nbins, int drop_bin, int tile_rows,
+                                   const Workspace& ws, void* dst, int redirect_bin,
+                                   void* redirect_dst, hipStream_t s);
+
 hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                        int nbins, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                       int redirect_bin, void* redirect_dst, hipStream_t s) {
+                       int redirect_bin, void* redirect_dst, hipStream_t s, const uint16_t* ids_src,
+                       uint16_t* ids_dst, uint16_t* ids_red) {
     if (n <= 0) return hipSuccess;
+    t_side = SideField{ids_src, ids_dst, ids_red, false};
+    hipError_t e = launch_pack_rows(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
+                                    redirect_bin, redirect_dst, s);
+    const bool rest = ids_src && !t_side.used;
+    t_side = SideField{};
+    if (e != hipSuccess || !rest) return e;
+    // the kernel that moved the rows cannot carry the ids: a 2-byte-row pack
+    return launch_pack_rows(ids_src, 2, n, dest, nbins, drop_bin, tile_rows, ws, ids_dst,
+                            redirect_bin, ids_red, s);
+}
+
+static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n,
+                                   const void* dest, int nbins, int drop_bin, int tile_rows,
+                                   const Workspace& ws, void* dst, int redirect_bin,
+                                   void* redirect_dst, hipStream_t s) {
     // Widest unit dividing the row and every base address.
     uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
-    prof_begin(s, K_PACK);
+    // profiler: the many-bin sorted-image pack and narrow (< 4-byte) rows apart
+    const int kid = (g_tune.pack_fine && nbins > 64 && nbins <= 1024 && tile_rows == kFineTR)
+                        ? K_PACK_FINE
+                        : (row_bytes < 4 ? K_PACK_NARROW : K_PACK);
+    prof_begin(s, kid);
     hipError_t e = hipErrorNotSupported;
     if (g_tune.pack_compact && nbins == 2 && drop_bin == 1 && redirect_bin < 0) {
         if ((a & 15) == 0) e = compact_t<16>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
@@ -1155,7 +1342,7 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
         e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
                      redirect_dst, s);
     if (e != hipErrorNotSupported) {
-        prof_end(s, K_PACK);
+        prof_end(s, kid);
         return e;
     }
     if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
@@ -1163,7 +1350,7 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
     else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
     else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
     else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    prof_end(s, K_PACK);
+    prof_end(s, kid);
     return e;
 }
 

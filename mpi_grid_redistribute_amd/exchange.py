@@ -59,14 +59,16 @@ def plan_layout(send_counts, recv_counts, rank, redirect_self):
 
 
 def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=None,
-             scratch=None):
+             scratch=None, pack_all=None):
     """Run steps 1-4.  ``bin_counts``: int64 tensor [size] of rows per
     destination (on ``device``).  ``pack(field, send, redirect_bin, out,
     out_offset)`` packs field ``field`` (the redirect bin's rows into ``out``
     from byte ``out_offset``).  ``extra_rows(total_recv)``: spare
     rows to allocate after the received ones (the halo appends there).
     ``scratch(name, nbytes)``: a reusable device buffer (the send buffers),
-    else fresh allocations.  Returns (outs, layout); outs are new flat uint8
+    else fresh allocations.  ``pack_all(sends, outs, redirect_bin,
+    out_offsets)``, when given, packs every field in one call instead (fields
+    moved by one kernel, e.g. rows with their fine cells).  Returns (outs, layout); outs are new flat uint8
     tensors of (total_recv + extra) * row_bytes[f] bytes (>= 1 byte)."""
     sc, rc = transport.exchange_counts(bin_counts)
     check_counts(sc, rc)
@@ -79,12 +81,15 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
         nbytes = max(lay.total_send * rb, 1)
         snd = (scratch(f"send{f}", nbytes) if scratch is not None
                else torch.empty(nbytes, dtype=torch.uint8, device=device))
-        if lay.redirect_self:
-            pack(f, snd, rank, out, int(lay.recv_offsets[rank]) * rb)
-        else:
-            pack(f, snd, -1, None, 0)
         outs.append(out)
         sends.append(snd)
+    redirect = rank if lay.redirect_self else -1
+    offs = [int(lay.recv_offsets[rank]) * rb if lay.redirect_self else 0 for rb in row_bytes]
+    if pack_all is not None:
+        pack_all(sends, outs, redirect, offs)
+    else:
+        for f in range(len(row_bytes)):
+            pack(f, sends[f], redirect, outs[f] if lay.redirect_self else None, offs[f])
     transport.exchange_rows(sends, outs, list(row_bytes), sc, lay.send_offsets, rc,
                             lay.recv_offsets)
     return outs, lay

@@ -73,35 +73,110 @@ class _Plan:
             pass
 
 
-def _fine_sort(plan, dim, dev, data, position, return_positions):
-    """bin (fine plan, no wrap) -> scan -> stable pack of data (and positions)."""
+def _as_ids(fine_ids, n, dev):
+    """uint16 device ids of n rows (torch int16/uint16 tensor or numpy array)."""
+    t = fine_ids if isinstance(fine_ids, torch.Tensor) else torch.from_numpy(
+        np.ascontiguousarray(np.asarray(fine_ids).astype(np.uint16)).view(np.int16))
+    if t.dtype not in (torch.int16, torch.uint16):
+        raise TypeError(f"fine_ids must be 16-bit (got {t.dtype})")
+    t = t.to(dev).contiguous().reshape(-1)
+    if t.numel() != n:
+        raise ValueError(f"fine_ids has {t.numel()} entries for {n} rows")
+    return t
+
+
+def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
+    """count (mgr_count_ids) -> scan -> stable pack of every field by the
+    uint16 ids (the fine cells).  Returns ([sorted flat fields], counts)."""
+    hint = max([f.row_bytes for f in fields] + [1])
+    small = _lib.load().mgr_dest_bytes(int(nb)) == 1   # <= 256 bins: 1-byte dest array
+    tile_rows, ws, d8 = _scratch(n, nb, hint, dev, scratch, dest=small, tag="_fine")
+    s = _lib.stream_handle()
+    counts = torch.empty(nb, dtype=torch.int64, device=dev)
+    # 65..1024 fine cells, 4-byte-multiple rows: ranks computed once, the
+    # ranked pack only places rows (mgr_rank_ids + mgr_pack_ranked)
+    ranked = (64 < nb <= 1024 and tile_rows % 256 == 0 and tile_rows <= 4096
+              and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64 for f in fields))
+    if ranked:
+        T = (n + tile_rows - 1) // tile_rows
+        get = scratch.get if scratch is not None else (
+            lambda name, nbytes: torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev))
+        ranks = get("ranks_fine", 2 * max(n, 1))
+        tstarts = get("tstarts_fine", 2 * max(T * nb, 1))
+        _lib.call("mgr_rank_ids", _lib.ptr(ids), n, nb, tile_rows, _lib.ptr(ranks),
+                  _lib.ptr(tstarts), _lib.ptr(ws), s)
+        _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+        outs = []
+        for f in fields:
+            o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
+            _lib.call("mgr_pack_ranked", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(ids),
+                      _lib.ptr(ranks), _lib.ptr(tstarts), nb, tile_rows, _lib.ptr(ws),
+                      _lib.ptr(o), s)
+            outs.append(o)
+        return outs, counts
+    dest = d8 if small else ids
+    _lib.call("mgr_count_ids", _lib.ptr(ids), n, nb, tile_rows, _lib.ptr(d8), _lib.ptr(ws), s)
+    _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+    outs = []
+    for f in fields:
+        o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
+        _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
+                  tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
+        outs.append(o)
+    return outs, counts
+
+
+def _offsets_like(data, counts, dev):
+    """offsets[nb+1] from device counts, in the container of ``data``; host
+    results are checked for a failed scan (-1 counts) at the copy, device
+    results stay asynchronous."""
+    nb = counts.numel()
+    offsets = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+    offsets[1:] = torch.cumsum(counts, 0)
+    if isinstance(data, torch.Tensor) and data.is_cuda:
+        return offsets
+    check_counts(counts.cpu().numpy(), [])
+    return offsets.cpu() if isinstance(data, torch.Tensor) else offsets.cpu().numpy()
+
+
+def _fine_sort(plan, dim, dev, data, position, return_positions, fine_ids=None):
+    """bin (fine plan, no wrap) -> scan -> stable pack of data (and
+    positions); with ``fine_ids`` (computed at the source, mgr_bin_count_fine)
+    no binning: count -> scan -> pack by the ids."""
     rows = Rows(data, dev)
     pos = Positions(position, dim, dev, data_rows=rows)
     if pos.n != rows.n:
         raise ValueError(f"data has {rows.n} rows, position has {pos.n}")
     n, nb = rows.n, plan.nbins
     prow = Rows(position, dev) if return_positions else None
-    hint = max(rows.row_bytes, prow.row_bytes if prow else 1)
-    tile_rows, ws, dest = _scratch(n, nb, hint, dev)
-    s = _lib.stream_handle()
-    counts = torch.empty(nb, dtype=torch.int64, device=dev)
-    _lib.call("mgr_bin_count", plan.h, ctypes.c_void_p(pos.addr), pos.code, n, pos.stride, 0,
-              _lib.ptr(dest), tile_rows, _lib.ptr(ws), s)
-    _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
-    outs = []
-    for f in [rows] + ([prow] if prow else []):
-        o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
-        _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
-                  tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
-        outs.append(f.wrap(o, n))
-    offsets = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
-    offsets[1:] = torch.cumsum(counts, 0)
-    if not (isinstance(data, torch.Tensor) and data.is_cuda):
-        # device results stay asynchronous (a failed scan shows as -1 counts);
-        # host results are checked at the copy
-        check_counts(counts.cpu().numpy(), [])
-        offsets = offsets.cpu() if isinstance(data, torch.Tensor) else offsets.cpu().numpy()
-    return tuple(outs) + (offsets,)
+    fields = [rows] + ([prow] if prow else [])
+    if fine_ids is not None:
+        outs, counts = _sort_by_ids(fields, _as_ids(fine_ids, n, dev), n, nb, dev)
+    else:
+        hint = max(rows.row_bytes, prow.row_bytes if prow else 1)
+        tile_rows, ws, dest = _scratch(n, nb, hint, dev)
+        s = _lib.stream_handle()
+        counts = torch.empty(nb, dtype=torch.int64, device=dev)
+        _lib.call("mgr_bin_count", plan.h, ctypes.c_void_p(pos.addr), pos.code, n, pos.stride, 0,
+                  _lib.ptr(dest), tile_rows, _lib.ptr(ws), s)
+        _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+        outs = []
+        for f in fields:
+            o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
+            _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
+                      tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
+            outs.append(o)
+    res = [f.wrap(o, n) for f, o in zip(fields, outs)]
+    return tuple(res) + (_offsets_like(data, counts, dev),)
+
+
+class _IdField:
+    """A 2-byte-row field of n rows: the fine cells travelling with the rows."""
+
+    row_bytes = 2
+
+    def __init__(self, flat):
+        self.flat = flat
 
 
 class Scratch:
@@ -131,19 +206,20 @@ class Scratch:
         self.bufs.clear()
 
 
-def _scratch(n, nbins, max_row_bytes, dev, cache=None):
+def _scratch(n, nbins, max_row_bytes, dev, cache=None, dest=True, tag=""):
     """(tile_rows, workspace, dest) for n rows and nbins bins; from ``cache``
-    (a Scratch) when given, else fresh."""
+    (a Scratch, buffers named with ``tag``) when given, else fresh."""
     tile_rows = _lib.load().mgr_tile_rows(int(max_row_bytes), int(nbins))
     wsb = _lib.load().mgr_workspace_bytes(int(n), int(nbins), int(tile_rows))
     if wsb < 0:
         raise _lib.MgrError("mgr_workspace_bytes: bad arguments")
     db = max(int(n), 1) * _lib.load().mgr_dest_bytes(int(nbins))
     if cache is not None:
-        return tile_rows, cache.get("ws", wsb), cache.get("dest", db)
+        return (tile_rows, cache.get("ws" + tag, wsb),
+                cache.get("dest" + tag, db) if dest else None)
     ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
-    dest = torch.empty(db, dtype=torch.uint8, device=dev)
-    return tile_rows, ws, dest
+    d = torch.empty(db, dtype=torch.uint8, device=dev) if dest else None
+    return tile_rows, ws, d
 
 
 class MPIGridRedistributor:
@@ -239,17 +315,25 @@ class MPIGridRedistributor:
 
     # ------------------------------------------------- redistribution (L2)
     def redistribute_by_position(self, data, position, periodic=True, overload_lengths=None,
-                                 return_positions=False):
+                                 return_positions=False, fine_cells=None):
         """redist.py:115-166.  Returns the rows of ``data`` whose position
         falls in this rank's cell, from every rank, in source-rank order;
         ``position`` is wrapped in place when periodic (S1).  With
         ``overload_lengths`` the halo rows follow (redist.py:161-166; the
-        halo exchange always runs periodic, :165)."""
+        halo exchange always runs periodic, :165).  With ``fine_cells``
+        (config 5, no reference counterpart) the received rows come back
+        stably sorted by fine cell with their offsets, = ``fine_cell_sort``
+        of the plain result, computed from fine cells binned at the source."""
         self._check_host_alias(data, position)
         rows = Rows(data, self._dev)
         pos = Positions(position, self.dim, self._dev, data_rows=rows)
         if pos.n != rows.n:
             raise ValueError(f"data has {rows.n} rows, position has {pos.n}")
+        if fine_cells is not None:
+            if overload_lengths is not None:
+                raise NotImplementedError("fine_cells together with overload_lengths")
+            return self._redistribute_fine(data, position, rows, pos, periodic, fine_cells,
+                                           return_positions)
         halo = overload_lengths is not None
         if halo:
             self._check_halo(overload_lengths)
@@ -295,6 +379,52 @@ class MPIGridRedistributor:
             return res, fields[1].wrap(res_p, m + mo)
         return res
 
+    def _fine_plan(self, fine_cells):
+        fine = np.array(fine_cells).astype(np.int64)
+        if fine.ndim != 1 or len(fine) != self.dim:
+            raise ValueError(f"fine_cells must have {self.dim} entries")
+        key = tuple(int(x) for x in fine)
+        plan = self._fine_plans.get(key)
+        if plan is None:
+            plan = self._fine_plans[key] = _Plan(self.grid_topology, self.box_length, 0,
+                                                 fine=fine)
+        return plan
+
+    def _redistribute_fine(self, data, position, rows, pos, periodic, fine_cells,
+                           return_positions):
+        """Source: bin + fine cell of every row (mgr_bin_count_fine), the
+        fine cells packed and exchanged as a 2-byte field beside the rows;
+        destination: count -> scan -> pack by the received fine cells."""
+        fplan = self._fine_plan(fine_cells)
+        fids = self._scratch.get("fine_src", max(rows.n, 1) * 2)
+        fields = [rows, _IdField(fids)]
+        if return_positions:
+            fields.append(None)
+
+        def binner(dest, tile_rows, ws):
+            _lib.call("mgr_bin_count_fine", self._plan.h, fplan.h, ctypes.c_void_p(pos.addr),
+                      pos.code, pos.n, pos.stride, int(bool(periodic)), _lib.ptr(dest),
+                      _lib.ptr(fids), tile_rows, _lib.ptr(ws), _lib.stream_handle())
+            pos.finish()
+            if return_positions:
+                fields[2] = Rows(position, self._dev)
+
+        hint = [rows.row_bytes, 2]
+        if return_positions:
+            hint.append(self._pos_row_bytes(position, pos))
+        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=hint, side_ids=True)
+        ids = outs[1][: 2 * m].view(torch.int16) if m else torch.empty(0, dtype=torch.int16,
+                                                                        device=self._dev)
+        recv = [_IdField(outs[0])] + ([_IdField(outs[2])] if return_positions else [])
+        recv[0].row_bytes = rows.row_bytes
+        if return_positions:
+            recv[1].row_bytes = fields[2].row_bytes
+        sorted_, counts = _sort_by_ids(recv, ids, m, fplan.nbins, self._dev, self._scratch)
+        res = [rows.wrap(sorted_[0], m)]
+        if return_positions:
+            res.append(fields[2].wrap(sorted_[1], m))
+        return tuple(res) + (_offsets_like(data, counts, self._dev),)
+
     def exchange_overload_by_position(self, data, position, overload_lengths,
                                       return_positions=False, periodic=True):
         """redist.py:202-309: the overload (halo) rows of this rank's cell
@@ -321,7 +451,7 @@ class MPIGridRedistributor:
         res = rows.wrap(ov_d, mo)
         return (res, prow.wrap(ov_p, mo)) if return_positions else res
 
-    def fine_cell_sort(self, data, position, fine_cells, return_positions=False):
+    def fine_cell_sort(self, data, position, fine_cells, return_positions=False, fine_ids=None):
         """Destination-side stable sort of this rank's rows by fine cell, for
         particle-mesh deposition (the reference has
         no such step).  The fine cell of a row is the reference's binning
@@ -330,16 +460,12 @@ class MPIGridRedistributor:
         numbered row-major.  ``position`` is read, never wrapped (the rows were
         wrapped by the redistribution).  Returns (sorted data, offsets
         [prod(fine_cells)+1]) -- or (data, positions, offsets) with
-        ``return_positions`` -- in the containers of the inputs."""
-        fine = np.array(fine_cells).astype(np.int64)
-        if fine.ndim != 1 or len(fine) != self.dim:
-            raise ValueError(f"fine_cells must have {self.dim} entries")
-        key = tuple(int(x) for x in fine)
-        plan = self._fine_plans.get(key)
-        if plan is None:
-            plan = self._fine_plans[key] = _Plan(self.grid_topology, self.box_length, 0,
-                                                 fine=fine)
-        return _fine_sort(plan, self.dim, self._dev, data, position, return_positions)
+        ``return_positions`` -- in the containers of the inputs.
+        ``fine_ids``: the rows' fine cells as computed at the source
+        (uint16, ``GridPartitioner.partition_device(..., fine_cells=...)`` /
+        mgr_bin_count_fine); the rows are then not binned again."""
+        plan = self._fine_plan(fine_cells)
+        return _fine_sort(plan, self.dim, self._dev, data, position, return_positions, fine_ids)
 
     def get_cell_number_from_indexes_host(self, indexes, periodic=True):
         """redist.py:73-85 on the host (neighbour ranks of the halo exchange)."""
@@ -382,8 +508,10 @@ class MPIGridRedistributor:
         outs, m = self._run([rows], binner, rows.n, drop=True)
         return rows.wrap(outs[0], m)
 
-    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None):
-        """bin -> scan -> count exchange -> pack -> row exchange."""
+    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None, side_ids=None):
+        """bin -> scan -> count exchange -> pack -> row exchange.  ``side_ids``:
+        field 1 is the rows' 2-byte side field (fine cells), packed by the
+        same kernel as field 0 (mgr_pack_ids)."""
         P = self.size
         nb = P + 1 if drop else P
         hint = row_bytes_hint or [f.row_bytes for f in fields]
@@ -393,16 +521,29 @@ class MPIGridRedistributor:
         bin_counts = torch.empty(nb, dtype=torch.int64, device=self._dev)
         _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(bin_counts), stream)
 
+        def red_ptr(out, off):
+            # address arithmetic, not a slice: an empty tail slice has no data pointer
+            return ctypes.c_void_p(out.data_ptr() + off if out is not None else 0)
+
         def pack(f, snd, redirect_bin, out, out_offset):
             fld = fields[f]
-            # address arithmetic, not a slice: an empty tail slice has no data pointer
-            red = ctypes.c_void_p(out.data_ptr() + out_offset if out is not None else 0)
             _lib.call("mgr_pack", _lib.ptr(fld.flat), fld.row_bytes, n, _lib.ptr(dest), nb,
                       P if drop else -1, tile_rows, _lib.ptr(ws), _lib.ptr(snd), redirect_bin,
-                      red, stream)
+                      red_ptr(out, out_offset), stream)
+
+        def pack_all(sends, outs, redirect_bin, offs):
+            r = redirect_bin >= 0
+            _lib.call("mgr_pack_ids", _lib.ptr(fields[0].flat), fields[0].row_bytes, n,
+                      _lib.ptr(dest), nb, P if drop else -1, tile_rows, _lib.ptr(ws),
+                      _lib.ptr(sends[0]), redirect_bin, red_ptr(outs[0] if r else None, offs[0]),
+                      _lib.ptr(fields[1].flat), _lib.ptr(sends[1]),
+                      red_ptr(outs[1] if r else None, offs[1]), stream)
+            for f in range(2, len(fields)):
+                pack(f, sends[f], redirect_bin, outs[f] if r else None, offs[f])
 
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
-                             self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get)
+                             self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
+                             pack_all=pack_all if side_ids else None)
         return outs, lay.total_recv
 
     # ------------------------------------------------------------ helpers
@@ -447,6 +588,8 @@ class GridPartitioner:
         self._plan = _Plan(self.grid_topology, self.box_length, self.nbins)
         self._dev = device()
         self._cache = {}
+        self._fine_plans = {}
+        self._fine_buf = None
 
     def buffers(self, n, row_bytes):
         key = (int(n), int(row_bytes))
@@ -457,19 +600,45 @@ class GridPartitioner:
             self._cache = {key: (tile_rows, ws, dest, out, counts)}
         return self._cache[key]
 
-    def partition_device(self, data_flat, row_bytes, pos_tensor, periodic=True, stream=None):
+    def partition_device(self, data_flat, row_bytes, pos_tensor, periodic=True, stream=None,
+                         fine_cells=None):
         """Hot-path call on device buffers (no host sync).  ``data_flat``:
         uint8 device tensor of n*row_bytes; ``pos_tensor``: (n, >=dim)
         float32/float64 device tensor with unit column stride (wrapped in
-        place).  Returns (out_flat, bin_counts) device tensors."""
+        place).  Returns (out_flat, bin_counts) device tensors; with
+        ``fine_cells`` (config 5's source side) also every row's fine cell
+        inside its destination cell, partitioned like the rows (uint16 ids
+        for ``MPIGridRedistributor.fine_cell_sort(..., fine_ids=)``):
+        (out_flat, fine_ids_out, bin_counts)."""
         n = int(pos_tensor.shape[0])
         tile_rows, ws, dest, out, counts = self.buffers(n, row_bytes)
         code = _lib.MGR_F32 if pos_tensor.dtype == torch.float32 else _lib.MGR_F64
-        _lib.call("mgr_partition_by_position", self._plan.h, _lib.ptr(pos_tensor), code, n,
-                  pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(data_flat), row_bytes,
-                  _lib.ptr(out), _lib.ptr(dest), _lib.ptr(counts), tile_rows, _lib.ptr(ws),
-                  _lib.stream_handle(stream))
-        return out, counts
+        s = _lib.stream_handle(stream)
+        if fine_cells is None:
+            _lib.call("mgr_partition_by_position", self._plan.h, _lib.ptr(pos_tensor), code, n,
+                      pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(data_flat), row_bytes,
+                      _lib.ptr(out), _lib.ptr(dest), _lib.ptr(counts), tile_rows, _lib.ptr(ws), s)
+            return out, counts
+        key = tuple(int(x) for x in fine_cells)
+        if key not in self._fine_plans:
+            self._fine_plans[key] = _Plan(self.grid_topology, self.box_length, 0,
+                                          fine=np.array(key))
+        fplan = self._fine_plans[key]
+        fid, fid_out = self.fine_buffers(n)
+        _lib.call("mgr_bin_count_fine", self._plan.h, fplan.h, _lib.ptr(pos_tensor), code, n,
+                  pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(dest), _lib.ptr(fid),
+                  tile_rows, _lib.ptr(ws), s)
+        _lib.call("mgr_scan", n, self.nbins, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+        _lib.call("mgr_pack_ids", _lib.ptr(data_flat), row_bytes, n, _lib.ptr(dest), self.nbins,
+                  -1, tile_rows, _lib.ptr(ws), _lib.ptr(out), -1, None, _lib.ptr(fid),
+                  _lib.ptr(fid_out), None, s)
+        return out, fid_out.view(torch.int16)[:n], counts
+
+    def fine_buffers(self, n):
+        if self._fine_buf is None or self._fine_buf[0].numel() < 2 * max(n, 1):
+            self._fine_buf = tuple(torch.empty(2 * max(n, 1), dtype=torch.uint8, device=self._dev)
+                                   for _ in range(2))
+        return self._fine_buf
 
     def partition_by_position(self, data, position, periodic=True):
         """Arrays in, (partitioned data, offsets[nbins+1]) out; position

@@ -99,3 +99,82 @@ def test_fine_after_redistribution_golden():
     outs = run_ranks(size, fn)
     for r in range(size):
         assert G.same_bytes(outs[r], fine[f"r{r}_sorted"]), r
+
+
+# ------------------------------------------- fine cells binned at the source
+def test_fused_fine_redistribution_golden():
+    """redistribute_by_position(..., fine_cells) -- fine cells computed by the
+    source's bin kernel, exchanged as a 2-byte field, rows sorted by them at
+    the destination -- == redistribution then fine_cell_sort, on the
+    reference's own fixtures (the Cfg5 pipeline)."""
+    f = G.load("redist_p8_rec36_view.npz")
+    fine = G.load("fine_p8_rec36_888.npz")
+    size = int(f["size"])
+    data = [d.copy() for d in G.per_rank(f, "data", size)]
+
+    def fn(comm, r):
+        R = MPIGridRedistributor(comm, f["topology"], f["box"])
+        return R.redistribute_by_position(data[r], data[r]["pos"], fine_cells=[8, 8, 8])
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        got, off = outs[r]
+        assert G.same_bytes(got, fine[f"r{r}_sorted"]), r
+        assert np.array_equal(np.diff(off), np.bincount(fine[f"r{r}_fine_id"], minlength=512)), r
+        assert G.same_bytes(data[r]["pos"], f[f"r{r}_pos_out"]), r   # wrapped in place
+
+
+@pytest.mark.parametrize("fine", [[8, 8, 8], [4, 4, 4], [2, 3, 4], [16, 16, 16], [1, 1, 64]])
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_fused_fine_vs_oracle(fine, dt):
+    """Four threaded ranks (2x2x1), out-of-box positions (the wrap), f64 and
+    f32 positions, <= 256 fine cells (1-byte destination array) and up to 4096,
+    with return_positions: bit-exact against the oracle's redistribution +
+    fine_cell_ids + stable sort."""
+    rng = np.random.default_rng(sum(fine) * 3 + (dt == np.float32))
+    size, topo, box = 4, [2, 2, 1], [1.0, 1.0, 1.0]
+    pos = [rng.uniform(-0.3, 1.3, (int(rng.integers(20_000, 60_000)), 3)).astype(dt)
+           for _ in range(size)]
+    data = [np.arange(len(p), dtype=np.int64) * 8 + r for r, p in enumerate(pos)]
+    pos_o = [p.copy() for p in pos]
+    loc = ro.redistribute_by_position_all_ranks(topo, box, size, data, pos_o)
+    geos = [ro.Geometry(topo, box, size, r) for r in range(size)]
+    lpos = ro.redistribute_by_cell_number_all_ranks(
+        size, pos_o, [ro.cell_number_from_position(g, p.copy()) for g, p in zip(geos, pos_o)])
+    nf = int(np.prod(fine))
+
+    def fn(comm, r):
+        R = MPIGridRedistributor(comm, topo, box)
+        return R.redistribute_by_position(data[r], pos[r], fine_cells=fine, return_positions=True)
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        fid = ro.fine_cell_ids(topo, fine, box, lpos[r])
+        exp, exp_off = ro.fine_cell_sort(loc[r], fid, nf)
+        got, gpos, off = outs[r]
+        assert G.same_bytes(got, exp), r
+        assert np.array_equal(off, exp_off), r
+        assert G.same_bytes(gpos, lpos[r][np.argsort(fid, kind="stable")]), r
+        assert G.same_bytes(pos[r], pos_o[r]), r
+
+
+def test_partition_fine_ids_then_sort():
+    """The 1-GPU Cfg5 step's device API: GridPartitioner.partition_device(...,
+    fine_cells) partitions the rows and their fine cells; fine_cell_sort(...,
+    fine_ids=) of a destination's segment == fine_cell_sort binning again."""
+    n = 1 << 20
+    rec, pos = mgr.synth_wide(n, seed=9)
+    P = mgr.GridPartitioner([2, 2, 2], [1.0] * 3)
+    out, fids, counts = P.partition_device(rec.reshape(-1), 36, pos, fine_cells=[8, 8, 8])
+    out2, counts2 = mgr.GridPartitioner([2, 2, 2], [1.0] * 3).partition_device(
+        rec.reshape(-1).clone(), 36, pos.clone())
+    assert torch.equal(counts, counts2) and torch.equal(out[: n * 36], out2[: n * 36])
+    c = counts.cpu().numpy()
+    starts = np.concatenate([[0], np.cumsum(c)])
+    R = run_ranks(8, lambda comm, r: MPIGridRedistributor(comm, [2, 2, 2], [1.0] * 3))
+    for cell in (0, 5):
+        seg = out[starts[cell] * 36: starts[cell + 1] * 36].reshape(-1, 36)
+        a, oa = R[cell].fine_cell_sort(seg, seg.view(torch.float32)[:, :3], [8, 8, 8],
+                                       fine_ids=fids[starts[cell]: starts[cell + 1]])
+        b, ob = R[cell].fine_cell_sort(seg, seg.view(torch.float32)[:, :3], [8, 8, 8])
+        assert torch.equal(a, b) and torch.equal(oa, ob)
