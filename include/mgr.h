@@ -222,15 +222,37 @@ int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride
                    const double* hi, const double* lo, uint16_t* flags, void* stream);
 int mgr_select_count(const uint16_t* flags, int64_t n, int mask, void* dest, int tile_rows,
                      void* workspace, void* stream);
-/* mgr_select_pack2: the selection of mgr_select_count + mgr_scan applied to
- * two fields of the same n rows in one pass (the payload rows and their
- * position rows, redist.py:274-275 / :164), = mgr_pack(src1, rb1, ..., 2,
- * 1, ...) then mgr_pack(src2, rb2, ...).  Fused for 16-byte-aligned rows of
- * <= 64 bytes with 24-byte (f64) or 12-byte (f32) position rows; other
- * shapes run the two packs.                                                 */
-int mgr_select_pack2(const void* src1, int64_t row_bytes1, void* dst1, const void* src2,
-                     int64_t row_bytes2, void* dst2, int64_t n, const void* dest, int tile_rows,
-                     const void* workspace, void* stream);
+/* The halo face flags computed by the binning kernel itself, against the
+ * limits of the cell each row lands in: mgr_bin_count + flags[r] (uint16, the
+ * layout of mgr_halo_flags) for cell_length[d] (numpy's box/topology,
+ * redist.py:49-51) and overload_lengths[d].  The flags travel with the rows
+ * (mgr_pack_ids) and equal mgr_halo_flags of the rank that receives them --
+ * and of every neighbour they are forwarded to, whose cell differs from it
+ * only in the dimension of the exchange -- so no rank re-reads positions.  */
+int mgr_bin_count_halo(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n,
+                       int64_t row_stride, int periodic, void* dest, uint16_t* flags,
+                       const double* cell_length, const double* overload_lengths, int tile_rows,
+                       void* workspace, void* stream);
+/* Multi-selection: set k = the rows whose flag bit bits[k] is set (nsets <=
+ * 16; a row may be in several sets), all sets in one pass.  mgr_msel_count
+ * writes the per-(set, tile) counts for mgr_scan(n, nsets, ...) (bin_counts
+ * = the set sizes); then mgr_msel_pack writes one field's selected rows (any
+ * width): set k's rows, in row order, to dsts[k] (nsets device pointers; NULL
+ * = set k not written).  The halo's sends of a dimension and direction
+ * (redist.py:271-275) go straight to a neighbour's staging buffer or, for a
+ * self-neighbour, into the halo store.                                    */
+int mgr_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits, int tile_rows,
+                   void* workspace, void* stream);
+int mgr_msel_pack(const void* src, int64_t row_bytes, int64_t n, const uint16_t* flags,
+                  int nsets, const int* bits, int tile_rows, const void* workspace,
+                  void* const* dsts, void* stream);
+/* mgr_msel_pack of nfields (1..3) fields of the same rows in one pass (the
+ * flags read and the sets listed once): srcs[f] rows of row_bytes[f]; set k
+ * of field f goes to dsts[f * nsets + k]; field 0's NULLs decide which sets
+ * are written.                                                            */
+int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                         const uint16_t* flags, int nsets, const int* bits, int tile_rows,
+                         const void* workspace, void* const* dsts, void* stream);
 
 /* ------------------------------------------------------------ exchange --
  * Replaces comm.alltoall(send_buff) + np.concatenate (redist.py:199):
@@ -273,12 +295,14 @@ int mgr_exchange_schedule(int rank, int size, int nfields, const int64_t* row_by
                           const int64_t* send_counts, const int64_t* send_offsets,
                           const int64_t* recv_counts, const int64_t* recv_offsets, int skip_self,
                           mgr_xop* ops, int max_ops);
-/* One isend/irecv pair of the halo exchange (redist.py:289-303): send
- * send_bytes to rank dest and receive recv_bytes from rank source, grouped
- * (ncclSend + ncclRecv); dest == source == me is a device copy.  Sizes must
- * match the peers' (exchange them first, e.g. as 8-byte messages).         */
-int mgr_sendrecv(mgr_comm* comm, const void* send, int64_t send_bytes, int dest, void* recv,
-                 int64_t recv_bytes, int source, void* stream);
+/* One group of point-to-point operations (kinds MGR_XOP_SEND / _RECV, byte
+ * counts, device buffers), posted in order: RCCL matches a pair of ranks'
+ * sends and receives in posting order, so the halo's two sequential steps
+ * per dimension (redist.py:289-303) become one group when each rank posts
+ * step 1 (send right, receive from left) before step 2.  Operations with
+ * this rank as peer pair up in order as device copies.                     */
+int mgr_group_p2p(mgr_comm* comm, int nops, const int* kinds, const int* peers,
+                  void* const* bufs, const int64_t* bytes, void* stream);
 /* Element-wise max all-reduce of count doubles (bench timing, barriers).   */
 int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,
                                void* stream);

@@ -51,7 +51,11 @@ SIGNATURES = {
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
     "mgr_halo_flags": (_I, [_P, _I, _I64, _I64, _I, _P, _P, _P, _P]),
     "mgr_select_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
-    "mgr_select_pack2": (_I, [_P, _I64, _P, _P, _I64, _P, _I64, _P, _I, _P, _P]),
+    "mgr_bin_count_halo": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P, _P, _I, _P, _P]),
+    "mgr_msel_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
+    "mgr_msel_pack": (_I, [_P, _I64, _I64, _P, _I, _P, _I, _P, _P, _P]),
+    "mgr_msel_pack_fields": (_I, [_I, _P, _P, _I64, _P, _I, _P, _I, _P, _P, _P]),
+    "mgr_group_p2p": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "mgr_comm_unique_id": (_I, [_P]),
     "mgr_comm_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),
     "mgr_comm_destroy": (_I, [_P]),
@@ -60,7 +64,6 @@ SIGNATURES = {
     "mgr_exchange_counts": (_I, [_P, _P, _P, _P]),
     "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "mgr_exchange_schedule": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I]),
-    "mgr_sendrecv": (_I, [_P, _P, _I64, _I, _P, _I64, _I, _P]),
     "mgr_comm_allreduce_max_f64": (_I, [_P, _P, _P, _I64, _P]),
     "mgr_synth_uniform": (_I, [ctypes.c_uint64, _I64, _I64, _I, _P, _P, _P, _P]),
     "mgr_tune": (_I, [ctypes.c_char_p, _I64]),

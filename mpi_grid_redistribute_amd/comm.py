@@ -75,23 +75,36 @@ class Transport:
         """sends/outs: per-field uint8 tensors; counts/offsets in rows (host)."""
         raise NotImplementedError
 
-    def sendrecv(self, send, dest, recv, source):
-        """One isend/irecv pair of the halo exchange (redist.py:289-303):
-        send the flat uint8 tensor ``send`` to rank ``dest`` and fill ``recv``
-        (pre-sized by the caller) from rank ``source``."""
+    def p2p(self, ops):
+        """One batch of the halo exchange's point-to-point messages
+        (redist.py:289-303): ``ops`` = [("send" | "recv", peer, flat uint8
+        tensor), ...] in posting order; a pair of ranks' sends and receives
+        match in that order (each rank posts step 1 -- send right, receive
+        from the left -- before step 2).  Receive tensors are pre-sized."""
         raise NotImplementedError
 
     def barrier(self):
         pass
 
 
+def _self_pairs(ops, rank):
+    """The k-th non-empty send to ``rank`` feeds its k-th non-empty receive."""
+    sends = [t for k, p, t in ops if k == "send" and p == rank and t.numel()]
+    recvs = [t for k, p, t in ops if k == "recv" and p == rank and t.numel()]
+    if len(sends) != len(recvs):
+        raise RuntimeError(f"{len(sends)} messages to self, {len(recvs)} receives from self")
+    for snd, rcv in zip(sends, recvs):
+        if snd.numel() != rcv.numel():
+            raise RuntimeError(f"self message of {snd.numel()} bytes into {rcv.numel()}")
+        rcv.copy_(snd)
+
+
 class SelfComm(Transport):
     """One rank, one GPU (or N virtual destinations on one GPU)."""
 
-    def sendrecv(self, send, dest, recv, source):
-        assert dest == 0 and source == 0 and send.numel() == recv.numel()
-        if recv.numel():
-            recv.copy_(send)
+    def p2p(self, ops):
+        assert all(p == 0 for _, p, _ in ops)
+        _self_pairs(ops, 0)
 
     def exchange_counts(self, send_counts):
         s = send_counts.detach().to("cpu").numpy().astype(np.int64)
@@ -170,9 +183,17 @@ class RcclComm(Transport):
                                        recv_counts, recv_offsets),
                   _lib.stream_handle())
 
-    def sendrecv(self, send, dest, recv, source):
-        _lib.call("mgr_sendrecv", self._h, _lib.ptr(send), send.numel(), int(dest),
-                  _lib.ptr(recv), recv.numel(), int(source), _lib.stream_handle())
+    def p2p(self, ops):
+        """One RCCL group (mgr_group_p2p); messages to self are device copies."""
+        n = len(ops)
+        if not n:
+            return
+        kinds = (ctypes.c_int * n)(*[_lib.MGR_XOP_SEND if k == "send" else _lib.MGR_XOP_RECV
+                                     for k, _, _ in ops])
+        peers = (ctypes.c_int * n)(*[int(p) for _, p, _ in ops])
+        bufs = (ctypes.c_void_p * n)(*[t.data_ptr() if t.numel() else 0 for _, _, t in ops])
+        nbytes = (ctypes.c_int64 * n)(*[t.numel() for _, _, t in ops])
+        _lib.call("mgr_group_p2p", self._h, n, kinds, peers, bufs, nbytes, _lib.stream_handle())
 
     def allreduce_max(self, values):
         t = torch.as_tensor(values, dtype=torch.float64, device="cuda").reshape(-1)
@@ -221,17 +242,23 @@ class MpiHostComm(Transport):
                 out[a:a + recv_counts[s] * rb].copy_(torch.from_numpy(np.ascontiguousarray(got[s])),
                                                      non_blocking=False)
 
-    def sendrecv(self, send, dest, recv, source):
-        host = send.detach().cpu().numpy() if send.numel() else np.zeros(0, np.uint8)
-        req = self.comm.isend(host, dest=int(dest), tag=_HALO_TAG)
-        got = self.comm.irecv(source=int(source), tag=_HALO_TAG).wait()
-        req.wait()
-        got = np.ascontiguousarray(got, dtype=np.uint8).reshape(-1)
-        if got.size != recv.numel():
-            raise RuntimeError(f"halo message from rank {source}: {got.size} bytes, "
-                               f"expected {recv.numel()}")
-        if got.size:
-            recv.copy_(torch.from_numpy(got))
+    def p2p(self, ops):
+        """Host-staged isend/irecv (tag 0, as redist.py:290-299): every
+        non-empty send posted first, then every receive waited in order."""
+        _self_pairs(ops, self.rank)
+        reqs = [self.comm.isend(t.detach().cpu().numpy(), dest=int(p), tag=_HALO_TAG)
+                for k, p, t in ops if k == "send" and p != self.rank and t.numel()]
+        for k, p, t in ops:
+            if k != "recv" or p == self.rank or not t.numel():
+                continue
+            got = np.ascontiguousarray(self.comm.irecv(source=int(p), tag=_HALO_TAG).wait(),
+                                       dtype=np.uint8).reshape(-1)
+            if got.size != t.numel():
+                raise RuntimeError(f"halo message from rank {p}: {got.size} bytes, "
+                                   f"expected {t.numel()}")
+            t.copy_(torch.from_numpy(got))
+        for r in reqs:
+            r.wait()
 
     def barrier(self):
         self.comm.alltoall([0] * self.size)
@@ -267,16 +294,16 @@ class TorchDistComm(Transport):
                                         output_split_sizes=out_split, input_split_sizes=in_split,
                                         group=self.group)
 
-    def sendrecv(self, send, dest, recv, source):
-        if dest == self.rank and source == self.rank:
-            if recv.numel():
-                recv.copy_(send)
-            return
+    def p2p(self, ops):
+        _self_pairs(ops, self.rank)
         reqs = []
-        if send.numel():
-            reqs.append(self.dist.isend(send.contiguous(), self._global(dest), group=self.group))
-        if recv.numel():
-            reqs.append(self.dist.irecv(recv, self._global(source), group=self.group))
+        for k, p, t in ops:
+            if p == self.rank or not t.numel():
+                continue
+            if k == "send":
+                reqs.append(self.dist.isend(t.contiguous(), self._global(p), group=self.group))
+            else:
+                reqs.append(self.dist.irecv(t, self._global(p), group=self.group))
         for r in reqs:
             r.wait()
 

@@ -20,10 +20,12 @@ constexpr int kStageMaxRowBytes = 64;
 // One workgroup per tile: its waves split the tile's 64-row rounds into
 // contiguous runs (wave w: rows [w*rows_per_wave, ...)), bin them, and add
 // their wave-aggregated counts into one LDS histogram for the tile.
-// kF: also write every row's fine cell (FineGeom, u16) to fine_out -- the
-// destination-side fine sort of config 5 then needs no second binning pass.
+// SIDE: also write a u16 per row to side_out -- its fine cell (kSideFine,
+// FineGeom: the destination-side fine sort of config 5 then needs no second
+// binning pass) or its halo face flags (kSideHalo, HaloGeom: the overload
+// exchange then needs no flag pass over the received positions).
 template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT, int DEPTH,
-          bool kF>
+          int SIDE>
 __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
@@ -31,8 +33,8 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
                                                            int64_t T, int tile_rows,
                                                            int per_wave_lds, int skip_clean,
                                                            int xcd, uint64_t* __restrict__ scan_flags,
-                                                           FineGeom fg,
-                                                           uint16_t* __restrict__ fine_out) {
+                                                           FineGeom fg, HaloGeom hg,
+                                                           uint16_t* __restrict__ side_out) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     clear_scan_flags(scan_flags);
     const int w = threadIdx.x >> 6, lane = lane_id();
@@ -63,6 +65,21 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
         }
         const unsigned long long peers = match_bin(b, valid, g.nbits);
         if (valid && rank_in(peers) == 0) atomicAdd(&hist[b], __popcll(peers));
+    };
+    // the side u16 of one round: a full round as 16 8-byte stores (lane 4k
+    // gathers lanes 4k..4k+3), like the destination bytes
+    const bool side8 = ((uintptr_t)side_out & 7) == 0;
+    auto side_store = [&](unsigned v, bool valid, int r0) {
+        if (SIDE == kSideNone) return;
+        if (side8 && rows - r0 >= 64) {
+            const unsigned v1 = __shfl_down(v, 1, 64), v2 = __shfl_down(v, 2, 64),
+                           v3 = __shfl_down(v, 3, 64);
+            if ((lane & 3) == 0)
+                *(uint2*)(side_out + row0 + r0 + lane) =
+                    make_uint2((v & 0xffffu) | (v1 << 16), (v2 & 0xffffu) | (v3 << 16));
+        } else if (valid) {
+            side_out[row0 + r0 + lane] = (uint16_t)v;
+        }
     };
 
     if constexpr (NU > 0) {
@@ -104,12 +121,11 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             wave_sync();
             unsigned b = 0;
             bool dirty = false;
-            if (valid) {
-                long long fc = 0;
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM, kF>((PosT*)(stage + lane * rb), g,
-                                                                nullptr, &dirty, &fg, &fc);
-                if (kF) fine_out[row0 + r0 + lane] = (uint16_t)fc;
-            }
+            long long sc = 0;
+            if (valid)
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM, SIDE>((PosT*)(stage + lane * rb), g,
+                                                                  nullptr, &dirty, &fg, &hg, &sc);
+            side_store((unsigned)sc, valid, r0);
             // write the slab back only if a row of it changed (skip_clean)
             if (kPeriodic && (!skip_clean || __ballot(dirty) != 0ull)) {
                 wave_sync();
@@ -150,12 +166,11 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             const bool valid = r0 + lane < rows;
             unsigned b = 0;
             bool dirty = false;
-            if (valid) {
-                long long fc = 0;
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM, kF>(pos + (row0 + r0 + lane) * stride,
-                                                                g, nullptr, &dirty, &fg, &fc);
-                if (kF) fine_out[row0 + r0 + lane] = (uint16_t)fc;
-            }
+            long long sc = 0;
+            if (valid)
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM, SIDE>(pos + (row0 + r0 + lane) * stride,
+                                                                  g, nullptr, &dirty, &fg, &hg, &sc);
+            side_store((unsigned)sc, valid, r0);
             account(b, valid, r0);
             wave_sync();
         }
@@ -242,14 +257,17 @@ __global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t*
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s,
-                              const FineGeom* fg, uint16_t* fine_out) {
+                              const FineGeom* fg, const HaloGeom* hg, uint16_t* side_out) {
     // nontemporal slab loads/stores always (every A/B favoured them); one
     // slab in flight per wave (two measured slower with the write-back,
     // DESIGN.md §3.3)
-    auto k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, true>
-                : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, false>;
+    auto k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideFine>
+                : hg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideHalo>
+                     : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideNone>;
     FineGeom f{};
     if (fg) f = *fg;
+    HaloGeom h{};
+    if (hg) h = *hg;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
     int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each
@@ -258,64 +276,65 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nwaves), (size_t)lds, s, (PosT*)pos, n,
                        stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave,
-                       g_tune.bin_skip_clean, g_tune.xcd_bin || g.nbins > 64, ws.flags, f,
-                       fine_out);
+                       g_tune.bin_skip_clean, g_tune.xcd_bin || g.nbins > 64, ws.flags, f, h,
+                       side_out);
     return hipGetLastError();
 }
 
 template <typename PosT, bool kP, typename DestT, int NU>
 static hipError_t bin_count_dim(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                                 int tile_rows, const Workspace& ws, hipStream_t s,
-                                const FineGeom* fg, uint16_t* fo) {
+                                const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
     switch (g.dim) {
-        case 1: return bin_count_t<PosT, kP, DestT, NU, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
-        case 2: return bin_count_t<PosT, kP, DestT, NU, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
-        case 3: return bin_count_t<PosT, kP, DestT, NU, 3>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
-        default: return bin_count_t<PosT, kP, DestT, NU, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+        case 1: return bin_count_t<PosT, kP, DestT, NU, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+        case 2: return bin_count_t<PosT, kP, DestT, NU, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+        case 3: return bin_count_t<PosT, kP, DestT, NU, 3>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+        default: return bin_count_t<PosT, kP, DestT, NU, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
     }
 }
 
 template <typename PosT, bool kP, typename DestT>
 static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s,
-                              const FineGeom* fg, uint16_t* fo) {
+                              const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
     const int64_t rb = stride * (int64_t)sizeof(PosT);
     if (g_tune.bin_staged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0) {
         switch ((int)((rb + 15) / 16)) {   // 16-byte units per lane per 64-row slab
-            case 1: return bin_count_dim<PosT, kP, DestT, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
-            case 2: return bin_count_dim<PosT, kP, DestT, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
-            case 3: return bin_count_dim<PosT, kP, DestT, 3>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
-            default: return bin_count_dim<PosT, kP, DestT, 4>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+            case 1: return bin_count_dim<PosT, kP, DestT, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+            case 2: return bin_count_dim<PosT, kP, DestT, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+            case 3: return bin_count_dim<PosT, kP, DestT, 3>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+            default: return bin_count_dim<PosT, kP, DestT, 4>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
         }
     }
-    return bin_count_dim<PosT, kP, DestT, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+    return bin_count_dim<PosT, kP, DestT, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
 }
 
 template <typename PosT, typename DestT>
 static hipError_t bin_count_p(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
                               void* dest, int tile_rows, const Workspace& ws, hipStream_t s,
-                              const FineGeom* fg, uint16_t* fo) {
-    return periodic ? bin_count_w<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo)
-                    : bin_count_w<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s, fg, fo);
+                              const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
+    return periodic ? bin_count_w<PosT, true, DestT>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo)
+                    : bin_count_w<PosT, false, DestT>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
 }
 
 template <typename PosT>
 static hipError_t bin_count_d(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
                               void* dest, int tile_rows, const Workspace& ws, hipStream_t s,
-                              const FineGeom* fg, uint16_t* fo) {
+                              const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
     if (dest_bytes(g.nbins) == 1)
-        return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fo);
-    return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fo);
+        return bin_count_p<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fo);
+    return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fo);
 }
 
 hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
-                            hipStream_t s, const FineGeom* fg, uint16_t* fine_out) {
+                            hipStream_t s, const FineGeom* fg, uint16_t* fine_out,
+                            const HaloGeom* hg) {
     if (n <= 0) return hipSuccess;
     const int kid = fg ? K_BIN_FINE : K_BIN_COUNT;
     prof_begin(s, kid);
-    hipError_t e = pos_f32 ? bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fine_out)
-                           : bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, fine_out);
+    hipError_t e = pos_f32 ? bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out)
+                           : bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out);
     prof_end(s, kid);
     return e;
 }

@@ -295,6 +295,74 @@ int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* po
     return MGR_OK;
 }
 
+int mgr_bin_count_halo(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n,
+                       int64_t row_stride, int periodic, void* dest, uint16_t* flags,
+                       const double* cell_length, const double* overload_lengths, int tile_rows,
+                       void* workspace, void* stream) {
+    int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
+    if (rc) return rc;
+    if ((rc = check_tile(tile_rows))) return rc;
+    if (plan->g.fine) return fail(MGR_EINVAL, "a fine-cell plan has no halo");
+    if (!cell_length || !overload_lengths) return fail(MGR_EINVAL, "null cell/overload lengths");
+    if (n > 0 && (!dest || !workspace || !flags)) return fail(MGR_EINVAL, "null dest/flags/workspace");
+    mgr::Geom g = plan->g;
+    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    mgr::HaloGeom hg;
+    memset(&hg, 0, sizeof hg);
+    for (int d = 0; d < g.dim; ++d) {
+        hg.cl[d] = cell_length[d];
+        hg.ol[d] = overload_lengths[d];
+    }
+    const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
+    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
+                                 tile_rows, ws, (hipStream_t)stream, nullptr, flags, &hg));
+    return MGR_OK;
+}
+
+static int check_sets(int nsets, const int* bits) {
+    if (nsets < 1 || nsets > 16 || !bits) return fail(MGR_EINVAL, "nsets %d (1..16)", nsets);
+    for (int k = 0; k < nsets; ++k)
+        if (bits[k] < 0 || bits[k] > 15) return fail(MGR_EINVAL, "set %d: flag bit %d", k, bits[k]);
+    return MGR_OK;
+}
+
+int mgr_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits, int tile_rows,
+                   void* workspace, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc || (rc = check_sets(nsets, bits))) return rc;
+    if (n < 0) return fail(MGR_EINVAL, "n < 0");
+    if (n > 0 && (!flags || !workspace)) return fail(MGR_EINVAL, "null argument");
+    const mgr::Workspace ws = mgr::carve(workspace, n, nsets, tile_rows);
+    HIP_OK(mgr::launch_msel_count(flags, n, nsets, bits, tile_rows, ws, (hipStream_t)stream));
+    return MGR_OK;
+}
+
+int mgr_msel_pack(const void* src, int64_t row_bytes, int64_t n, const uint16_t* flags,
+                  int nsets, const int* bits, int tile_rows, const void* workspace,
+                  void* const* dsts, void* stream) {
+    return mgr_msel_pack_fields(1, &src, &row_bytes, n, flags, nsets, bits, tile_rows, workspace,
+                                dsts, stream);
+}
+
+int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                         const uint16_t* flags, int nsets, const int* bits, int tile_rows,
+                         const void* workspace, void* const* dsts, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc || (rc = check_sets(nsets, bits))) return rc;
+    if (nfields < 1 || nfields > 3 || !srcs || !row_bytes)
+        return fail(MGR_EINVAL, "nfields %d (1..3)", nfields);
+    for (int f = 0; f < nfields; ++f)
+        if (row_bytes[f] < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes[f]);
+    if (n > 0 && (!flags || !workspace || !dsts)) return fail(MGR_EINVAL, "null argument");
+    for (int f = 0; n > 0 && f < nfields; ++f)
+        if (!srcs[f]) return fail(MGR_EINVAL, "null argument");
+    if (n <= 0) return MGR_OK;
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nsets, tile_rows);
+    HIP_OK(mgr::launch_msel_pack(nfields, srcs, row_bytes, n, flags, nsets, bits, tile_rows, ws,
+                                 dsts, (hipStream_t)stream));
+    return MGR_OK;
+}
+
 int mgr_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, void* dest,
                   void* workspace, void* stream) {
     int rc = check_tile(tile_rows);
@@ -446,21 +514,6 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
 }
 
 // ------------------------------------------------------ halo (f1)
-int mgr_select_pack2(const void* src1, int64_t row_bytes1, void* dst1, const void* src2,
-                     int64_t row_bytes2, void* dst2, int64_t n, const void* dest, int tile_rows,
-                     const void* workspace, void* stream) {
-    int rc = check_tile(tile_rows);
-    if (rc) return rc;
-    if (row_bytes1 < 1 || row_bytes2 < 1)
-        return fail(MGR_EINVAL, "row_bytes %lld / %lld", (long long)row_bytes1, (long long)row_bytes2);
-    if (n > 0 && (!src1 || !src2 || !dst1 || !dst2 || !dest || !workspace))
-        return fail(MGR_EINVAL, "null argument");
-    const mgr::Workspace ws = mgr::carve((void*)workspace, n, 2, tile_rows);
-    HIP_OK(mgr::launch_select_pack2(src1, row_bytes1, dst1, src2, row_bytes2, dst2, n, dest,
-                                    tile_rows, ws, (hipStream_t)stream));
-    return MGR_OK;
-}
-
 int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
                    const double* hi, const double* lo, uint16_t* flags, void* stream) {
     if (pos_dtype != MGR_F32 && pos_dtype != MGR_F64)
@@ -647,25 +700,45 @@ int mgr_exchange_rows(mgr_comm* comm, int nfields, const void* const* send, void
     return MGR_OK;
 }
 
-int mgr_sendrecv(mgr_comm* comm, const void* send, int64_t send_bytes, int dest, void* recv,
-                 int64_t recv_bytes, int source, void* stream) {
-    if (!comm) return fail(MGR_EINVAL, "null comm");
-    if (dest < 0 || dest >= comm->size || source < 0 || source >= comm->size)
-        return fail(MGR_EINVAL, "peer out of range (dest %d, source %d, size %d)", dest, source,
-                    comm->size);
-    if (send_bytes < 0 || recv_bytes < 0) return fail(MGR_EINVAL, "negative size");
-    if ((send_bytes > 0 && !send) || (recv_bytes > 0 && !recv)) return fail(MGR_EINVAL, "null buffer");
-    hipStream_t s = (hipStream_t)stream;
-    if (dest == comm->rank && source == comm->rank) {   // self exchange: a device copy
-        if (send_bytes != recv_bytes) return fail(MGR_EINVAL, "self sendrecv size mismatch");
-        if (send_bytes > 0) HIP_OK(hipMemcpyAsync(recv, send, (size_t)send_bytes, hipMemcpyDeviceToDevice, s));
-        return MGR_OK;
+int mgr_group_p2p(mgr_comm* comm, int nops, const int* kinds, const int* peers,
+                  void* const* bufs, const int64_t* bytes, void* stream) {
+    if (!comm || nops < 0 || (nops > 0 && (!kinds || !peers || !bufs || !bytes)))
+        return fail(MGR_EINVAL, "null argument");
+    for (int i = 0; i < nops; ++i) {
+        if (kinds[i] != MGR_XOP_SEND && kinds[i] != MGR_XOP_RECV)
+            return fail(MGR_EINVAL, "op %d: kind %d", i, kinds[i]);
+        if (peers[i] < 0 || peers[i] >= comm->size) return fail(MGR_EINVAL, "op %d: peer %d", i, peers[i]);
+        if (bytes[i] < 0 || (bytes[i] > 0 && !bufs[i])) return fail(MGR_EINVAL, "op %d: buffer", i);
     }
+    hipStream_t s = (hipStream_t)stream;
+    // the self pairs: the k-th send to me feeds the k-th receive from me (a
+    // device copy, RCCL is not involved)
+    std::vector<int> ss, rr;
+    for (int i = 0; i < nops; ++i)
+        if (peers[i] == comm->rank && bytes[i] > 0) (kinds[i] == MGR_XOP_SEND ? ss : rr).push_back(i);
+    if (ss.size() != rr.size()) return fail(MGR_EINVAL, "self sends %zu != self receives %zu", ss.size(), rr.size());
+    for (size_t k = 0; k < ss.size(); ++k) {
+        if (bytes[ss[k]] != bytes[rr[k]])
+            return fail(MGR_EINVAL, "self pair %zu: %lld bytes sent, %lld received", k,
+                        (long long)bytes[ss[k]], (long long)bytes[rr[k]]);
+        HIP_OK(hipMemcpyAsync(bufs[rr[k]], bufs[ss[k]], (size_t)bytes[ss[k]], hipMemcpyDeviceToDevice, s));
+    }
+    bool any = false;
+    for (int i = 0; i < nops; ++i) any |= peers[i] != comm->rank && bytes[i] > 0;
+    if (!any) return MGR_OK;
+    mgr::prof_begin(s, mgr::K_EXCHANGE);
     NCCL_OK(ncclGroupStart());
     Group g;
-    if (send_bytes > 0) GROUP_CALL(g, ncclSend(send, (size_t)send_bytes, ncclUint8, dest, comm->nccl, s));
-    if (recv_bytes > 0) GROUP_CALL(g, ncclRecv(recv, (size_t)recv_bytes, ncclUint8, source, comm->nccl, s));
-    return g.end();
+    for (int i = 0; i < nops; ++i) {
+        if (peers[i] == comm->rank || bytes[i] == 0) continue;
+        if (kinds[i] == MGR_XOP_SEND)
+            GROUP_CALL(g, ncclSend(bufs[i], (size_t)bytes[i], ncclUint8, peers[i], comm->nccl, s));
+        else
+            GROUP_CALL(g, ncclRecv(bufs[i], (size_t)bytes[i], ncclUint8, peers[i], comm->nccl, s));
+    }
+    const int rc = g.end();
+    mgr::prof_end(s, mgr::K_EXCHANGE);
+    return rc;
 }
 
 int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, int64_t count,

@@ -140,13 +140,21 @@ __device__ __forceinline__ bool same_bits(PosT a, PosT b) {
 // The wrapped value is stored only when its bits differ from the input
 // (the in-place mutation of redist.py:68 / :328-329 is then complete: an
 // in-box coordinate wraps to itself) and *dirty records that a store happened.
-// kF: also the coordinate's fine index (FineGeom) from the same quotient t/L
-// -- exactly what the fine plan computes from the stored position later.
-template <typename PosT, bool kPeriodic, bool kF = false>
+// SIDE, a per-row side output computed from the same values:
+//   kSideFine: the coordinate's fine index (FineGeom) from the same quotient
+//     t/L -- exactly what the fine plan computes from the stored position;
+//   kSideHalo: the coordinate's two face flags against its cell's limits
+//     (HaloGeom): bit 0 = x > (k+1)*cl - ol, bit 1 = x < k*cl + ol, the
+//     float64 comparisons of redist.py:271-276 for the rank the row lands on.
+constexpr int kSideNone = 0, kSideFine = 1, kSideHalo = 2;
+
+template <typename PosT, bool kPeriodic, int SIDE = kSideNone>
 __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw,
                                                bool* dirty, const FineGeom* fg = nullptr,
-                                               long long* kfine = nullptr) {
+                                               const HaloGeom* hg = nullptr,
+                                               long long* side = nullptr) {
     long long k, kf = 0;
+    double xs = 0.0;   // the stored (wrapped) coordinate, as numpy compares it
     const PosT in = *p;
     if (sizeof(PosT) == 4 && g.compute_f32) {
         float x = (float)in;
@@ -156,7 +164,8 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
         }
         const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];  // f32 / f32 -> f32
         k = trunc_i64((double)q * g.nd[d]);          // * int64 scalar -> f64
-        if (kF) kf = trunc_i64((double)q * fg->nd[d]);
+        if (SIDE == kSideFine) kf = trunc_i64((double)q * fg->nd[d]);
+        if (SIDE == kSideHalo) xs = f32_to_f64_x86(x);
     } else {
         double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)in) : (double)in;
         if (kPeriodic) {
@@ -167,13 +176,14 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
         }
         const double q = g.pow2[d] ? x * g.invL[d] : x / g.L[d];
         k = trunc_i64(q * g.nd[d]);
-        if (kF) kf = trunc_i64(q * fg->nd[d]);
+        if (SIDE == kSideFine) kf = trunc_i64(q * fg->nd[d]);
+        if (SIDE == kSideHalo) xs = x;
     }
     if (raw) *raw = k;
     const long long n = g.n[d];
     if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
     if (g.fine) k %= g.fmod[d];   // fine-cell plan: index inside the rank's cell
-    if (kF) {
+    if (SIDE == kSideFine) {
         const long long nf = fg->n[d];
         if (!(kf >= 0 && kf < nf)) kf = floormod_i64(floormod_i64(kf, nf) + nf, nf);
         // kf % f without a 64-bit division: kf - f*k when the coarse index k
@@ -182,28 +192,37 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
         const long long f = fg->fmod[d];
         long long m = kf - f * k;
         if (!(m >= 0 && m < f)) m = kf % f;
-        *kfine = m;
+        *side = m;
+    }
+    if (SIDE == kSideHalo) {
+        // limits (redist.py:110-111): k * cl and (k + 1) * cl, int64 * float64
+        const double hi = (double)(k + 1) * hg->cl[d] - hg->ol[d];
+        const double lo = (double)k * hg->cl[d] + hg->ol[d];
+        *side = (xs > hi ? 1 : 0) | (xs < lo ? 2 : 0);
     }
     return k;
 }
 
 // DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
-// kF: *fine gets the row's fine cell (row-major over fg->fmod).
-template <typename PosT, bool kPeriodic, int DIM = 0, bool kF = false>
+// SIDE: *side gets the row's fine cell (row-major over fg->fmod) or its face
+// flags (bit 2d: right face of dimension d, bit 2d+1: left face).
+template <typename PosT, bool kPeriodic, int DIM = 0, int SIDE = kSideNone>
 __device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx,
                                              bool* dirty, const FineGeom* fg = nullptr,
-                                             long long* fine = nullptr) {
-    long long cell = 0, fc = 0;
+                                             const HaloGeom* hg = nullptr,
+                                             long long* side = nullptr) {
+    long long cell = 0, sc = 0;
     const int nd = DIM > 0 ? DIM : g.dim;
 #pragma unroll
     for (int d = 0; d < (DIM > 0 ? DIM : MGR_MAX_DIM); ++d) {
         if (DIM == 0 && d >= nd) break;
-        long long kf = 0;
-        cell += g.off[d] * bin_coord<PosT, kPeriodic, kF>(row + d, g, d, idx ? idx + d : nullptr,
-                                                          dirty, fg, &kf);
-        if (kF) fc += (long long)((int)fg->off[d] * (int)kf);   // < 4096 fine cells
+        long long sd = 0;
+        cell += g.off[d] * bin_coord<PosT, kPeriodic, SIDE>(row + d, g, d, idx ? idx + d : nullptr,
+                                                            dirty, fg, hg, &sd);
+        if (SIDE == kSideFine) sc += (long long)((int)fg->off[d] * (int)sd);   // < 4096 cells
+        if (SIDE == kSideHalo) sc |= sd << (2 * d);
     }
-    if (kF) *fine = fc;
+    if (SIDE != kSideNone) *side = sc;
     return cell;
 }
 
@@ -346,6 +365,64 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t
 }
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+
+// ------------------------------------------------- flag-set selections
+// The halo's selections read 16-bit face flags in chunks of kSelChunk rows:
+// lane l holds rows [16 l, 16 l + 16) of a chunk as 8 packed words (two
+// 16-byte loads per lane, in flight together), so a set's membership is one
+// 16-bit mask per lane and its order is (lane, bit) = row order.  Set k's
+// flag bit: nibble k of a 64-bit word (no dynamic indexing into a
+// kernel-argument array).
+constexpr int kSelChunk = 1024, kSelWords = kSelChunk / 128;
+
+__device__ __forceinline__ void chunk_flags(const uint16_t* __restrict__ flags, int64_t c0,
+                                            int crows, int lane, uint32_t (&fw)[kSelWords]) {
+    const int r = 16 * lane;
+    const uint16_t* p = flags + c0 + r;
+    if (crows == kSelChunk && ((uintptr_t)(flags + c0) & 15) == 0) {
+        const uint4* q = (const uint4*)p;
+        const uint4 a = q[0], b = q[1];
+        fw[0] = a.x; fw[1] = a.y; fw[2] = a.z; fw[3] = a.w;
+        fw[4] = b.x; fw[5] = b.y; fw[6] = b.z; fw[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kSelWords; ++i) {
+            const uint32_t lo = r + 2 * i < crows ? p[2 * i] : 0u;
+            const uint32_t hi = r + 2 * i + 1 < crows ? p[2 * i + 1] : 0u;
+            fw[i] = lo | (hi << 16);
+        }
+    }
+}
+
+// bit j of the result: flag bit b of the lane's row j
+__device__ __forceinline__ uint32_t set_mask(const uint32_t (&fw)[kSelWords], int b) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < kSelWords; ++i)
+        m |= (((fw[i] >> b) & 1u) << (2 * i)) | (((fw[i] >> (16 + b)) & 1u) << (2 * i + 1));
+    return m;
+}
+
+__device__ __forceinline__ int set_bit(uint64_t bits, int k) { return (int)((bits >> (4 * k)) & 15u); }
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// exclusive prefix over the wave's lanes; *total = the sum
+__device__ __forceinline__ int wave_excl(int v, int* total) {
+    const int lane = lane_id();
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
 
 // XCD-contiguous tile order.  Workgroups are dealt to the 8 XCDs round-robin
 // (blockIdx % 8 labels the XCD, MI355X_MICROARCH.md "Workgroup dispatch"), so

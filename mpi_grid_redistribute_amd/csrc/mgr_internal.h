@@ -59,6 +59,13 @@ struct FineGeom {
     int nbins;
 };
 
+// The halo's face thresholds (redist.py:271-276) for every cell index:
+// cell_length[d] (numpy's box/topology) and overload_lengths[d].
+struct HaloGeom {
+    double cl[MGR_MAX_DIM];
+    double ol[MGR_MAX_DIM];
+};
+
 // Workspace carve for (n, nbins, tile_rows).
 struct Workspace {
     int32_t* counts;     // [nbins][T] destination-major tile histogram
@@ -87,7 +94,12 @@ void prof_end(hipStream_t s, int k);
 hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
                             hipStream_t s, const FineGeom* fg = nullptr,
-                            uint16_t* fine_out = nullptr);
+                            uint16_t* side_out = nullptr, const HaloGeom* hg = nullptr);
+hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits,
+                             int tile_rows, const Workspace& ws, hipStream_t s);
+hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
+                            int64_t n, const uint16_t* flags, int nsets, const int* bits,
+                            int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s);
 hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                             const Workspace& ws, uint8_t* dest8, hipStream_t s);
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
@@ -112,9 +124,6 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
-hipError_t launch_select_pack2(const void* src1, int64_t rb1, void* dst1, const void* src2,
-                               int64_t rb2, void* dst2, int64_t n, const void* dest,
-                               int tile_rows, const Workspace& ws, hipStream_t s);
 hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
 hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,

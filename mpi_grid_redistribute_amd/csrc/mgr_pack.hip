@@ -6,6 +6,7 @@
 
 namespace mgr {
 
+
 // ------------------------------------------------------------------ pack
 // Kernel 3 of the hot path.  Per round: ballot match -> rank inside the
 // wave; slot = tile segment start of the bin + running count + rank; the
@@ -236,125 +237,175 @@ __global__ __launch_bounds__(256) void compact_kernel(
     }
 }
 
-// One batch of D rounds of a compaction for one field: unit-transposed
-// unconditional loads (dropped rows read the tile's first unit), kept units
-// stored to their slots from base.
-template <int W, int UPR, int D>
-__device__ __forceinline__ void compact_batch(const typename Unit<W>::T* __restrict__ s_u,
-                                              typename Unit<W>::T* __restrict__ d_u,
-                                              const unsigned long long (&m)[D], int r0,
-                                              long long base, int lane) {
+
+// Multi-selection pack (the halo's sends, msel counts + mgr_scan with nbins
+// = nsets), up to kSelFields fields of the same rows in one launch.  Set k's
+// rows of field f go, in row order, to dsts[f][k] (null: set k is not
+// written), so one launch places a set straight where it is consumed (a
+// staging buffer for a neighbour, or the halo store itself when the
+// neighbour is this rank).  One wave per tile, kSelChunk rows at a time: the
+// chunk's flags are read once (chunk_flags); per set, the lanes' membership
+// masks and a wave prefix list the set's rows in row order in LDS (u16 entry:
+// chunk row | set << 10), the sets one after the other; then one copy loop
+// per field moves every listed row -- 64 / upr rows per instruction, W-byte
+// units (the widest the field's alignment allows), four instructions in
+// flight -- to its set's next output row.  A single chain of loads per chunk
+// and few registers keep enough waves and bytes in flight for a sparse
+// gather.  Rows wider than 64 units are copied one after the other, lanes
+// across the row.
+constexpr int kSelCap = 2048;   // LDS entries per wave (>= kSelChunk)
+constexpr int kSelFields = 3;
+struct SelFields {
+    const uint8_t* src[kSelFields];
+    int64_t row_bytes[kSelFields];
+    int wlog[kSelFields];                 // log2 of the copy unit
+    uint8_t* dst[kSelFields][16];
+};
+
+template <int W>
+__device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_t row_bytes,
+                                         uint8_t* const* dst, const long long* at,
+                                         const int* start, const uint16_t* list, int fill,
+                                         int lane) {
     using U = typename Unit<W>::T;
-    U v[D][UPR];
+    const int64_t upr = row_bytes / W;
+    const U* __restrict__ sp = (const U*)src;
+    if (upr <= 64) {
+        const int per = 64 / (int)upr;   // rows per copy instruction
+        const int lr = lane / (int)upr;
+        const int u = lane - lr * (int)upr;
+        for (int i0 = 0; i0 < fill; i0 += 4 * per) {
+            U v[4];
+            U* o[4];
 #pragma unroll
-    for (int q = 0; q < D; ++q) {
-#pragma unroll
-        for (int k = 0; k < UPR; ++k) {
-            const int u = 64 * k + lane, r = u / UPR;
-            const int64_t idx = ((m[q] >> r) & 1ull) ? (int64_t)(r0 + 64 * q) * UPR + u : 0;
-            v[q][k] = s_u[idx];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-#pragma unroll
-        for (int k = 0; k < UPR; ++k) {
-            const int u = 64 * k + lane, r = u / UPR, part = u - r * UPR;
-            if ((m[q] >> r) & 1ull) {
-                const long long slot = base + __popcll(m[q] & ((1ull << r) - 1ull));
-                d_u[slot * UPR + part] = v[q][k];
+            for (int q = 0; q < 4; ++q) {
+                const int i = i0 + q * per + lr;
+                const bool ok = lr < per && i < fill;
+                const unsigned e = list[ok ? i : 0];
+                const int k = (int)(e >> 10);
+                o[q] = ok ? (U*)dst[k] + (at[k] + (i - start[k])) * upr + u : nullptr;
+                v[q] = sp[(int64_t)(e & 1023u) * upr + u];
             }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (o[q]) *o[q] = v[q];
         }
-        base += __popcll(m[q]);
+    } else {
+        for (int i = 0; i < fill; ++i) {
+            const unsigned e = list[i];
+            const int k = (int)(e >> 10);
+            const U* rs = sp + (int64_t)(e & 1023u) * upr;
+            U* rd = (U*)dst[k] + (at[k] + (i - start[k])) * upr;
+            for (int64_t q = lane; q < upr; q += 64) rd[q] = rs[q];
+        }
     }
 }
 
-// Two fields under one selection (the halo's payload rows and their position
-// rows, redist.py:271-275 applied to data and position alike): the dest bytes
-// are read and balloted once, both fields' kept rows copied in the same pass.
-template <int W1, int U1, int W2, int U2>
-__global__ __launch_bounds__(256) void compact2_kernel(
-    const uint8_t* __restrict__ src1, uint8_t* __restrict__ dst1,
-    const uint8_t* __restrict__ src2, uint8_t* __restrict__ dst2, int64_t n,
-    const uint8_t* __restrict__ dest, const int64_t* __restrict__ offsets, int64_t T,
+__global__ __launch_bounds__(256) void msel_pack_kernel(
+    SelFields fs, int nf, int64_t n, const uint16_t* __restrict__ flags, int nsets, uint64_t bits,
+    const int64_t* __restrict__ offsets, const int64_t* __restrict__ set_starts, int64_t T,
     int tile_rows, const uint32_t* __restrict__ scan_err) {
-    constexpr int D = 4;
+    __shared__ uint16_t list_s[4][kSelCap];
+    __shared__ uint8_t* dst_s[4][kSelFields][16];
+    __shared__ long long at_s[4][16];    // next output row of every set
+    __shared__ int start_s[4][16], cnt_s[4][16];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = (int64_t)blockIdx.x * 4 + w;
     if (tile >= T || scan_failed(scan_err)) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
-    long long base = offsets[tile];
-    const auto* s1 = (const typename Unit<W1>::T*)src1 + row0 * U1;
-    const auto* s2 = (const typename Unit<W2>::T*)src2 + row0 * U2;
-    auto* d1 = (typename Unit<W1>::T*)dst1;
-    auto* d2 = (typename Unit<W2>::T*)dst2;
-    unsigned nb_[D];
+    uint16_t* list = list_s[w];
+    long long* at = at_s[w];
+    int* start = start_s[w];
+    int* cnt = cnt_s[w];
+    uint32_t live = 0;   // sets with a destination (in field 0: all fields alike)
 #pragma unroll
-    for (int q = 0; q < D; ++q) {
-        const int r = 64 * q + lane;
-        nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
+    for (int k = 0; k < 16; ++k) {
+        if (k >= nsets) break;
+        if (fs.dst[0][k]) live |= 1u << k;
+        if (lane == k) {
+#pragma unroll
+            for (int f = 0; f < kSelFields; ++f) dst_s[w][f][k] = fs.dst[f][k];
+            at[k] = offsets[(int64_t)k * T + tile] - set_starts[k];
+            cnt[k] = 0;
+        }
     }
-    for (int r0 = 0; r0 < rows; r0 += 64 * D) {
-        unsigned long long m[D];
-        long long kept = 0;
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-            m[q] = __ballot(nb_[q] == 0u);
-            kept += __popcll(m[q]);
+    wave_sync();
+    for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
+        uint32_t fw[kSelWords];
+        chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
+        auto flush = [&](int fill) {
+            wave_sync();
+            for (int f = 0; f < nf; ++f) {
+                const uint8_t* sp = fs.src[f] + (row0 + c0) * fs.row_bytes[f];
+                uint8_t* const* d = dst_s[w][f];
+                switch (fs.wlog[f]) {
+                    case 4: sel_copy<16>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
+                    case 3: sel_copy<8>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
+                    case 2: sel_copy<4>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
+                    case 1: sel_copy<2>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
+                    default: sel_copy<1>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
+                }
+            }
+            wave_sync();
+            if (lane < nsets) {
+                at[lane] += cnt[lane];
+                cnt[lane] = 0;
+            }
+            wave_sync();
+        };
+        int fill = 0;
+        for (int k = 0; k < nsets; ++k) {
+            if (!((live >> k) & 1u)) continue;
+            uint32_t m = set_mask(fw, set_bit(bits, k));
+            int total;
+            int pos = wave_excl(__popc(m), &total);
+            if (!total) continue;
+            if (fill + total > kSelCap) {
+                flush(fill);
+                fill = 0;
+            }
+            if (lane == 0) {
+                start[k] = fill;
+                cnt[k] = total;
+            }
+            pos += fill;
+            while (m) {
+                const int j = __builtin_ctz(m);
+                m &= m - 1u;
+                list[pos++] = (uint16_t)((16 * lane + j) | (k << 10));
+            }
+            fill += total;
         }
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-            const int r = r0 + 64 * (D + q) + lane;
-            nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
-        }
-        if (kept) {
-            compact_batch<W1, U1, D>(s1, d1, m, r0, base, lane);
-            compact_batch<W2, U2, D>(s2, d2, m, r0, base, lane);
-        }
-        base += kept;
+        if (fill) flush(fill);
     }
 }
 
-// Unit shape (W bytes, U units per row) of a compaction field; 0 if none of
-// the fused kernel's instantiations fits.
-static int compact2_shape(uintptr_t a, int64_t row_bytes, int* W) {
-    if ((a & 15) == 0 && row_bytes <= 64) { *W = 16; return (int)(row_bytes / 16); }
-    if ((a & 7) == 0 && row_bytes == 24) { *W = 8; return 3; }
-    if ((a & 3) == 0 && row_bytes == 12) { *W = 4; return 3; }
-    return 0;
-}
-
-hipError_t launch_select_pack2(const void* src1, int64_t rb1, void* dst1, const void* src2,
-                               int64_t rb2, void* dst2, int64_t n, const void* dest,
-                               int tile_rows, const Workspace& ws, hipStream_t s) {
+hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
+                            int64_t n, const uint16_t* flags, int nsets, const int* bits,
+                            int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    int w1 = 0, w2 = 0;
-    const int u1 = compact2_shape((uintptr_t)src1 | (uintptr_t)dst1 | (uintptr_t)rb1, rb1, &w1);
-    const int u2 = compact2_shape((uintptr_t)src2 | (uintptr_t)dst2 | (uintptr_t)rb2, rb2, &w2);
-    const dim3 grid((unsigned)((ws.T + 3) / 4));
-    auto go = [&](auto k) {
-        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, (const uint8_t*)src1, (uint8_t*)dst1,
-                           (const uint8_t*)src2, (uint8_t*)dst2, n, (const uint8_t*)dest,
-                           ws.offsets, ws.T, tile_rows, ws.scan_err);
-        return hipGetLastError();
-    };
-    if (g_tune.pack_compact && w1 == 16 && u1 >= 1 && u1 <= 4 && u2 == 3 && (w2 == 8 || w2 == 4)) {
-        prof_begin(s, K_PACK);
-        hipError_t e = hipErrorNotSupported;
-#define MGR_C2(U1_)                                                                  \
-    case U1_:                                                                        \
-        e = w2 == 8 ? go(compact2_kernel<16, U1_, 8, 3>) : go(compact2_kernel<16, U1_, 4, 3>); \
-        break;
-        switch (u1) { MGR_C2(1) MGR_C2(2) MGR_C2(3) MGR_C2(4) default: break; }
-#undef MGR_C2
-        prof_end(s, K_PACK);
-        if (e != hipErrorNotSupported) return e;
+    if (nfields < 1 || nfields > kSelFields) return hipErrorInvalidValue;
+    uint64_t sb = 0;
+    for (int k = 0; k < nsets; ++k) sb |= (uint64_t)(bits[k] & 15) << (4 * k);
+    SelFields fs{};
+    for (int f = 0; f < nfields; ++f) {
+        fs.src[f] = (const uint8_t*)srcs[f];
+        fs.row_bytes[f] = row_bytes[f];
+        uintptr_t a = (uintptr_t)srcs[f] | (uintptr_t)row_bytes[f];
+        for (int k = 0; k < nsets; ++k) {
+            // a set is written in every field or in none (field 0 decides)
+            fs.dst[f][k] = dsts[0 * nsets + k] ? (uint8_t*)dsts[f * nsets + k] : nullptr;
+            a |= (uintptr_t)fs.dst[f][k];
+        }
+        fs.wlog[f] = (a & 15) == 0 ? 4 : (a & 7) == 0 ? 3 : (a & 3) == 0 ? 2 : (a & 1) == 0 ? 1 : 0;
     }
-    // other shapes: one selection pack per field
-    hipError_t e = launch_pack(src1, rb1, n, dest, 2, 1, tile_rows, ws, dst1, -1, nullptr, s);
-    if (e != hipSuccess) return e;
-    return launch_pack(src2, rb2, n, dest, 2, 1, tile_rows, ws, dst2, -1, nullptr, s);
+    const dim3 grid((unsigned)((ws.T + 3) / 4));
+    prof_begin(s, K_PACK);
+    hipLaunchKernelGGL(msel_pack_kernel, grid, dim3(256), 0, s, fs, nfields, n, flags, nsets, sb,
+                       ws.offsets, ws.bin_starts, ws.T, tile_rows, ws.scan_err);
+    prof_end(s, K_PACK);
+    return hipGetLastError();
 }
 
 // Rows of any width: one lane copies one kept row.

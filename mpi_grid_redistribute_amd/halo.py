@@ -19,13 +19,34 @@ positions are not shifted across the periodic boundary; with
 ``periodic=False`` the left send uses the right neighbour's flag (:287);
 ``redistribute_by_position`` never forwards ``periodic`` (:165).
 
-On the GPU a dimension costs one pass over the new rows' flags, four
-selection counts + scans, the packs of the selected rows into contiguous
-send buffers (HIP kernels, libmgr.so) and two point-to-point steps over the
-transport (RCCL ncclSend/ncclRecv for ``RcclComm``); the local rows' flags
-for every dimension come from ONE pass over the local positions
-(``mgr_halo_flags``).  Host syncs: two per dimension (selection counts,
-received counts) -- the reference blocks on every message too.
+On the GPU every row carries 16 face-flag bits (bit 2d: coordinate d beyond
+the right threshold, bit 2d+1: below the left one).  Through
+``redistribute_by_position`` the binning kernel computes them against the
+limits of the cell the row lands in (mgr_bin_count_halo) and they travel
+with the row; called directly, one pass over the local positions computes
+them (mgr_halo_flags).  They stay valid on every rank a row is forwarded to:
+a neighbour's cell differs from the sender's only in the dimension of the
+exchange, whose bits are not read again.
+
+  1. the local rows' 2*dim selections counted in ONE pass (mgr_msel_count,
+     mgr_scan); one group exchanges the counts with the neighbours; one host
+     sync reads them;
+  2. the local sends of every dimension whose neighbours are other ranks
+     (and of dimension 0) are packed in one pass (mgr_msel_pack_fields:
+     data, positions when carried, flags), each set straight to its place;
+  3. per dimension d: the received rows so far (the buffer) are selected the
+     same way (2 sets) -- a small set; from d = 1 their counts travel as an
+     8-byte message and one host sync reads them; then ONE group moves, in
+     the reference's order (step 1, then step 2), the local piece and the
+     buffer piece of every field to each neighbour, the receives landing
+     appended to the buffer in place.  A dimension whose neighbours are this
+     rank itself (a grid extent of 1) sends nothing: its pieces are packed
+     straight into the buffer where the receives would land.
+Host syncs: 1 + (dim - 1) per exchange.  The buffer is an append-only store:
+redistribute_by_position hands over the spare rows of its output, so the
+final concatenate(data, overload) (:166) costs nothing while the halo fits;
+when the positions are not returned they are not carried at all (the flags
+already hold everything the selections read).
 """
 from __future__ import annotations
 
@@ -35,6 +56,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .comm import excl_cumsum
 
 
 def neighbours(R, d, periodic):
@@ -68,21 +90,31 @@ SELECT_TILE_ROWS = 4096
 
 def halo_capacity(R, m, overload_lengths):
     """Spare rows to reserve after a rank's m redistributed rows for its halo:
-    the uniform-density estimate m * (prod(1 + 2 ol/len) - 1), x1.25, + 4096.
-    A halo that outgrows it still works (exchange_overload then moves to its
-    own store and the caller concatenates)."""
+    the uniform-density estimate m * (prod(1 + 2 ol/len) - 1), x1.25, + 4096,
+    with ol capped at the cell length (the exchange reaches the immediate
+    neighbours only, so each factor is at most 3) and the whole at
+    (3^dim - 1) * m.  A halo that outgrows it still works (exchange_overload
+    then moves to its own store and the caller concatenates)."""
     cl = np.asarray(R.cell_length, dtype=np.float64)
-    ol = np.maximum(np.asarray(overload_lengths, dtype=np.float64), 0.0)
-    frac = float(np.prod(1.0 + 2.0 * ol / cl) - 1.0)
+    ol = np.minimum(np.maximum(np.asarray(overload_lengths, dtype=np.float64), 0.0), cl)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        frac = float(np.prod(1.0 + 2.0 * np.where(cl > 0, ol / cl, 1.0)) - 1.0)
+    frac = min(frac, 3.0 ** len(cl) - 1.0)
     return int(m * frac * 1.25) + 4096
 
 
 class DeviceSelect:
-    """Selections on the GPU: flags (mgr_halo_flags), per-mask 2-bin
-    partition counts (mgr_select_count + mgr_scan) and stable packs."""
+    """Selections on the GPU: face flags (mgr_halo_flags) and multi-set
+    selections (mgr_msel_count + mgr_scan + mgr_msel_pack)."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, scratch=None):
         self.dev = dev
+        self.scratch = scratch
+
+    def _buf(self, name, nbytes):
+        if self.scratch is not None:
+            return self.scratch.get(name, nbytes)
+        return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.dev)
 
     def flags(self, pos_flat, n, ncols, code, dim, hi, lo):
         f = torch.empty(max(n, 1), dtype=torch.int16, device=self.dev)
@@ -93,117 +125,243 @@ class DeviceSelect:
                   _lib.ptr(f), _lib.stream_handle())
         return f
 
-    def select(self, flags, n, mask, max_row_bytes):
-        """-> (handle, count tensor [1] on the device)."""
+    def msel(self, flags, n, bits, tag):
+        """Counts of the sets {rows with flag bit bits[k]} -> (handle, device
+        int64 counts [len(bits)])."""
         lib = _lib.load()
-        # long tiles: the selection pack is a wave-per-tile compaction
-        # (mgr_pack with 2 bins, bin 1 dropped), whose cost is per tile
         tile_rows = SELECT_TILE_ROWS
-        ws = torch.empty(int(lib.mgr_workspace_bytes(int(n), 2, tile_rows)), dtype=torch.uint8,
-                         device=self.dev)
-        dest = torch.empty(max(n, 1), dtype=torch.uint8, device=self.dev)
-        counts = torch.empty(2, dtype=torch.int64, device=self.dev)
+        k = len(bits)
+        ws = self._buf("msel_ws" + tag, int(lib.mgr_workspace_bytes(int(n), k, tile_rows)))
+        counts = torch.empty(k, dtype=torch.int64, device=self.dev)
+        cb = (ctypes.c_int * k)(*bits)
         s = _lib.stream_handle()
-        _lib.call("mgr_select_count", _lib.ptr(flags), n, int(mask), _lib.ptr(dest), tile_rows,
-                  _lib.ptr(ws), s)
-        _lib.call("mgr_scan", n, 2, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
-        return (n, dest, ws, tile_rows), counts[:1]
+        _lib.call("mgr_msel_count", _lib.ptr(flags), n, k, cb, tile_rows, _lib.ptr(ws), s)
+        _lib.call("mgr_scan", n, k, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+        return (n, flags, cb, k, ws, tile_rows), counts
 
-    def pack(self, handle, src_flat, row_bytes, dst_flat):
-        n, dest, ws, tile_rows = handle
-        _lib.call("mgr_pack", _lib.ptr(src_flat), row_bytes, n, _lib.ptr(dest), 2, 1, tile_rows,
-                  _lib.ptr(ws), _lib.ptr(dst_flat), -1, None, _lib.stream_handle())
+    def msel_pack(self, handle, src_flat, row_bytes, dsts):
+        """One field's selected rows: set k's rows, in row order, to dsts[k]
+        (a flat uint8 tensor, or None: set k not written)."""
+        n, flags, cb, k, ws, tile_rows = handle
+        ptrs = (ctypes.c_void_p * k)(*[None if t is None else _lib.ptr(t) for t in dsts])
+        _lib.call("mgr_msel_pack", _lib.ptr(src_flat), row_bytes, n, _lib.ptr(flags), k, cb,
+                  tile_rows, _lib.ptr(ws), ptrs, _lib.stream_handle())
 
-    def pack2(self, handle, src1, rb1, dst1, src2, rb2, dst2):
-        """Both fields of the selection in one pass (mgr_select_pack2)."""
-        n, dest, ws, tile_rows = handle
-        _lib.call("mgr_select_pack2", _lib.ptr(src1), rb1, _lib.ptr(dst1), _lib.ptr(src2), rb2,
-                  _lib.ptr(dst2), n, _lib.ptr(dest), tile_rows, _lib.ptr(ws),
-                  _lib.stream_handle())
+    def msel_pack_fields(self, handle, srcs, row_bytes, dsts):
+        """Several fields of the same rows in one pass: dsts[f][k] as in
+        msel_pack (field 0's None entries decide which sets are written)."""
+        n, flags, cb, k, ws, tile_rows = handle
+        nf = len(srcs)
+        sp = (ctypes.c_void_p * nf)(*[_lib.ptr(t) for t in srcs])
+        rb = (ctypes.c_int64 * nf)(*row_bytes)
+        dp = (ctypes.c_void_p * (nf * k))(*[None if t is None else _lib.ptr(t)
+                                             for row in dsts for t in row])
+        _lib.call("mgr_msel_pack_fields", nf, sp, rb, n, _lib.ptr(flags), k, cb, tile_rows,
+                  _lib.ptr(ws), dp, _lib.stream_handle())
+
+    def to_host(self, tensors):
+        """One device->host read of several small int64 tensors (one sync)."""
+        flat = torch.cat([t.reshape(-1) for t in tensors]) if len(tensors) > 1 else tensors[0]
+        host = flat.cpu().numpy()
+        out, o = [], 0
+        for t in tensors:
+            out.append(host[o:o + t.numel()].copy())
+            o += t.numel()
+        return out
 
 
 def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n,
-                      overload_lengths, periodic=True, sel=None, arena=None):
-    """Overload rows of rank R (redist.py:202-309).  ``data_flat``/``pos_flat``:
-    flat uint8 tensors of this rank's n rows (payload rows of ``rbd`` bytes;
-    positions (n, ncols) float32/float64 rows, ncols >= dim).  The overload
-    buffer only grows at its end (concat(buffer, from_a, from_b), :305), so
-    its rows live in an append-only store: ``arena`` = (data store, position
-    store, first row, spare rows), e.g. the free tail of the redistribution's
-    output, is used while the rows fit; beyond it the rows move once to a
-    store of their own with headroom.  Returns (overload data flat, overload
-    positions flat, rows, whether they stayed in the arena)."""
+                      overload_lengths, periodic=True, sel=None, arena=None, flags=None):
+    """Overload rows of rank R (redist.py:202-309).  ``data_flat``: flat uint8
+    tensor of this rank's n payload rows of ``rbd`` bytes; ``pos_flat``: their
+    positions (n, ncols) float32/float64 rows (ncols >= dim), or None when the
+    positions are not wanted back and ``flags`` is given.  ``flags``: the
+    rows' face flags (int16 [n]) when the binning computed them, else one pass
+    computes them from the positions here.  The overload buffer only grows at
+    its end (concat(buffer, from_a, from_b), :305), so its rows live in an
+    append-only store: ``arena`` = (data store, position store or None, first
+    row, spare rows), e.g. the free tail of the redistribution's output, is
+    used while the rows fit; beyond it the rows move once to a store of their
+    own with headroom.  Returns (overload data flat, overload positions flat
+    or None, rows, whether they stayed in the arena)."""
     dim = R.dim
     assert len(overload_lengths) == dim, \
         "Overload lengths must be the same length as the dimensions"  # redist.py:245
     dev = data_flat.device
     sel = sel or DeviceSelect(dev)
+    carry_pos = pos_flat is not None
+    if flags is None:
+        hi, lo = thresholds(R, overload_lengths)
+        flags = sel.flags(pos_flat, n, ncols, pos_code, dim, hi, lo)
+    flags_flat = flags.reshape(-1).view(torch.uint8)[: 2 * n]
     isz = 4 if pos_code == _lib.MGR_F32 else 8
-    rbp = ncols * isz
-    hi, lo = thresholds(R, overload_lengths)
-    seg_local = (sel.flags(pos_flat, n, ncols, pos_code, dim, hi, lo), n, data_flat, pos_flat)
+    srcs = [data_flat] + ([pos_flat] if carry_pos else []) + [flags_flat]
+    rbs = [rbd] + ([ncols * isz] if carry_pos else []) + [2]
+    F, FL = len(rbs), len(rbs) - 1                        # fields; the flags field
+    me = transport.rank
+    nb = [neighbours(R, d, periodic) for d in range(dim)]
+    selfd = [a == me and b == me for a, b, _, _ in nb]
+
+    # 1. the local rows' counts of every dimension's two selections, one pass
+    S = 2 * dim
+    lh, lcount = sel.msel(flags, n, list(range(S)), "_local")
+    # 2. local counts to the neighbours (step 1 then step 2 of every dimension)
+    send_l = torch.zeros(S, dtype=torch.int64, device=dev)
+    send_l.copy_(lcount)
+    for d, (a, b, keep_a, keep_b) in enumerate(nb):
+        if not keep_a:
+            send_l[2 * d].zero_()
+        if not keep_b:
+            send_l[2 * d + 1].zero_()
+    recv_l = torch.zeros(S, dtype=torch.int64, device=dev)   # [from_b, from_a] per dimension
+    ops = []
+    for d, (a, b, _, _) in enumerate(nb):
+        ops += [("send", a, send_l[2 * d:2 * d + 1].view(torch.uint8)),
+                ("recv", b, recv_l[2 * d:2 * d + 1].view(torch.uint8)),
+                ("send", b, send_l[2 * d + 1:2 * d + 2].view(torch.uint8)),
+                ("recv", a, recv_l[2 * d + 1:2 * d + 2].view(torch.uint8))]
+    transport.p2p(ops)
+    ls, rl = sel.to_host([send_l, recv_l])                   # host sync 1
+
+    # the append-only overload store: data (+ positions) + flags
+    st = [None] * F
+    base, cap, in_arena = 0, 0, False
     if arena is not None:
-        st_d, st_p, base, cap = arena
-    else:
-        st_d = st_p = None
-        base, cap = 0, 0
-    in_arena = arena is not None
+        st[0] = arena[0]
+        if carry_pos:
+            st[1] = arena[1]
+        base, cap, in_arena = arena[2], arena[3], True
+        st[FL] = torch.empty(max(cap, 1) * 2, dtype=torch.uint8, device=dev)
+    fbase = [base] * (F - 1) + [0]                           # the flags store is our own
     m = 0
-    for d in range(dim):
-        a, b, keep_a, keep_b = neighbours(R, d, periodic)
-        segs = [seg_local]
-        if m:
-            ov_d = st_d[base * rbd:(base + m) * rbd]
-            ov_p = st_p[base * rbp:(base + m) * rbp]
-            segs.append((sel.flags(ov_p, m, ncols, pos_code, dim, hi, lo), m, ov_d, ov_p))
-        sends = []
-        for mask, keep in ((1 << (2 * d), keep_a), (1 << (2 * d + 1), keep_b)):
-            picks = [sel.select(f, k, mask, max(rbd, rbp)) + (dd, pp)
-                     for f, k, dd, pp in segs if k > 0] if keep else []
-            sends.append(picks)
-        flat_counts = [p[1] for picks in sends for p in picks]
-        host = torch.cat(flat_counts).cpu().tolist() if flat_counts else []
-        cnt = [host[: len(sends[0])], host[len(sends[0]):]]
-        bufs = []
-        for picks, cs in zip(sends, cnt):
-            tot = int(sum(cs))
-            bd = torch.empty(max(tot * rbd, 1), dtype=torch.uint8, device=dev)
-            bp = torch.empty(max(tot * rbp, 1), dtype=torch.uint8, device=dev)
-            o = 0
-            for (h, _, dd, pp), c in zip(picks, cs):
-                if c:
-                    # two selection packs: the fused one (sel.pack2) measured
-                    # no faster (sparse rows cost a line each either way)
-                    sel.pack(h, dd, rbd, bd[o * rbd:])
-                    sel.pack(h, pp, rbp, bp[o * rbp:])
-                o += c
-            bufs.append((tot, bd[: tot * rbd], bp[: tot * rbp]))
-        # row counts first (8-byte messages), both steps, then one host sync
-        n_a, n_b = bufs[0][0], bufs[1][0]
-        cs = torch.tensor([n_a, n_b], dtype=torch.int64, device=dev)
-        cr = torch.zeros(2, dtype=torch.int64, device=dev)
-        transport.sendrecv(cs[0:1].view(torch.uint8), a, cr[0:1].view(torch.uint8), b)  # :289-295
-        transport.sendrecv(cs[1:2].view(torch.uint8), b, cr[1:2].view(torch.uint8), a)  # :298-303
-        r_from_b, r_from_a = (int(x) for x in cr.cpu().tolist())
-        new_m = m + r_from_a + r_from_b
-        if st_d is None or new_m > cap:
-            # outgrew the store: a store of its own with headroom, rows so far moved once
-            ncap = max(2 * new_m, 1024)
-            nd = torch.empty(ncap * rbd, dtype=torch.uint8, device=dev)
-            npb = torch.empty(ncap * rbp, dtype=torch.uint8, device=dev)
+
+    def store(f, row0=0, rows=None):
+        o = (fbase[f] + row0) * rbs[f]
+        return st[f][o:] if rows is None else st[f][o:o + rows * rbs[f]]
+
+    def ensure(new_m):
+        nonlocal st, fbase, cap, in_arena
+        if st[0] is not None and new_m <= cap:
+            return
+        # outgrew the store: a store of its own with headroom, rows so far moved once
+        ncap = max(2 * new_m, 1024)
+        nst = [torch.empty(ncap * rb, dtype=torch.uint8, device=dev) for rb in rbs]
+        for f in range(F):
             if m:
-                nd[: m * rbd].copy_(st_d[base * rbd:(base + m) * rbd])
-                npb[: m * rbp].copy_(st_p[base * rbp:(base + m) * rbp])
-            st_d, st_p, base, cap, in_arena = nd, npb, 0, ncap, False
+                nst[f][: m * rbs[f]].copy_(store(f, 0, m))
+        st, fbase, cap, in_arena = nst, [0] * F, ncap, False
+
+    def local_pieces(d):
+        """Rows this rank sends in dimension d: its local piece then its
+        buffer piece, to a (step 1) and to b (step 2)."""
+        a, b, keep_a, keep_b = nb[d]
+        return (int(ls[2 * d]) if keep_a else 0), (int(ls[2 * d + 1]) if keep_b else 0)
+
+    # local sends staged for the neighbours: every non-self dimension's sets
+    # (and dimension 0's, whose place in the store is known now) in one pass;
+    # the sets of a later self dimension are written straight into the store
+    # when that dimension comes (their place depends on the earlier receives)
+    stage_off, off = {}, 0
+    for d in range(dim):
+        if not selfd[d]:
+            nla, nlb = local_pieces(d)
+            stage_off[d] = off
+            off += nla + nlb
+    lbuf = [sel._buf(f"halo_local{f}", off * rbs[f]) for f in range(F)]
+
+    def local_dsts(d, f, ia, ib):
+        """Set -> destination of dimension d's local pieces, field f."""
+        nla, nlb = local_pieces(d)
+        rb = rbs[f]
+        if selfd[d]:   # step 1 (to a = me) lands at ib, step 2 (to b = me) at ia
+            return {2 * d: store(f, ib, nla) if nla else None,
+                    2 * d + 1: store(f, ia, nlb) if nlb else None}
+        o = stage_off[d]
+        return {2 * d: lbuf[f][o * rb:(o + nla) * rb] if nla else None,
+                2 * d + 1: lbuf[f][(o + nla) * rb:(o + nla + nlb) * rb] if nlb else None}
+
+    def pack_local(dims, places):
+        dsts = [[None] * S for _ in range(F)]
+        for d in dims:
+            for f in range(F):
+                for k, t in local_dsts(d, f, *places.get(d, (0, 0))).items():
+                    dsts[f][k] = t
+        if any(t is not None for t in dsts[0]):
+            sel.msel_pack_fields(lh, srcs, rbs, dsts)
+
+    first = [d for d in range(dim) if not selfd[d] or d == 0]
+    if selfd[0]:
+        nla, nlb = local_pieces(0)
+        ensure(nla + nlb)
+    pack_local(first, {0: (0, local_pieces(0)[1])} if selfd[0] else {})
+
+    for d, (a, b, keep_a, keep_b) in enumerate(nb):
+        sa, sb = 2 * d, 2 * d + 1
+        # 3. the buffer's selections for this dimension (rows received so far)
+        gc = np.zeros(2, dtype=np.int64)
+        rg = np.zeros(2, dtype=np.int64)
+        gh = None
+        if d > 0:
+            send_g = torch.zeros(2, dtype=torch.int64, device=dev)
+            recv_g = torch.zeros(2, dtype=torch.int64, device=dev)
+            if m:
+                gh, gcount = sel.msel(store(FL, 0, m).view(torch.int16), m, [sa, sb], "_ghost")
+                send_g.copy_(gcount)
+            if not keep_a:
+                send_g[0].zero_()
+            if not keep_b:
+                send_g[1].zero_()
+            transport.p2p([("send", a, send_g[0:1].view(torch.uint8)),
+                           ("recv", b, recv_g[0:1].view(torch.uint8)),
+                           ("send", b, send_g[1:2].view(torch.uint8)),
+                           ("recv", a, recv_g[1:2].view(torch.uint8))])
+            gc, rg = sel.to_host([send_g, recv_g])            # host sync per dimension
+        nla, nlb = local_pieces(d)
+        nga, ngb = int(gc[0]), int(gc[1])
+        # what it receives: from_b (step 1) and from_a (step 2), each a local
+        # piece and a buffer piece of the sender
+        rlb, rla = int(rl[sa]), int(rl[sb])
+        rgb, rga = int(rg[0]), int(rg[1])
+        new_m = m + rla + rga + rlb + rgb
+        ensure(new_m)
         # concat(buffer, from_a, from_b) (redist.py:305): appended in place
-        od, op = st_d[base * rbd:], st_p[base * rbp:]
-        ia, ib = m, m + r_from_a
-        transport.sendrecv(bufs[0][1], a, od[ib * rbd:(ib + r_from_b) * rbd], b)
-        transport.sendrecv(bufs[0][2], a, op[ib * rbp:(ib + r_from_b) * rbp], b)
-        transport.sendrecv(bufs[1][1], b, od[ia * rbd:(ia + r_from_a) * rbd], a)
-        transport.sendrecv(bufs[1][2], b, op[ia * rbp:(ia + r_from_a) * rbp], a)
+        ia, ib = m, m + rla + rga
+        if selfd[d] and d > 0:
+            pack_local([d], {d: (ia, ib)})
+        gsz = nga + ngb
+        gbuf = None
+        if gsz:
+            if selfd[d]:
+                gd = [[store(f, ib + nla, nga) if nga else None,
+                       store(f, ia + nlb, ngb) if ngb else None] for f in range(F)]
+            else:
+                gbuf = [sel._buf(f"halo_ghost{f}", gsz * rbs[f]) for f in range(F)]
+                gd = [[gbuf[f][: nga * rbs[f]] if nga else None,
+                       gbuf[f][nga * rbs[f]:gsz * rbs[f]] if ngb else None] for f in range(F)]
+            sel.msel_pack_fields(gh, [store(f, 0, m) for f in range(F)], rbs, gd)
+        if selfd[d]:
+            m = new_m
+            continue
+        ops = []
+        o = stage_off[d]
+        for step in (1, 2):
+            to, frm = (a, b) if step == 1 else (b, a)
+            nl, ng = (nla, nga) if step == 1 else (nlb, ngb)
+            lo_, go_ = (o, 0) if step == 1 else (o + nla, nga)
+            rl_, rg_, at = (rlb, rgb, ib) if step == 1 else (rla, rga, ia)
+            for f in range(F):
+                rb = rbs[f]
+                if nl:
+                    ops.append(("send", to, lbuf[f][lo_ * rb:(lo_ + nl) * rb]))
+                if ng:
+                    ops.append(("send", to, gbuf[f][go_ * rb:(go_ + ng) * rb]))
+                if rl_:
+                    ops.append(("recv", frm, store(f, at, rl_)))
+                if rg_:
+                    ops.append(("recv", frm, store(f, at + rl_, rg_)))
+        transport.p2p(ops)
         m = new_m
     if not m:
         empty = torch.empty(0, dtype=torch.uint8, device=dev)
-        return empty, empty, 0, in_arena
-    return st_d[base * rbd:(base + m) * rbd], st_p[base * rbp:(base + m) * rbp], m, in_arena
+        return empty, (empty if carry_pos else None), 0, in_arena
+    return store(0, 0, m), (store(1, 0, m) if carry_pos else None), m, in_arena

@@ -40,7 +40,7 @@ from . import _lib
 from ._arrays import Positions, Rows, box_dtype_code, device, id_array
 from .comm import SelfComm, as_transport
 from .exchange import check_counts, exchange
-from .halo import exchange_overload, halo_capacity
+from .halo import DeviceSelect, exchange_overload, halo_capacity, thresholds
 
 
 class _Plan:
@@ -337,9 +337,10 @@ class MPIGridRedistributor:
         halo = overload_lengths is not None
         if halo:
             self._check_halo(overload_lengths)
-        want_pos = return_positions or halo
+            return self._redistribute_halo(data, position, rows, pos, periodic,
+                                           overload_lengths, return_positions)
         fields = [rows]
-        if want_pos:
+        if return_positions:
             fields.append(None)  # filled after binning (wrapped values)
 
         def binner(dest, tile_rows, ws):
@@ -347,36 +348,65 @@ class MPIGridRedistributor:
                       pos.stride, int(bool(periodic)), _lib.ptr(dest), tile_rows, _lib.ptr(ws),
                       _lib.stream_handle())
             pos.finish()
-            if want_pos:  # redist.py:164: the wrapped positions, full rows
+            if return_positions:  # the wrapped positions, full rows
                 fields[1] = Rows(position, self._dev)
 
         row_bytes_hint = [rows.row_bytes]
-        if want_pos:
+        if return_positions:
             row_bytes_hint.append(self._pos_row_bytes(position, pos))
-        extra = (lambda m_: halo_capacity(self, m_, overload_lengths)) if halo else None
-        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=row_bytes_hint,
-                            extra_rows=extra)
-        if not halo:
-            res = rows.wrap(outs[0], m)
-            if return_positions:
-                return res, fields[1].wrap(outs[1], m)
-            return res
-        rbd, rbp = rows.row_bytes, fields[1].row_bytes
-        # the halo rows are appended in place after the m received rows while
-        # they fit the spare capacity (no concatenation copies)
+        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=row_bytes_hint)
+        res = rows.wrap(outs[0], m)
+        if return_positions:
+            return res, fields[1].wrap(outs[1], m)
+        return res
+
+    def _redistribute_halo(self, data, position, rows, pos, periodic, overload_lengths,
+                           return_positions):
+        """redist.py:157-166 with overload_lengths: the binning kernel also
+        writes every row's halo face flags against the cell it lands in
+        (mgr_bin_count_halo); rows, flags (a side field of the same pack) and
+        wrapped positions (:164) are redistributed together; the overload
+        exchange (halo.py) then starts from the received flags and appends
+        the halo rows in place after the m received rows while they fit the
+        spare capacity (no concatenation copies)."""
+        flags_src = self._scratch.get("halo_flags_src", max(rows.n, 1) * 2)
+        rp = bool(return_positions)
+        fields = [rows, _IdField(flags_src)] + ([None] if rp else [])
+        cl = np.ascontiguousarray(self.cell_length, dtype=np.float64)
+        ol = np.ascontiguousarray(np.asarray(overload_lengths, dtype=np.float64))
+
+        def binner(dest, tile_rows, ws):
+            _lib.call("mgr_bin_count_halo", self._plan.h, ctypes.c_void_p(pos.addr), pos.code,
+                      pos.n, pos.stride, int(bool(periodic)), _lib.ptr(dest), _lib.ptr(flags_src),
+                      cl.ctypes.data_as(ctypes.c_void_p), ol.ctypes.data_as(ctypes.c_void_p),
+                      tile_rows, _lib.ptr(ws), _lib.stream_handle())
+            pos.finish()
+            if rp:   # redist.py:164: the wrapped positions travel with the rows
+                fields[2] = Rows(position, self._dev)
+
+        hint = [rows.row_bytes, 2] + ([self._pos_row_bytes(position, pos)] if rp else [])
+        extra = lambda m_: halo_capacity(self, m_, overload_lengths)  # noqa: E731
+        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=hint,
+                            extra_rows=extra, side_ids=True)
+        rbd = rows.row_bytes
+        rbp = fields[2].row_bytes if rp else 0
         cap = outs[0].numel() // max(rbd, 1) - m
+        flags = outs[1][: 2 * m].view(torch.int16) if m else torch.empty(
+            0, dtype=torch.int16, device=self._dev)
         ov_d, ov_p, mo, in_place = exchange_overload(
-            self, self.comm, outs[0][: m * rbd], rbd, outs[1][: m * rbp],
+            self, self.comm, outs[0][: m * rbd], rbd, outs[2][: m * rbp] if rp else None,
             int(position.shape[1]), pos.code, m, list(overload_lengths), periodic=True,
-            arena=(outs[0], outs[1], m, cap))
+            sel=DeviceSelect(self._dev, self._scratch),
+            arena=(outs[0], outs[2] if rp else None, m, cap), flags=flags)
         if in_place:   # redist.py:166: concatenate(data, overload)
-            res_d, res_p = outs[0][: (m + mo) * rbd], outs[1][: (m + mo) * rbp]
+            res_d = outs[0][: (m + mo) * rbd]
+            res_p = outs[2][: (m + mo) * rbp] if rp else None
         else:
             res_d = torch.cat([outs[0][: m * rbd], ov_d])
-            res_p = torch.cat([outs[1][: m * rbp], ov_p]) if return_positions else None
+            res_p = torch.cat([outs[2][: m * rbp], ov_p]) if rp else None
         res = rows.wrap(res_d, m + mo)
-        if return_positions:
-            return res, fields[1].wrap(res_p, m + mo)
+        if rp:
+            return res, fields[2].wrap(res_p, m + mo)
         return res
 
     def _fine_plan(self, fine_cells):
@@ -445,9 +475,17 @@ class MPIGridRedistributor:
             raise TypeError(f"position dtype {position.dtype} not supported (float32/float64)")
         if prow.n != rows.n:
             raise ValueError(f"data has {rows.n} rows, position has {prow.n}")
+        sel = DeviceSelect(self._dev, self._scratch)
+        ncols = int(position.shape[1])
+        flags, pflat = None, prow.flat
+        if not return_positions:   # the flags are all the selections read
+            hi, lo = thresholds(self, overload_lengths)
+            flags = sel.flags(prow.flat, rows.n, ncols, code, self.dim, hi, lo)
+            pflat = None
         ov_d, ov_p, mo, _ = exchange_overload(self, self.comm, rows.flat, rows.row_bytes,
-                                              prow.flat, int(position.shape[1]), code, rows.n,
-                                              list(overload_lengths), periodic=bool(periodic))
+                                              pflat, ncols, code, rows.n,
+                                              list(overload_lengths), periodic=bool(periodic),
+                                              sel=sel, flags=flags)
         res = rows.wrap(ov_d, mo)
         return (res, prow.wrap(ov_p, mo)) if return_positions else res
 

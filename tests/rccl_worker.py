@@ -2,7 +2,7 @@
 
 Runs the product transport -- RcclComm, i.e. libmgr.so's mgr_exchange_counts,
 mgr_exchange_rows (grouped ncclSend/ncclRecv, receives in place at
-source-ordered offsets) and mgr_sendrecv (the halo's isend/irecv pairs) --
+source-ordered offsets) and mgr_group_p2p (the halo's isend/irecv batches) --
 between distinct ranks, and checks every rank's result bit-exact against the
 reference's own outputs (tests/golden/*.npz) and the oracle.  Replaces
 ``comm.alltoall`` (redist.py:199) and the isend/irecv pairs (redist.py:289-303).

@@ -89,16 +89,20 @@ def test_product_refuses_without_gpu():
         m.GridPartitioner([2], [1.0])
 
 
-def test_select_pack2_validation(lib):
-    """mgr_select_pack2 argument checks run on the host before any launch."""
-    from mpi_grid_redistribute_amd import _lib
-    fn = lib.mgr_select_pack2
-    tr = _lib.SELECT_TILE_ROWS if hasattr(_lib, "SELECT_TILE_ROWS") else 4096
+def test_msel_validation(lib):
+    """mgr_msel_count / mgr_msel_pack argument checks run on the host before
+    any launch."""
     buf = ctypes.create_string_buffer(64)
     p = ctypes.cast(buf, ctypes.c_void_p)
-    assert fn(p, 0, p, p, 24, p, 1, p, tr, p, None) < 0          # row_bytes < 1
+    bits = (ctypes.c_int * 2)(0, 1)
+    bad = (ctypes.c_int * 2)(0, 16)
+    assert lib.mgr_msel_count(p, 5, 0, bits, 4096, p, None) < 0        # no sets
+    assert b"nsets" in lib.mgr_last_error()
+    assert lib.mgr_msel_count(p, 5, 2, bad, 4096, p, None) < 0         # flag bit 16
+    assert b"flag bit" in lib.mgr_last_error()
+    assert lib.mgr_msel_count(p, 5, 2, bits, 100, p, None) < 0         # tile not a multiple of 64
+    assert lib.mgr_msel_pack(p, 0, 5, p, 2, bits, 4096, p, p, None) < 0  # row_bytes < 1
     assert b"row_bytes" in lib.mgr_last_error()
-    assert fn(None, 32, p, p, 24, p, 5, p, tr, p, None) < 0      # null source with rows
+    assert lib.mgr_msel_pack(None, 8, 5, p, 2, bits, 4096, p, p, None) < 0  # null source
     assert b"null" in lib.mgr_last_error()
-    assert fn(p, 32, p, p, 24, p, 5, p, 100, p, None) < 0        # tile not a multiple of 64
-    assert fn(None, 32, None, None, 24, None, 0, None, tr, None, None) == 0  # empty: no-op
+    assert lib.mgr_msel_pack(None, 8, 0, None, 2, bits, 4096, None, None, None) == 0  # empty

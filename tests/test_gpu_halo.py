@@ -1,6 +1,7 @@
 """GPU parity of the overload (halo) exchange (redist.py:161-166, :202-309):
-HIP selection kernels (mgr_halo_flags, mgr_select_count, mgr_scan,
-mgr_pack) + the transport's sendrecv, bit-exact against the reference's own
+face flags from the binning kernel (mgr_bin_count_halo) or mgr_halo_flags,
+multi-selections (mgr_msel_count, mgr_scan, mgr_msel_pack) and the
+transport's grouped point-to-point batches, bit-exact against the reference's own
 outputs (tests/golden/halo_*.npz) and the NumPy oracle on larger inputs."""
 import numpy as np
 import pytest
@@ -107,8 +108,8 @@ def test_halo_large_vs_oracle_with_positions():
 
 
 def test_halo_rccl_single_rank():
-    """RcclComm at world size 1: neighbours are the rank itself (mgr_sendrecv
-    self copy), periodic self-images without a shift."""
+    """RcclComm at world size 1: neighbours are the rank itself (mgr_group_p2p
+    self copies), periodic self-images without a shift."""
     from mpi_grid_redistribute_amd import RcclComm
     f = G.load("halo_p1_self.npz")
     comm = RcclComm(RcclComm.unique_id(), 1, 0)
@@ -165,37 +166,85 @@ def test_halo_in_place_and_overflow(clustered):
     assert all(fits) if not clustered else not any(fits)
 
 
-@pytest.mark.parametrize("compact", [1, 0])
-@pytest.mark.parametrize("rb1,rb2", [(32, 24), (16, 12), (48, 24), (64, 12), (36, 12), (32, 16)])
-@pytest.mark.parametrize("n,frac", [(1, 1.0), (4095, 0.1), (4097, 0.5), (300001, 0.07),
-                                    (1 << 20, 0.0), (1 << 20, 1.0)])
-def test_select_pack2(n, frac, rb1, rb2, compact):
-    """mgr_select_pack2 (fused two-field selection pack, the fused kernel or
-    its two-pack fallback for other row shapes) = data[sel], pos[sel] in
-    order, the selection the halo takes per direction (redist.py:271-275)."""
-    from mpi_grid_redistribute_amd import _lib
+@pytest.mark.parametrize("rb,offset", [(32, 0), (24, 0), (12, 0), (36, 0), (6, 0), (3, 0),
+                                       (64, 0), (100, 0), (200, 8), (7, 1)])
+@pytest.mark.parametrize("n,nsets", [(1, 2), (4095, 6), (4097, 1), (300001, 6), (1 << 18, 16)])
+def test_msel_pack(n, nsets, rb, offset):
+    """mgr_msel_count + mgr_scan + mgr_msel_pack: set k = rows with flag bit
+    bits[k], every set's rows in order, set after set (the halo's local sends
+    of every dimension and direction, redist.py:271-275) -- the <= 64-byte
+    kernel and the wide/unaligned one."""
     from mpi_grid_redistribute_amd.halo import DeviceSelect
-    rng = np.random.default_rng(n + rb1 * 7 + rb2)
-    flags = (rng.random(n) < frac).astype(np.uint16) * 4 + rng.integers(0, 2, n).astype(np.uint16)
-    a = rng.integers(0, 256, (n, rb1), dtype=np.uint8)
-    b = rng.integers(0, 256, (n, rb2), dtype=np.uint8)
-    keep = (flags & 4) != 0
-    _lib.tune("pack_compact", compact)
-    try:
-        sel = DeviceSelect(torch.device("cuda"))
-        fl = torch.from_numpy(flags.view(np.int16)).cuda()
-        h, cnt = sel.select(fl, n, 4, max(rb1, rb2))
-        da = torch.from_numpy(a.reshape(-1)).cuda()
-        db = torch.from_numpy(b.reshape(-1)).cuda()
-        k = int(keep.sum())
-        oa = torch.full((max(k, 1) * rb1 + 64,), 0xAB, dtype=torch.uint8, device="cuda")
-        ob = torch.full((max(k, 1) * rb2 + 64,), 0xCD, dtype=torch.uint8, device="cuda")
-        sel.pack2(h, da, rb1, oa, db, rb2, ob)
+    rng = np.random.default_rng(n + 7 * rb + nsets)
+    flags = rng.integers(0, 1 << 16, n).astype(np.uint16) & rng.integers(0, 1 << 16, n).astype(np.uint16)
+    flags[rng.random(n) < 0.5] = 0
+    bits = list(rng.permutation(16)[:nsets])
+    a = rng.integers(0, 256, (n, rb), dtype=np.uint8)
+    sel = DeviceSelect(torch.device("cuda"))
+    fl = torch.from_numpy(flags.view(np.int16)).cuda()
+    h, cnt = sel.msel(fl, n, bits, "_t")
+    src = torch.zeros(n * rb + offset, dtype=torch.uint8, device="cuda")
+    src[offset:].copy_(torch.from_numpy(a.reshape(-1)))
+    want = [a[(flags >> b) & 1 == 1] for b in bits]
+    tot = sum(len(w) for w in want)
+    dst = torch.full((tot * rb + offset + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    starts = np.concatenate([[0], np.cumsum([len(w_) for w_ in want])])
+    sel.msel_pack(h, src[offset:], rb, [dst[offset + starts[k] * rb:] for k in range(nsets)])
+    torch.cuda.synchronize()
+    assert cnt.cpu().tolist() == [len(w) for w in want]
+    out = dst.cpu().numpy()
+    exp = np.concatenate(want).reshape(-1) if tot else np.zeros(0, np.uint8)
+    np.testing.assert_array_equal(out[offset:offset + tot * rb], exp)
+    assert (out[:offset] == 0xAB).all() and (out[offset + tot * rb:] == 0xAB).all()
+
+
+@pytest.mark.parametrize("rec_bytes", [100, 7])
+def test_halo_wide_rows_vs_oracle(rec_bytes):
+    """Payload rows wider than 64 bytes (and odd-sized ones) through the
+    fused halo path: 4 ranks, f32 positions."""
+    rng = np.random.default_rng(rec_bytes)
+    size, topo, box, ol = 4, [2, 1, 2], [2.0, 1.0, 1.0], [0.2, 0.3, 0.1]
+    pos = [rng.uniform(0.0, 1.0, (20_000 + 500 * r, 3)).astype(np.float32) * np.float32([2, 1, 1])
+           for r in range(size)]
+    data = [rng.integers(0, 256, (len(p), rec_bytes), dtype=np.uint8) for p in pos]
+    pos_o = [p.copy() for p in pos]
+    exp = ro.redistribute_by_position_overload_all_ranks(topo, box, size, data, pos_o, ol)
+
+    def fn(comm, r):
+        out = MPIGridRedistributor(comm, topo, box).redistribute_by_position(
+            data[r], pos[r], overload_lengths=ol)
         torch.cuda.synchronize()
-        assert int(cnt.item()) == k
-        oa, ob = oa.cpu().numpy(), ob.cpu().numpy()
-        np.testing.assert_array_equal(oa[: k * rb1].reshape(k, rb1), a[keep])
-        np.testing.assert_array_equal(ob[: k * rb2].reshape(k, rb2), b[keep])
-        assert (oa[max(k, 1) * rb1:] == 0xAB).all() and (ob[max(k, 1) * rb2:] == 0xCD).all()
-    finally:
-        _lib.tune("pack_compact", 1)
+        return out
+
+    outs = run_ranks(size, fn)
+    for r in range(size):
+        assert G.same_bytes(outs[r], exp[r]), r
+
+
+def test_msel_pack_scattered_destinations():
+    """mgr_msel_pack writes set k to dsts[k] wherever it lies (here in
+    reverse order with gaps) and skips sets whose destination is None."""
+    from mpi_grid_redistribute_amd.halo import DeviceSelect
+    rng = np.random.default_rng(5)
+    n, rb, bits = 70_001, 24, [0, 1, 2, 3]
+    flags = rng.integers(0, 16, n).astype(np.uint16)
+    a = rng.integers(0, 256, (n, rb), dtype=np.uint8)
+    sel = DeviceSelect(torch.device("cuda"))
+    h, cnt = sel.msel(torch.from_numpy(flags.view(np.int16)).cuda(), n, bits, "_s")
+    want = [a[(flags >> b) & 1 == 1] for b in bits]
+    gap = 3
+    sizes = [len(w_) * rb for w_ in want]
+    buf = torch.full((sum(sizes) + gap * rb * 5,), 0x77, dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(a.reshape(-1)).cuda()
+    place, o = {}, gap * rb
+    for k in (3, 2, 0):          # set 1 skipped
+        place[k] = o
+        o += sizes[k] + gap * rb
+    sel.msel_pack(h, src, rb, [buf[place[k]:] if k in place else None for k in range(4)])
+    out = buf.cpu().numpy()
+    for k in (3, 2, 0):
+        np.testing.assert_array_equal(out[place[k]:place[k] + sizes[k]], want[k].reshape(-1))
+    mask = np.ones(len(out), bool)
+    for k in (3, 2, 0):
+        mask[place[k]:place[k] + sizes[k]] = False
+    assert (out[mask] == 0x77).all()

@@ -6,7 +6,7 @@ output bit-exact against the reference's fixtures and the oracle.
   3-5 deployment).
 * With fewer GPUs (the 1-GPU test box): all ranks on GPU 0, each with its own
   NCCL_HOSTID so RCCL connects them with its socket transport -- the same
-  mgr_exchange_counts / mgr_exchange_rows / mgr_sendrecv calls, offsets,
+  mgr_exchange_counts / mgr_exchange_rows / mgr_group_p2p calls, offsets,
   ring order, skewed and empty counts, between distinct ranks.
 Replaces ``comm.alltoall`` (redist.py:199) and the halo's isend/irecv pairs
 (redist.py:289-303).

@@ -6,8 +6,8 @@ from_b) and the periodic=False flag quirk -- through the same
 NumPy stand-in instead of the HIP kernels.  Checked against the reference's
 own outputs (tests/golden/halo_*.npz).
 
-* world_size 2 and 4 with torch.distributed ``gloo`` (TorchDistComm.sendrecv);
-* 6-27 threaded ranks on the mpi4py-style fake comm (MpiHostComm.sendrecv).
+* world_size 2 and 4 with torch.distributed ``gloo`` (TorchDistComm.p2p);
+* 6-27 threaded ranks on the mpi4py-style fake comm (MpiHostComm.p2p).
 """
 import os
 import socket
@@ -43,8 +43,11 @@ class GeoRank:
 
 
 class CpuSelect:
-    """NumPy stand-in for halo.DeviceSelect (mgr_halo_flags / mgr_select_count
-    / mgr_scan / mgr_pack)."""
+    """NumPy stand-in for halo.DeviceSelect (mgr_halo_flags / mgr_msel_count
+    / mgr_scan / mgr_msel_pack)."""
+
+    def _buf(self, name, nbytes):
+        return torch.empty(max(int(nbytes), 1), dtype=torch.uint8)
 
     def flags(self, pos_flat, n, ncols, code, dim, hi, lo):
         dt = np.float32 if code == _lib.MGR_F32 else np.float64
@@ -55,18 +58,25 @@ class CpuSelect:
             f |= (p[:, d] < lo[d]).astype(np.uint16) << (2 * d + 1)
         return torch.from_numpy(f.view(np.int16))
 
-    def select(self, flags, n, mask, max_row_bytes):
-        idx = np.nonzero(flags.numpy().view(np.uint16)[:n] & mask)[0]
-        return (idx,), torch.tensor([len(idx)], dtype=torch.int64)
+    def msel(self, flags, n, bits, tag):
+        fl = flags.numpy().view(np.uint16)[:n]
+        sets = [np.nonzero((fl >> b) & 1)[0] for b in bits]
+        return sets, torch.tensor([len(s) for s in sets], dtype=torch.int64)
 
-    def pack(self, handle, src_flat, row_bytes, dst_flat):
-        idx = handle[0]
-        rows = src_flat.numpy().reshape(-1, row_bytes)[idx].reshape(-1)
-        dst_flat[: rows.size].copy_(torch.from_numpy(rows.copy()))
+    def msel_pack(self, handle, src_flat, row_bytes, dsts):
+        src = src_flat.numpy()
+        rows = src[: (len(src) // row_bytes) * row_bytes].reshape(-1, row_bytes)
+        for idx, d in zip(handle, dsts):
+            if d is not None and len(idx):
+                d[: len(idx) * row_bytes].copy_(torch.from_numpy(rows[idx].reshape(-1).copy()))
 
-    def pack2(self, handle, src1, rb1, dst1, src2, rb2, dst2):
-        self.pack(handle, src1, rb1, dst1)
-        self.pack(handle, src2, rb2, dst2)
+    def msel_pack_fields(self, handle, srcs, row_bytes, dsts):
+        for src, rb, d in zip(srcs, row_bytes, dsts):
+            self.msel_pack(handle, src, rb, [t if t0 is not None else None
+                                             for t, t0 in zip(d, dsts[0])])
+
+    def to_host(self, tensors):
+        return [t.numpy().copy() for t in tensors]
 
 
 def _flat(a):
@@ -89,7 +99,7 @@ def local_inputs(f, case):
     return local, local_pos, True
 
 
-def run_rank(f, case, transport, r, spare=None):
+def run_rank(f, case, transport, r, spare=None, carry_pos=True):
     """``spare``: None = the overload gets a store of its own; else the local
     rows sit at the head of a store with ``spare`` free rows after them (the
     layout redistribute_by_position hands over) and the halo appends there."""
@@ -108,15 +118,25 @@ def run_rank(f, case, transport, r, spare=None):
         st_d[: n * rbd].copy_(d_flat)
         st_p[: n * rbp].copy_(p_flat)
         d_flat, p_flat, arena = st_d[: n * rbd], st_p[: n * rbp], (st_d, st_p, n, spare)
+    flags = None
+    if not carry_pos:   # flags computed up front, positions not carried
+        from mpi_grid_redistribute_amd.halo import thresholds
+        hi, lo = thresholds(R, list(f["overload"]))
+        flags = CpuSelect().flags(p_flat, n, p.shape[1], code, R.dim, hi, lo)
+        p_flat = None
+        if arena is not None:
+            arena = (arena[0], None, n, spare)
     ov_d, ov_p, m, in_arena = exchange_overload(R, transport, d_flat, rbd, p_flat, p.shape[1],
                                                 code, n, list(f["overload"]), periodic=periodic,
-                                                sel=CpuSelect(), arena=arena)
+                                                sel=CpuSelect(), arena=arena, flags=flags)
+    assert (ov_p is None) == (not carry_pos)
     if spare is not None:
         assert in_arena == (m <= spare), (m, spare, in_arena)
         assert torch.equal(st_d[: n * rbd], _flat(d)), "the local rows were overwritten"
         if in_arena and periodic:
             whole = st_d[: (n + m) * rbd].numpy().view(d.dtype).reshape((n + m,) + d.shape[1:])
-            assert np.array_equal(st_p[n * rbp:(n + m) * rbp].numpy(), ov_p.numpy())
+            if carry_pos:
+                assert np.array_equal(st_p[n * rbp:(n + m) * rbp].numpy(), ov_p.numpy())
             return whole
     ov = ov_d.numpy().view(d.dtype).reshape((m,) + d.shape[1:])
     return np.concatenate([d, ov]) if periodic else ov
@@ -153,11 +173,13 @@ def test_gloo_halo(case):
                                   "halo_p27_333_ids.npz", "halo_p6_321_i32.npz",
                                   "halo_p1_self.npz", "halo_direct_p6_321_nonperiodic.npz",
                                   "halo_direct_p8_nonperiodic.npz"])
-def test_threaded_halo(case):
+@pytest.mark.parametrize("carry_pos", [True, False])
+def test_threaded_halo(case, carry_pos):
     f = G.load(case)
     size = int(f["size"])
-    outs = run_ranks(size, lambda comm, r: run_rank(f, case, MpiHostComm(comm), r)
-                     if size > 1 else run_rank(f, case, _SelfT(), r))
+    outs = run_ranks(size, lambda comm, r: run_rank(f, case, MpiHostComm(comm), r,
+                                                    carry_pos=carry_pos)
+                     if size > 1 else run_rank(f, case, _SelfT(), r, carry_pos=carry_pos))
     for r in range(size):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
 
@@ -165,19 +187,19 @@ def test_threaded_halo(case):
 @pytest.mark.parametrize("spare", [0, 3, 40, 10**6])
 @pytest.mark.parametrize("case", ["halo_p8_f64_rec32.npz", "halo_p1_self.npz",
                                   "halo_direct_p8_nonperiodic.npz"])
-def test_threaded_halo_in_place(case, spare):
+@pytest.mark.parametrize("carry_pos", [True, False])
+def test_threaded_halo_in_place(case, spare, carry_pos):
     """The halo rows appended in place after the local rows (the arena that
     redistribute_by_position passes), fitting or outgrowing the spare rows."""
     f = G.load(case)
     size = int(f["size"])
-    outs = run_ranks(size, lambda comm, r: run_rank(f, case, MpiHostComm(comm), r, spare)
-                     if size > 1 else run_rank(f, case, _SelfT(), r, spare))
+    outs = run_ranks(size, lambda comm, r: run_rank(f, case, MpiHostComm(comm), r, spare,
+                                                    carry_pos)
+                     if size > 1 else run_rank(f, case, _SelfT(), r, spare, carry_pos))
     for r in range(size):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r, spare)
 
 
-class _SelfT:
-    rank, size = 0, 1
-
-    def sendrecv(self, send, dest, recv, source):
-        recv.copy_(send)
+def _SelfT():
+    from mpi_grid_redistribute_amd.comm import SelfComm
+    return SelfComm()
