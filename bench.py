@@ -42,12 +42,26 @@ N_CFG2 = 1 << 26                 # config 2: 64M on one GPU
 N_CFG3_PER_GPU = 1_000_000_000 // 8  # config 3: 1B over 8 GPUs
 N_CFG5_PER_GPU = 512_000_000 // 8    # config 5: 512M over 8 GPUs
 
-# Algorithmic bytes per particle, 24-byte f64 positions,
-# 32-byte records, 1-byte destinations.
-BYTES_PER_PARTICLE = {
-    "bin_count": 24 + 24 + 1,    # read pos, write wrapped pos, write dest
-    "pack": 1 + 32 + 32,         # read dest, read record, write record
-}
+# Algorithmic bytes per row of one launch (DESIGN.md §4 Measurement): what
+# the kernel must read and write at least, per row it processes.
+def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512):
+    if cfg == 5:
+        ts = 2.0 * fine_bins / fine_tile_rows        # u16 tile starts per row
+        return {
+            "bin_fine": 36 + 1 + 2,          # read the 36-B record (staged slab), dest, fine id
+            "pack": 1 + 36 + 2 + 36 + 2,     # dest, record + fine id in, record + fine id out
+            "count_ids": 2 + 2 + ts,         # mgr_rank_ids: ids in, ranks + tile starts out
+            "pack_fine": 2 + 2 + ts + 36 + 36,   # mgr_pack_ranked: ids, ranks, starts, record
+        }
+    if halo:
+        return {
+            "bin_count": 24 + 24 + 1 + 2,    # positions in + wrapped out, dest, face flags
+            "pack": 1 + 32 + 2 + 32 + 2,     # dest, record + flags in, record + flags out
+        }
+    return {
+        "bin_count": 24 + 24 + 1,            # read pos, write wrapped pos, write dest
+        "pack": 1 + 32 + 32,                 # read dest, read record, write record
+    }
 
 
 def topology_for(n):
@@ -85,6 +99,22 @@ def cpu_baseline():
                       f"{[round(x, 3) for x in r['seconds']]} s, {el:.1f} s wall"}
 
 
+def cpu_baseline_cfg1():
+    """BASELINE config 1's own shape on the oracle: 8 rank processes x 125k
+    uniform particles (1M total) on a 2x2x2 grid, best of 5 iterations."""
+    from oracle import mp_baseline
+
+    avail = len(os.sched_getaffinity(0))
+    if avail < 8:
+        return None
+    n = 125_000
+    r = mp_baseline.run(size=8, n_per_rank=n, iters=5, topo=(2, 2, 2))
+    return {"value": r["value"], "unit": "particles/s", "cores": r["ranks"], "kind": "port",
+            "sample": f"BASELINE config 1: 8 rank processes x {n} uniform particles (1M), grid "
+                      f"[2, 2, 2], numpy restatement of redist.py:157-199, pickled all-to-all "
+                      f"over pipes, best of 5 {[round(x, 4) for x in r['seconds']]} s"}
+
+
 def cpu_baseline_c():
     """Optimised host comparison point (oracle/, the checker): the threaded C
     restatement of the local stage (wrap + bin + stable partition, exactly the
@@ -92,9 +122,8 @@ def cpu_baseline_c():
     layout, best of 3."""
     from oracle import c_oracle
 
-    avail = len(os.sched_getaffinity(0))
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(avail, omp) if omp > 0 else avail
+    # 8 threads: the same core count as the 8-rank port baselines
+    threads = min(8, len(os.sched_getaffinity(0)))
     n = 1 << 24
     pos, ids = c_oracle.synth_uniform(SEED, 0, n, 3, 1.0)
     rec = np.empty((n, 4), dtype=np.float64)
@@ -154,6 +183,7 @@ def main():
     # CPU baseline first: its rank processes are spawned before this process
     # touches the GPU
     cpu = cpu_baseline() if (world == 1 and not args.no_cpu_baseline) else None
+    cpu_1 = cpu_baseline_cfg1() if (world == 1 and not args.no_cpu_baseline) else None
     cpu_c = cpu_baseline_c() if (world == 1 and not args.no_cpu_baseline) else None
     torch.cuda.set_device(local)
     dist = None
@@ -171,7 +201,6 @@ def main():
         cfg = 3
     topo = topology_for(world) if multi else [2, 2, 2]
     rb, pos_desc = 32, "(N,3) float64, wrapped in place"
-    bytes_pp = dict(BYTES_PER_PARTICLE)
     if not multi:
         n = args.n or N_CFG2
         part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
@@ -256,7 +285,8 @@ def main():
     # exchange inside the timed region: every timed launch adds two event
     # records to the stream (measured ~2-3 us of step time per kernel).  The
     # other kernels are timed in an untimed detail pass after the region.
-    timed = {"report": ["pack", "exchange", "halo"], "all": list(_lib.PROFILE_KERNELS),
+    timed = {"report": ["pack", "exchange", "halo", "halo_pack", "pack_fine"],
+             "all": list(_lib.PROFILE_KERNELS),
              "none": []}[args.prof]
     _lib.profile_select(timed)
     _lib.profile_enable(bool(timed))
@@ -281,7 +311,10 @@ def main():
         ms, cnt = _lib.profile_read(k)
         if cnt:
             kernels[k] = {"avg_ms": ms / cnt, "launches": cnt, "in_timed_region": True}
-    missing = [k for k in ("bin_count", "scan", "pack") if k not in kernels]
+            if _lib.alg_read(k):   # host-counted bytes (the halo's selections)
+                kernels[k]["alg_bytes_per_launch"] = _lib.alg_read(k) / cnt
+    missing = [k for k in list(row_bytes_per_kernel(cfg, bool(args.overload > 0))) + ["scan"]
+               if k not in kernels]
     if missing:
         # detail pass (not timed): the kernels left out of the timed region
         _lib.profile_reset()
@@ -307,22 +340,27 @@ def main():
                 "note": "rank 0: bytes sent + received per grouped ncclSend/ncclRecv over its "
                         "avg duration; peak = 7 links x 153 GB/s (link rate taken as "
                         "bidirectional)"}
+    # per-kernel algorithmic bytes per launch: per-row figure x the rows one
+    # launch processes (n: every launch of these kernels covers this rank's
+    # rows -- received rows at N > 1 are ~n for the uniform inputs), or the
+    # host-counted bytes of the halo's selections
+    fine_tr = int(_lib.load().mgr_tile_rows(36, 512)) if cfg == 5 else 2048
+    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr).items():
+        if k in kernels:
+            kernels[k]["alg_bytes_per_launch"] = b * n
+    for k, e in kernels.items():
+        if "alg_bytes_per_launch" in e:
+            e["alg_GBps"] = e["alg_bytes_per_launch"] / (e["avg_ms"] / 1e3) / 1e9
     roofline = None
-    if args.overload <= 0 and cfg != 5:
-        # one bin and one pack launch per step over all n rows
-        dom = max(("bin_count", "pack"), key=lambda k: kernels.get(k, {"avg_ms": 0})["avg_ms"])
-        assert args.prof == "none" or kernels[dom]["in_timed_region"], \
-            f"dominant kernel {dom} was not timed inside the timed region"
-        alg_bytes = bytes_pp[dom] * n
-        achieved = alg_bytes / (kernels[dom]["avg_ms"] / 1e3) / 1e9
-        for k in ("bin_count", "pack"):
-            if k in kernels:
-                kernels[k]["alg_GBps"] = bytes_pp[k] * n / (kernels[k]["avg_ms"] / 1e3) / 1e9
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                    "traffic": load_traffic(dom, workload), "alg_bytes_per_launch": alg_bytes}
-    # config 5 / halo steps launch the pack several times on different row
-    # counts: per-kernel averages are reported, the roofline is not
+    timed_bytes = {k: e for k, e in kernels.items() if "alg_GBps" in e and e["in_timed_region"]}
+    if timed_bytes:
+        # the dominant kernel: the most device time per step
+        dom = max(timed_bytes, key=lambda k: timed_bytes[k]["avg_ms"] * timed_bytes[k]["launches"])
+        e = kernels[dom]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": e["alg_GBps"],
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": e["alg_GBps"] / HBM_PEAK_GBS,
+                    "traffic": load_traffic(dom, workload),
+                    "alg_bytes_per_launch": e["alg_bytes_per_launch"]}
 
     total = n * world * args.steps
     value = total / elapsed
@@ -346,6 +384,7 @@ def main():
             "kernels": kernels,
             "xgmi": xgmi,
             "cpu_baseline": cpu,
+            "cpu_baseline_cfg1": cpu_1,
             "cpu_baseline_c": cpu_c,
         }
         print(json.dumps(line), flush=True)

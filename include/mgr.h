@@ -331,9 +331,11 @@ int mgr_tune(const char* key, int64_t value);
  * launch's own stream.  mgr_profile_read synchronises those events and
  * returns the accumulated device time (ms) and launch count of the named
  * kernel ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx",
- * "synth", "halo", "bin_fine" (mgr_bin_count_fine), "count_ids", "pack_fine"
- * (the 65..1024-bin sorted-image pack), "pack_narrow" (rows < 4 bytes)) or
- * of the RCCL grouped row exchange ("exchange").                          */
+ * "synth", "halo" (mgr_halo_flags, mgr_msel_count), "bin_fine"
+ * (mgr_bin_count_fine), "count_ids" (mgr_count_ids, mgr_rank_ids),
+ * "pack_fine" (the 65..1024-bin sorted-image and ranked packs),
+ * "pack_narrow" (rows < 4 bytes), "halo_pack" (mgr_msel_pack*)) or of the
+ * RCCL grouped row exchange ("exchange").                                  */
 int mgr_profile_enable(int on);
 int mgr_profile_reset(void);
 int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);

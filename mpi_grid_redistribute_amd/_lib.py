@@ -121,6 +121,10 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        # MGR_TUNE="key=value,..." (A/B measurement of kernel variants)
+        for kv in filter(None, os.environ.get("MGR_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            check(lib.mgr_tune(k.strip().encode(), int(v)), f"MGR_TUNE {kv}")
     return _lib
 
 
@@ -161,11 +165,30 @@ def tune(key, value):
 # --------------------------------------------------------------- profiler
 # Profiler kernel names (mgr_internal.h KernelId).
 PROFILE_KERNELS = ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx", "synth",
-                   "exchange", "halo", "bin_fine", "count_ids", "pack_fine", "pack_narrow")
+                   "exchange", "halo", "bin_fine", "count_ids", "pack_fine", "pack_narrow",
+                   "halo_pack")
+
+
+_prof_on = False
+_alg = {}
 
 
 def profile_enable(on=True):
+    global _prof_on
     call("mgr_profile_enable", int(bool(on)))
+    _prof_on = bool(on)
+
+
+def alg_add(kernel, nbytes):
+    """Algorithmic bytes of a launch whose size only the host code knows
+    (the halo's selections: rows scanned and rows copied), summed per
+    profiler kernel name while profiling is enabled."""
+    if _prof_on:
+        _alg[kernel] = _alg.get(kernel, 0) + int(nbytes)
+
+
+def alg_read(kernel):
+    return _alg.get(kernel, 0)
 
 
 def profile_select(kernels=None):
@@ -185,6 +208,7 @@ def profile_select(kernels=None):
 
 def profile_reset():
     call("mgr_profile_reset")
+    _alg.clear()
 
 
 def profile_read(kernel):

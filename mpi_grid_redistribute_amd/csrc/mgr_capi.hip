@@ -96,7 +96,7 @@ const char* kernel_name(int k) {
     static const char* names[K_NUM_KERNELS] = {"bin_count", "scan", "pack", "cell_ids",
                                                "bin_ids", "cellnum_idx", "synth",
                                                "exchange", "halo", "bin_fine", "count_ids",
-                                               "pack_fine", "pack_narrow"};
+                                               "pack_fine", "pack_narrow", "halo_pack"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 

@@ -85,7 +85,7 @@ int nbits_for(int nbins);
 // Kernel ids for the profiler.
 enum KernelId { K_BIN_COUNT, K_SCAN, K_PACK, K_CELL_IDS, K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH,
                 K_EXCHANGE, K_HALO, K_BIN_FINE, K_COUNT_IDS, K_PACK_FINE, K_PACK_NARROW,
-                K_NUM_KERNELS };
+                K_HALO_PACK, K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);

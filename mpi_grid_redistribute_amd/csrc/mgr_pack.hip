@@ -401,10 +401,10 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
         fs.wlog[f] = (a & 15) == 0 ? 4 : (a & 7) == 0 ? 3 : (a & 3) == 0 ? 2 : (a & 1) == 0 ? 1 : 0;
     }
     const dim3 grid((unsigned)((ws.T + 3) / 4));
-    prof_begin(s, K_PACK);
+    prof_begin(s, K_HALO_PACK);
     hipLaunchKernelGGL(msel_pack_kernel, grid, dim3(256), 0, s, fs, nfields, n, flags, nsets, sb,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, ws.scan_err);
-    prof_end(s, K_PACK);
+    prof_end(s, K_HALO_PACK);
     return hipGetLastError();
 }
 

@@ -136,6 +136,7 @@ class DeviceSelect:
         cb = (ctypes.c_int * k)(*bits)
         s = _lib.stream_handle()
         _lib.call("mgr_msel_count", _lib.ptr(flags), n, k, cb, tile_rows, _lib.ptr(ws), s)
+        _lib.alg_add("halo", 2 * n)                        # the flags, read once
         _lib.call("mgr_scan", n, k, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
         return (n, flags, cb, k, ws, tile_rows), counts
 
@@ -147,10 +148,12 @@ class DeviceSelect:
         _lib.call("mgr_msel_pack", _lib.ptr(src_flat), row_bytes, n, _lib.ptr(flags), k, cb,
                   tile_rows, _lib.ptr(ws), ptrs, _lib.stream_handle())
 
-    def msel_pack_fields(self, handle, srcs, row_bytes, dsts):
+    def msel_pack_fields(self, handle, srcs, row_bytes, dsts, rows_out=0):
         """Several fields of the same rows in one pass: dsts[f][k] as in
-        msel_pack (field 0's None entries decide which sets are written)."""
+        msel_pack (field 0's None entries decide which sets are written).
+        ``rows_out``: the rows the written sets hold (byte accounting)."""
         n, flags, cb, k, ws, tile_rows = handle
+        _lib.alg_add("halo_pack", 2 * n + 2 * rows_out * sum(row_bytes))
         nf = len(srcs)
         sp = (ctypes.c_void_p * nf)(*[_lib.ptr(t) for t in srcs])
         rb = (ctypes.c_int64 * nf)(*row_bytes)
@@ -287,7 +290,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                 for k, t in local_dsts(d, f, *places.get(d, (0, 0))).items():
                     dsts[f][k] = t
         if any(t is not None for t in dsts[0]):
-            sel.msel_pack_fields(lh, srcs, rbs, dsts)
+            sel.msel_pack_fields(lh, srcs, rbs, dsts, sum(sum(local_pieces(d)) for d in dims))
 
     first = [d for d in range(dim) if not selfd[d] or d == 0]
     if selfd[0]:
@@ -338,7 +341,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                 gbuf = [sel._buf(f"halo_ghost{f}", gsz * rbs[f]) for f in range(F)]
                 gd = [[gbuf[f][: nga * rbs[f]] if nga else None,
                        gbuf[f][nga * rbs[f]:gsz * rbs[f]] if ngb else None] for f in range(F)]
-            sel.msel_pack_fields(gh, [store(f, 0, m) for f in range(F)], rbs, gd)
+            sel.msel_pack_fields(gh, [store(f, 0, m) for f in range(F)], rbs, gd, gsz)
         if selfd[d]:
             m = new_m
             continue

@@ -32,6 +32,7 @@ Documented divergences from the reference:
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -85,6 +86,9 @@ def _as_ids(fine_ids, n, dev):
     return t
 
 
+_FINE_RANKED = os.environ.get("MGR_FINE_RANKED", "1") != "0"   # A/B measurement only
+
+
 def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
     """count (mgr_count_ids) -> scan -> stable pack of every field by the
     uint16 ids (the fine cells).  Returns ([sorted flat fields], counts)."""
@@ -95,7 +99,7 @@ def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
     counts = torch.empty(nb, dtype=torch.int64, device=dev)
     # 65..1024 fine cells, 4-byte-multiple rows: ranks computed once, the
     # ranked pack only places rows (mgr_rank_ids + mgr_pack_ranked)
-    ranked = (64 < nb <= 1024 and tile_rows % 256 == 0 and tile_rows <= 4096
+    ranked = (_FINE_RANKED and 64 < nb <= 1024 and tile_rows % 256 == 0 and tile_rows <= 4096
               and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64 for f in fields))
     if ranked:
         T = (n + tile_rows - 1) // tile_rows

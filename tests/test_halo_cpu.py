@@ -70,7 +70,7 @@ class CpuSelect:
             if d is not None and len(idx):
                 d[: len(idx) * row_bytes].copy_(torch.from_numpy(rows[idx].reshape(-1).copy()))
 
-    def msel_pack_fields(self, handle, srcs, row_bytes, dsts):
+    def msel_pack_fields(self, handle, srcs, row_bytes, dsts, rows_out=0):
         for src, rb, d in zip(srcs, row_bytes, dsts):
             self.msel_pack(handle, src, rb, [t if t0 is not None else None
                                              for t, t0 in zip(d, dsts[0])])
