@@ -270,8 +270,12 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     if (hg) h = *hg;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
-    int nwaves = tile_rows / 64;                 // <= bin_waves waves, whole rounds each
-    while (nwaves > g_tune.bin_waves || (tile_rows / 64) % nwaves) --nwaves;
+    // <= bin_waves waves, whole rounds each.  Auto (0): 1 wave for f32
+    // positions (in-box rows wrap to themselves: a read-mostly pass, which
+    // streams best with more rounds per wave), 2 for f64 (the write-back)
+    const int want = g_tune.bin_waves > 0 ? g_tune.bin_waves : (sizeof(PosT) == 4 ? 1 : 2);
+    int nwaves = tile_rows / 64;
+    while (nwaves > want || (tile_rows / 64) % nwaves) --nwaves;
     const int lds = align16(g.nbins * 4) + per_wave * nwaves;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nwaves), (size_t)lds, s, (PosT*)pos, n,

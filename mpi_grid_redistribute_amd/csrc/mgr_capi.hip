@@ -798,7 +798,7 @@ int mgr_tune(const char* key, int64_t value) {
         if (value < -1 || value > (1 << 30)) return fail(MGR_EINVAL, "scan_spins %lld", (long long)value);
         mgr::g_tune.scan_spins = (int)value;
     } else if (!strcmp(key, "bin_waves")) {
-        if (value < 1 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);
+        if (value < 0 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);
         mgr::g_tune.bin_waves = (int)value;
     }
     else if (!strcmp(key, "tile_rounds")) {

@@ -141,7 +141,7 @@ struct Tune {
     int pack_fine = 1;     // sorted-image pack for 65..1024 bins (4-byte-multiple rows)
     int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
     int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
-    int bin_waves = 4;     // waves per bin workgroup (1..16; a tile's rounds split over them)
+    int bin_waves = 0;     // waves per bin workgroup (1..16; a tile's rounds split over them; 0: auto)
     int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
     int pack_compact = 1;  // selections (2 bins, bin 1 dropped): wave-per-tile compaction
     int pack_sel = 1;      // selection packs (2 bins, one dropped) load only kept rows

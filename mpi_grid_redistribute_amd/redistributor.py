@@ -87,6 +87,7 @@ def _as_ids(fine_ids, n, dev):
 
 
 _FINE_RANKED = os.environ.get("MGR_FINE_RANKED", "1") != "0"   # A/B measurement only
+FINE_TILE_ROWS = 2048   # the ranked pack's tile (mgr_pack.hip kFineTR)
 
 
 def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
@@ -99,7 +100,7 @@ def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
     counts = torch.empty(nb, dtype=torch.int64, device=dev)
     # 65..1024 fine cells, 4-byte-multiple rows: ranks computed once, the
     # ranked pack only places rows (mgr_rank_ids + mgr_pack_ranked)
-    ranked = (_FINE_RANKED and 64 < nb <= 1024 and tile_rows % 256 == 0 and tile_rows <= 4096
+    ranked = (_FINE_RANKED and 64 < nb <= 1024 and tile_rows == FINE_TILE_ROWS
               and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64 for f in fields))
     if ranked:
         T = (n + tile_rows - 1) // tile_rows
