@@ -37,6 +37,7 @@ class GeoRank:
         self.grid_topology = g.grid_topology
         self.rank_cell_index = g.rank_cell_index
         self.rank_cell_limits = g.rank_cell_limits
+        self.cell_length = np.asarray(box, dtype=np.float64) / np.asarray(topo)
 
     def get_cell_number_from_indexes_host(self, idx, periodic=True):
         return ro.cell_number_from_indexes(self._g, idx, periodic=periodic)
@@ -203,3 +204,18 @@ def test_threaded_halo_in_place(case, spare, carry_pos):
 def _SelfT():
     from mpi_grid_redistribute_amd.comm import SelfComm
     return SelfComm()
+
+
+def test_halo_capacity_clamped():
+    """halo_capacity caps the overload length at the cell length (the
+    exchange reaches the immediate neighbours only): ol >> cl reserves at
+    most (3^dim - 1) * m * 1.25 + 4096 rows, not a polynomial blow-up."""
+    from mpi_grid_redistribute_amd.halo import halo_capacity
+    R = GeoRank([2, 2, 2], [1.0, 1.0, 1.0], 8, 0)
+    m = 1_000_000
+    big = halo_capacity(R, m, [1.5, 3.0, 10.0])
+    assert big == halo_capacity(R, m, [0.5, 0.5, 0.5])
+    assert big <= int((3 ** 3 - 1) * m * 1.25) + 4096
+    assert halo_capacity(R, m, [0.0, 0.0, 0.0]) == 4096
+    small = halo_capacity(R, m, [0.05, 0.05, 0.05])
+    assert int(m * ((1.2 ** 3) - 1)) < small < big
