@@ -152,6 +152,9 @@ static int fill_box(mgr::Geom& g, int dim, const int64_t* n, const double* box, 
         g.pow2f[d] = Lf > 0.0f && isfinite(Lf) && frexpf(Lf, &e) == 0.5f && isnormal(1.0f / Lf);
         g.invLf[d] = g.pow2f[d] ? 1.0f / Lf : 0.0f;
     }
+    g.fast32 = 1;
+    for (int d = 0; d < dim; ++d)
+        if (n[d] >= ((int64_t)1 << 30)) g.fast32 = 0;
     return MGR_OK;
 }
 
@@ -289,6 +292,7 @@ int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* po
         fg.off[d] = fine_plan->g.off[d];
     }
     fg.nbins = fine_plan->g.nbins;
+    if (!fine_plan->g.fast32) g.fast32 = 0;   // the fine indexes must fit 32 bits too
     const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
     HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
                                  tile_rows, ws, (hipStream_t)stream, &fg, fine_ids));

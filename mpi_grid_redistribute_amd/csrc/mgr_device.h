@@ -203,6 +203,79 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
     return k;
 }
 
+// In-box fast path of bin_row: every coordinate in [0, L_d) with the fast
+// wrap (every in-box particle).  The same values as bin_coord, in 32-bit
+// integer arithmetic: an in-box quotient x/L lies in [0, 1], so trunc(q*n)
+// lies in [0, n] (n < 2^30, Geom::fast32) and the floor-mod reduces to
+// n -> 0; the cell number is below nbins.  NaN fails the range test, so the
+// x86 NaN rules never arise here.  Returns false (nothing written) when a
+// coordinate is outside; bin_row then takes the general path.
+template <typename PosT, bool kPeriodic, int DIM, int SIDE>
+__device__ __forceinline__ bool bin_row_fast(PosT* row, const Geom& g, bool* dirty,
+                                             const FineGeom* fg, const HaloGeom* hg,
+                                             long long* cell_out, long long* side) {
+    const bool f32c = sizeof(PosT) == 4 && g.compute_f32;
+    PosT in[DIM];
+    bool inb = true;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+        in[d] = row[d];
+        if (f32c) inb = inb && g.fastf[d] && (float)in[d] >= 0.0f && (float)in[d] < g.Lf[d];
+        else inb = inb && g.fast[d] && (double)in[d] >= 0.0 && (double)in[d] < g.L[d];
+    }
+    if (!inb) return false;
+    int cell = 0, sc = 0;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) {
+        int k, kf = 0;
+        double xs = 0.0;
+        if (f32c) {
+            float x = (float)in[d];
+            if (kPeriodic) {
+                const float y = x + g.Lf[d];
+                x = (y == g.twoLf[d]) ? 0.0f : y - g.Lf[d];
+                if (!same_bits((PosT)x, in[d])) { row[d] = (PosT)x; *dirty = true; }
+            }
+            const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];
+            k = (int)((double)q * g.nd[d]);
+            if (SIDE == kSideFine) kf = (int)((double)q * fg->nd[d]);
+            if (SIDE == kSideHalo) xs = (double)x;
+        } else {
+            double x = (double)in[d];
+            if (kPeriodic) {
+                const double y = x + g.L[d];
+                const double t = (y == g.twoL[d]) ? 0.0 : y - g.L[d];
+                const PosT w = sizeof(PosT) == 4 ? (PosT)(float)t : (PosT)t;
+                if (!same_bits(w, in[d])) { row[d] = w; *dirty = true; }
+                x = (double)w;
+            }
+            const double q = g.pow2[d] ? x * g.invL[d] : x / g.L[d];
+            k = (int)(q * g.nd[d]);
+            if (SIDE == kSideFine) kf = (int)(q * fg->nd[d]);
+            if (SIDE == kSideHalo) xs = x;
+        }
+        const int n = (int)g.n[d];
+        if (k >= n) k -= n;
+        if (g.fine) k %= (int)g.fmod[d];
+        if (SIDE == kSideFine) {
+            const int nf = (int)fg->n[d], f = (int)fg->fmod[d];
+            if (kf >= nf) kf -= nf;
+            int m = kf - f * k;
+            if (!(m >= 0 && m < f)) m = kf % f;
+            sc += (int)fg->off[d] * m;
+        }
+        if (SIDE == kSideHalo) {
+            const double hi = (double)(k + 1) * hg->cl[d] - hg->ol[d];
+            const double lo = (double)k * hg->cl[d] + hg->ol[d];
+            sc |= ((xs > hi ? 1 : 0) | (xs < lo ? 2 : 0)) << (2 * d);
+        }
+        cell += (int)g.off[d] * k;
+    }
+    *cell_out = cell;
+    if (SIDE != kSideNone) *side = sc;
+    return true;
+}
+
 // DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
 // SIDE: *side gets the row's fine cell (row-major over fg->fmod) or its face
 // flags (bit 2d: right face of dimension d, bit 2d+1: left face).
@@ -211,6 +284,11 @@ __device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long
                                              bool* dirty, const FineGeom* fg = nullptr,
                                              const HaloGeom* hg = nullptr,
                                              long long* side = nullptr) {
+    if constexpr (DIM > 0) {
+        long long c;
+        if (!idx && g.fast32 && bin_row_fast<PosT, kPeriodic, DIM, SIDE>(row, g, dirty, fg, hg, &c, side))
+            return c;
+    }
     long long cell = 0, sc = 0;
     const int nd = DIM > 0 ? DIM : g.dim;
 #pragma unroll

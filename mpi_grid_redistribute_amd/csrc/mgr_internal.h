@@ -45,6 +45,7 @@ struct Geom {
     int64_t off[MGR_MAX_DIM];            // row-major offsets, last axis fastest (S4)
     int fine;                            // fine-cell plan (mgr_plan_create_fine)
     int64_t fmod[MGR_MAX_DIM];           // fine cells per rank cell and dimension
+    int fast32;                          // every n[d] < 2^30: in-box rows bin in 32-bit ints
 };
 
 // The fine cells a row falls in, inside its destination's cell (SURVEY f4,
