@@ -134,6 +134,51 @@ def case_random(mgr, comm, sizes, seed, as_torch, hot=None, return_positions=Fal
     return len(exp)
 
 
+def case_fine_fused(mgr, comm, fine, seed):
+    """redistribute_by_position(fine_cells=...) over RCCL: the source's fine
+    ids travel as a side field, the destination sorts by them -- against the
+    oracle's redistribution + fine_cell_ids + stable sort."""
+    topo = TOPO[WORLD]
+    sizes = [int(np.random.default_rng(seed + r).integers(5_000, 40_000)) for r in range(WORLD)]
+    pos, data = rank_inputs(seed, sizes)
+    pos_o = [p.copy() for p in pos]
+    loc = ro.redistribute_by_position_all_ranks(topo, BOX, WORLD, data, pos_o)[RANK]
+    geos = [ro.Geometry(topo, BOX, WORLD, r) for r in range(WORLD)]
+    lpos = ro.redistribute_by_cell_number_all_ranks(
+        WORLD, pos_o, [ro.cell_number_from_position(g, p.copy()) for g, p in zip(geos, pos_o)])[RANK]
+    fid = ro.fine_cell_ids(topo, fine, BOX, lpos)
+    exp, exp_off = ro.fine_cell_sort(loc, fid, int(np.prod(fine)))
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    got, gpos, off = R.redistribute_by_position(data[RANK], pos[RANK], fine_cells=fine,
+                                                return_positions=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(as_bytes(got), as_bytes(exp)), "fine-sorted output"
+    assert np.array_equal(np.asarray(off), exp_off), "fine offsets"
+    assert np.array_equal(as_bytes(gpos), as_bytes(lpos[np.argsort(fid, kind="stable")])), \
+        "fine-sorted positions"
+
+
+def case_halo_random(mgr, comm, ol, return_positions, seed):
+    """The halo over RCCL at larger sizes (flags from the bin kernel, the
+    multi-selection packs, grouped p2p): against the oracle; with
+    return_positions the positions travel as a third field."""
+    topo = TOPO[WORLD]
+    sizes = [int(np.random.default_rng(seed + r).integers(10_000, 40_000)) for r in range(WORLD)]
+    pos, data = rank_inputs(seed, sizes)
+    pos_o = [p.copy() for p in pos]
+    exp = ro.redistribute_by_position_overload_all_ranks(topo, BOX, WORLD, data, pos_o, ol)[RANK]
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    out = R.redistribute_by_position(data[RANK], pos[RANK], overload_lengths=ol,
+                                     return_positions=return_positions)
+    torch.cuda.synchronize()
+    if return_positions:
+        out, opos = out
+        ids = as_bytes(out).view(exp.dtype)["id"]
+        want = np.stack([pos_o[s][i] for s, i in zip(ids // 1_000_000, ids % 1_000_000)])
+        assert np.array_equal(as_bytes(opos), as_bytes(want)), "halo positions"
+    assert np.array_equal(as_bytes(out), as_bytes(exp)), "halo output"
+
+
 def case_cell_number(mgr, comm):
     rng = np.random.default_rng(99)
     data = [rng.integers(0, 255, (int(rng.integers(0, 5000)), 7)).astype(np.uint8)
@@ -204,6 +249,11 @@ def main():
                                                      return_positions=True)),
             ("large_300k", lambda: case_random(mgr, comm, [300_000] * WORLD, 15, True)),
             ("scan_failure", lambda: case_scan_failure(mgr, comm)),
+            ("fine_fused_888", lambda: case_fine_fused(mgr, comm, [8, 8, 8], 21)),
+            ("fine_fused_234", lambda: case_fine_fused(mgr, comm, [2, 3, 4], 22)),
+            ("halo_random", lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], False, 23)),
+            ("halo_random_positions",
+             lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], True, 24)),
         ]
     cases.append(("cell_number_dropped_ids", lambda: case_cell_number(mgr, comm)))
     for name, fn in cases:
