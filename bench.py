@@ -64,6 +64,11 @@ def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512):
     }
 
 
+def _m(n):
+    """Workload size label: 2^26 -> 64M, 125_000_000 -> 125M."""
+    return f"{n >> 20}M" if n % (1 << 20) == 0 else f"{n / 1e6:g}M"
+
+
 def topology_for(n):
     dims = [1, 1, 1]
     k = 0
@@ -158,7 +163,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=0, help="particles per GPU (default: config size)")
+    ap.add_argument("--particles", "--n", dest="n", type=int, default=0,
+                    help="particles per GPU (default: config size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prof", choices=("report", "all", "none"), default="report",
                     help="kernels timed with HIP events inside the timed region: report = "
@@ -185,6 +191,12 @@ def main():
     cpu = cpu_baseline() if (world == 1 and not args.no_cpu_baseline) else None
     cpu_1 = cpu_baseline_cfg1() if (world == 1 and not args.no_cpu_baseline) else None
     cpu_c = cpu_baseline_c() if (world == 1 and not args.no_cpu_baseline) else None
+    if os.environ.get("MGR_BENCH_SHARED_GPU") == "1":
+        # rehearsal of the N>1 path on a 1-GPU box: every rank on GPU 0, each
+        # its own RCCL "host" (socket transport) -- numbers are not xGMI ones
+        os.environ["NCCL_HOSTID"] = f"mgr-bench-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     multi = world > 1 or args.exchange
@@ -208,7 +220,7 @@ def main():
             # one GPU's share of config 5: 64M 36-byte records; the local stage
             # (bin + scan + pack into 8 destinations) and the destination-side
             # fine-cell sort (8x8x8) of 64M rows inside one cell
-            workload = "cfg5_64M_rec36_2x2x2_local_partition_plus_fine_sort_888"
+            workload = f"cfg5_{_m(n)}_rec36_2x2x2_local_partition_plus_fine_sort_888"
             rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
             rec, pos = mgr.synth_wide(n, seed=SEED, gid0=0)
             recv, rpos = mgr.synth_wide(n, seed=SEED + 1, gid0=0, hi=0.5)
@@ -227,10 +239,10 @@ def main():
                 R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=recv_fids)
         else:
             if cfg == 4:
-                workload = "cfg4_64M_clustered_2x2x2_local_partition"
+                workload = f"cfg4_{_m(n)}_clustered_2x2x2_local_partition"
                 pos, rec = mgr.synth_clustered(n, seed=SEED, gid0=0)
             else:
-                workload = "cfg2_64M_uniform_2x2x2_local_partition"
+                workload = f"cfg2_{_m(n)}_uniform_2x2x2_local_partition"
                 pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=0)
             flat = rec.reshape(-1)
 
@@ -241,17 +253,17 @@ def main():
         comm = mgr.RcclComm.from_torch_distributed()
         R = mgr.MPIGridRedistributor(comm, topo, [1.0, 1.0, 1.0])
         if cfg == 5:
-            workload = "cfg5_rec36_per_gpu_64M_full_exchange_plus_fine_sort_888"
+            workload = f"cfg5_rec36_per_gpu_{_m(n)}_full_exchange_plus_fine_sort_888"
             rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
             rec, pos = mgr.synth_wide(n, seed=SEED, gid0=rank * n)
             def step():
                 R.redistribute_by_position(rec, pos, fine_cells=[8, 8, 8])
         else:
             if cfg == 4:
-                workload = "cfg4_clustered_per_gpu_125M_full_exchange"
+                workload = f"cfg4_clustered_per_gpu_{_m(n)}_full_exchange"
                 pos, rec = mgr.synth_clustered(n, seed=SEED, gid0=rank * n)
             else:
-                workload = "cfg3_uniform_per_gpu_125M_full_exchange"
+                workload = f"cfg3_uniform_per_gpu_{_m(n)}_full_exchange"
                 pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=rank * n)
 
             ol = [args.overload] * 3 if args.overload > 0 else None
