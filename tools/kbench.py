@@ -52,17 +52,16 @@ def run(variant):
     b.record()
     torch.cuda.synchronize()
     out = {"step": round(a.elapsed_time(b) / ITERS, 4)}
-    for k in ("bin_count", "scan", "scan_reduce", "scan_apply", "pack"):
+    for k in ("bin_count", "scan", "pack"):
         ms, cnt = _lib.profile_read(k)
         out[k] = round(ms / max(cnt, 1), 4)
     out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
     out["pack_GBps"] = round((2 * rb + 1) * N / (out["pack"] / 1e3) / 1e9, 1)
-    for k, v in {"bin_staged": 1, "pack_small": 1, "tile_rounds": 0,
-                 "pack_nt": 0, "pack_coop": 1, "pack_sorted": 0, "xcd_pack": 1, "xcd_bin": 0,
-                 "bin_skip_clean": 1, "bin_waves": 4, "bin_depth": 1, "pack_rpw": 1, "pack_many": 1,
-                 "scan_onepass": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
-                 "scan_max_chunks": 1024, "pack_sel": 1,
-                 "pack_compact": 1, "many_rows": 0}.items():
+    for k, v in {"bin_staged": 1, "tile_rounds": 0, "pack_nt": 0, "pack_coop": 1,
+                 "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1,
+                 "bin_waves": 0, "pack_rpw": 1, "pack_many": 1, "scan_chunk": 2048,
+                 "pack_img": 1, "many_super": 1, "scan_max_chunks": 1024, "pack_sel": 1,
+                 "pack_compact": 1, "many_rows": 0, "pack_fine": 1}.items():
         _lib.tune(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
