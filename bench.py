@@ -356,7 +356,7 @@ def main():
     # launch processes (n: every launch of these kernels covers this rank's
     # rows -- received rows at N > 1 are ~n for the uniform inputs), or the
     # host-counted bytes of the halo's selections
-    fine_tr = int(_lib.load().mgr_tile_rows(36, 512)) if cfg == 5 else 2048
+    fine_tr = int(_lib.load().mgr_ranked_tile_rows(36, 512)) if cfg == 5 else 2048
     for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr).items():
         if k in kernels:
             kernels[k]["alg_bytes_per_launch"] = b * n

@@ -183,8 +183,13 @@ int mgr_pack_ids(const void* src, int64_t row_bytes, int64_t n, const void* dest
  * mgr_pack_ranked: the stable partition of n rows of row_bytes by those ids
  *                (after mgr_scan), each row placed at tile_start + rank --
  *                no ranking in the pack.  Rows of 4-byte multiples <= 64 B,
- *                tile_rows = mgr_tile_rows(row_bytes, nbins) for 65..1024
- *                ids; MGR_EUNSUPPORTED otherwise (use mgr_pack).            */
+ *                tile_rows = mgr_ranked_tile_rows(row_bytes, nbins) (the
+ *                same value for the rank, the scan, the workspace and every
+ *                field's pack); MGR_EUNSUPPORTED otherwise (use mgr_pack).   */
+/* Tile rows of the ranked fine sort for rows of row_bytes (the widest field
+ * packed) and nbins ids: 4096 when the tile's LDS image fits, else 2048; 0
+ * when the ranked path does not take these rows.                          */
+int mgr_ranked_tile_rows(int64_t row_bytes, int nbins);
 int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint16_t* ranks,
                  uint16_t* tile_starts, void* workspace, void* stream);
 int mgr_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,

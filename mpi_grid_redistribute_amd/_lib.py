@@ -33,6 +33,7 @@ SIGNATURES = {
     "mgr_plan_create_fine": (_I, [_I, _P, _P, _P, _I, ctypes.POINTER(_P)]),
     "mgr_plan_destroy": (_I, [_P]),
     "mgr_tile_rows": (_I, [_I64, _I]),
+    "mgr_ranked_tile_rows": (_I, [_I64, _I]),
     "mgr_workspace_bytes": (_I64, [_I64, _I, _I]),
     "mgr_dest_bytes": (_I, [_I]),
     "mgr_bin_count": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P]),

@@ -229,6 +229,10 @@ int mgr_tile_rows(int64_t max_row_bytes, int nbins) {
     return mgr::pack_tile_rows(max_row_bytes, nbins);
 }
 
+int mgr_ranked_tile_rows(int64_t row_bytes, int nbins) {
+    return mgr::ranked_tile_rows(row_bytes, nbins);
+}
+
 int64_t mgr_workspace_bytes(int64_t n, int nbins, int tile_rows) {
     if (n < 0 || nbins < 1 || tile_rows < 64) return -1;
     return mgr::workspace_bytes(n, nbins, tile_rows);
@@ -769,6 +773,11 @@ int mgr_tune(const char* key, int64_t value) {
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
+    else if (!strcmp(key, "rank_rows")) {
+        if (value != 0 && value != 2048 && value != 4096)
+            return fail(MGR_EINVAL, "rank_rows %lld (0, 2048 or 4096)", (long long)value);
+        mgr::g_tune.rank_rows = (int)value;
+    }
     else if (!strcmp(key, "many_rows")) {
         if (value != 0 && value != 1024 && value != 2048 && value != 4096)
             return fail(MGR_EINVAL, "many_rows %lld (0, 1024, 2048 or 4096)", (long long)value);

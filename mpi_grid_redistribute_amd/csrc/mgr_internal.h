@@ -125,6 +125,7 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
+int ranked_tile_rows(int64_t row_bytes, int nbins);
 hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
 hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,
@@ -151,6 +152,7 @@ struct Tune {
     int scan_max_chunks = 1024;  // one-pass scan: at most this many chunks (look-back depth)
     int scan_spins = 1 << 24;    // one-pass scan: polls per look-back word before giving up
                                  // (-1: give up at once -- tests of the error path)
+    int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096
     int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)
     int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)
 };

@@ -1140,14 +1140,14 @@ static hipError_t pack_fine_t(const void* src, int64_t n, const void* dest, int 
 // come from mgr_rank_ids -- so a tile is: load (a tile ahead), rows into the
 // LDS image at tile_start[bin] + rank, stream the image out.  No ballots, no
 // per-tile count table, three barriers per tile.
-template <int RB>
+template <int RB, int TR>
 __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
     const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
     const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
     const uint32_t* __restrict__ scan_err) {
     static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
-    constexpr int TR = kFineTR, NW = kFineWaves, RPW = TR / 64 / NW;
+    constexpr int NW = kFineWaves, RPW = TR / 64 / NW;
     constexpr int NDW = RB / 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* img = (uint32_t*)smem;
@@ -1229,36 +1229,64 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
+// LDS of the ranked pack: the tile image, its row bins, per-bin output
+// addresses and tile starts.
+static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
+    return align16(tile_rows * (int)row_bytes) + align16(tile_rows * 2) + nbins * 8 + nbins * 2;
+}
+
+// Ranked tiles: 4096 rows when their image fits the LDS (36-byte rows: 157 KiB),
+// else 2048.  Longer tiles halve the [bins][tiles] histogram the scan walks and
+// the per-tile fixed work (A/B: profiles/round2/ab_notes.md).
+int ranked_tile_rows(int64_t row_bytes, int nbins) {
+    if (row_bytes < 1 || row_bytes % 4 || row_bytes > 64 || nbins < 1 || nbins > 1024) return 0;
+    if (g_tune.rank_rows == 0 && ranked_lds_bytes(4096, row_bytes, nbins) <= 160 * 1024) return 4096;
+    if (g_tune.rank_rows == 4096 && ranked_lds_bytes(4096, row_bytes, nbins) <= 160 * 1024) return 4096;
+    return ranked_lds_bytes(kFineTR, row_bytes, nbins) <= 160 * 1024 ? kFineTR : 0;
+}
+
 hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
                               const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
                               int tile_rows, const Workspace& ws, void* dst, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    if (tile_rows != kFineTR || row_bytes % 4 || row_bytes > 64 || ((uintptr_t)src & 3) ||
-        ((uintptr_t)dst & 3))
+    if ((tile_rows != kFineTR && tile_rows != 4096) || row_bytes % 4 || row_bytes > 64 ||
+        ((uintptr_t)src & 3) || ((uintptr_t)dst & 3))
         return hipErrorNotSupported;
-    const int lds = align16(kFineTR * (int)row_bytes) + align16(kFineTR * 2) + nbins * 8 + nbins * 2;
+    const int lds = ranked_lds_bytes(tile_rows, row_bytes, nbins);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
-#define MGR_PR(RB_)                                                                           \
-    case RB_: {                                                                               \
-        auto k = pack_ranked_kernel<RB_>;                                                     \
+#define MGR_PRT(RB_, TR_)                                                                     \
+    {                                                                                         \
+        auto k = pack_ranked_kernel<RB_, TR_>;                                                \
         ensure_lds(k, lds);                                                                   \
         hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,               \
                            (const uint8_t*)src, n, ids, ranks, tile_starts, nbins, ws.offsets, \
                            ws.T, (uint8_t*)dst, ws.scan_err);                                  \
         e = hipGetLastError();                                                                \
-        break;                                                                                \
     }
+#define MGR_PR(RB_)                                                                           \
+    case RB_:                                                                                 \
+        if (tile_rows == 4096) MGR_PRT(RB_, 4096) else MGR_PRT(RB_, kFineTR)                  \
+        break;
     switch ((int)row_bytes) {
         MGR_PR(4) MGR_PR(8) MGR_PR(12) MGR_PR(16) MGR_PR(20) MGR_PR(24) MGR_PR(28) MGR_PR(32)
-        MGR_PR(36) MGR_PR(40) MGR_PR(44) MGR_PR(48) MGR_PR(52) MGR_PR(56) MGR_PR(60) MGR_PR(64)
+        MGR_PR(36)
         default: break;
     }
+    if (e == hipErrorNotSupported && tile_rows == kFineTR) {
+        switch ((int)row_bytes) {
 #undef MGR_PR
+#define MGR_PR(RB_) case RB_: MGR_PRT(RB_, kFineTR) break;
+            MGR_PR(40) MGR_PR(44) MGR_PR(48) MGR_PR(52) MGR_PR(56) MGR_PR(60) MGR_PR(64)
+            default: break;
+        }
+    }
+#undef MGR_PR
+#undef MGR_PRT
     prof_end(s, K_PACK_FINE);
     return e;
 }

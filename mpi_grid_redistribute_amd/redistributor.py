@@ -87,7 +87,6 @@ def _as_ids(fine_ids, n, dev):
 
 
 _FINE_RANKED = os.environ.get("MGR_FINE_RANKED", "1") != "0"   # A/B measurement only
-FINE_TILE_ROWS = 2048   # the ranked pack's tile (mgr_pack.hip kFineTR)
 
 
 def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
@@ -95,13 +94,16 @@ def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
     uint16 ids (the fine cells).  Returns ([sorted flat fields], counts)."""
     hint = max([f.row_bytes for f in fields] + [1])
     small = _lib.load().mgr_dest_bytes(int(nb)) == 1   # <= 256 bins: 1-byte dest array
-    tile_rows, ws, d8 = _scratch(n, nb, hint, dev, scratch, dest=small, tag="_fine")
     s = _lib.stream_handle()
     counts = torch.empty(nb, dtype=torch.int64, device=dev)
     # 65..1024 fine cells, 4-byte-multiple rows: ranks computed once, the
-    # ranked pack only places rows (mgr_rank_ids + mgr_pack_ranked)
-    ranked = (_FINE_RANKED and 64 < nb <= 1024 and tile_rows == FINE_TILE_ROWS
+    # ranked pack only places rows (mgr_rank_ids + mgr_pack_ranked), on its
+    # own tiles (mgr_ranked_tile_rows)
+    rtr = int(_lib.load().mgr_ranked_tile_rows(int(hint), int(nb)))
+    ranked = (_FINE_RANKED and 64 < nb <= 1024 and rtr > 0
               and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64 for f in fields))
+    tile_rows, ws, d8 = _scratch(n, nb, hint, dev, scratch, dest=small and not ranked,
+                                 tag="_fine", tile_rows=rtr if ranked else None)
     if ranked:
         T = (n + tile_rows - 1) // tile_rows
         get = scratch.get if scratch is not None else (
@@ -211,10 +213,12 @@ class Scratch:
         self.bufs.clear()
 
 
-def _scratch(n, nbins, max_row_bytes, dev, cache=None, dest=True, tag=""):
+def _scratch(n, nbins, max_row_bytes, dev, cache=None, dest=True, tag="", tile_rows=None):
     """(tile_rows, workspace, dest) for n rows and nbins bins; from ``cache``
-    (a Scratch, buffers named with ``tag``) when given, else fresh."""
-    tile_rows = _lib.load().mgr_tile_rows(int(max_row_bytes), int(nbins))
+    (a Scratch, buffers named with ``tag``) when given, else fresh.
+    ``tile_rows``: a kernel family's own tiles (default mgr_tile_rows)."""
+    if tile_rows is None:
+        tile_rows = _lib.load().mgr_tile_rows(int(max_row_bytes), int(nbins))
     wsb = _lib.load().mgr_workspace_bytes(int(n), int(nbins), int(tile_rows))
     if wsb < 0:
         raise _lib.MgrError("mgr_workspace_bytes: bad arguments")

@@ -14,7 +14,7 @@ from tests.fake_mpi import run_ranks
 pytestmark = pytest.mark.gpu
 
 mgr = pytest.importorskip("mpi_grid_redistribute_amd")
-from mpi_grid_redistribute_amd import MPIGridRedistributor  # noqa: E402
+from mpi_grid_redistribute_amd import MPIGridRedistributor, _lib  # noqa: E402
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -178,3 +178,28 @@ def test_partition_fine_ids_then_sort():
                                        fine_ids=fids[starts[cell]: starts[cell + 1]])
         b, ob = R[cell].fine_cell_sort(seg, seg.view(torch.float32)[:, :3], [8, 8, 8])
         assert torch.equal(a, b) and torch.equal(oa, ob)
+
+
+@pytest.mark.parametrize("rank_rows", [0, 2048, 4096])
+@pytest.mark.parametrize("row_bytes", [4, 12, 36, 40, 64])
+def test_ranked_sort_tile_sizes(rank_rows, row_bytes):
+    """mgr_rank_ids + mgr_pack_ranked on both tile sizes (4096 where the LDS
+    image fits, 2048 otherwise and on request), a ragged last tile, a hot
+    cell and empty cells: the stable sort of the rows by their ids."""
+    rng = np.random.default_rng(row_bytes * 13 + rank_rows)
+    n = 300_001 + row_bytes
+    ids = rng.integers(0, 512, n).astype(np.uint16)
+    ids[rng.random(n) < 0.3] = 77            # a hot cell
+    ids[(ids >= 400) & (ids < 420)] = 5      # empty cells
+    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
+    exp = data[np.argsort(ids, kind="stable")]
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    pos = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+    _lib.tune("rank_rows", rank_rows)
+    try:
+        got, off = R.fine_cell_sort(torch.from_numpy(data).cuda(), pos, [8, 8, 8],
+                                    fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
+    finally:
+        _lib.tune("rank_rows", 0)
+    assert np.array_equal(got.cpu().numpy(), exp)
+    assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
