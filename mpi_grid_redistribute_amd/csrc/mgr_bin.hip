@@ -25,7 +25,7 @@ constexpr int kStageMaxRowBytes = 64;
 // binning pass) or its halo face flags (kSideHalo, HaloGeom: the overload
 // exchange then needs no flag pass over the received positions).
 template <typename PosT, bool kPeriodic, typename DestT, int NU, int DIM, bool NT, int DEPTH,
-          int SIDE>
+          int SIDE, int GEO = kGeoAny>
 __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos, int64_t n,
                                                            int64_t stride, Geom g,
                                                            DestT* __restrict__ dest,
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             bool dirty = false;
             long long sc = 0;
             if (valid)
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM, SIDE>((PosT*)(stage + lane * rb), g,
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM, SIDE, GEO>((PosT*)(stage + lane * rb), g,
                                                                   nullptr, &dirty, &fg, &hg, &sc);
             side_store((unsigned)sc, valid, r0);
             // write the slab back only if a row of it changed (skip_clean)
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(1024) void bin_count_kernel(PosT* __restrict__ pos,
             bool dirty = false;
             long long sc = 0;
             if (valid)
-                b = (unsigned)bin_row<PosT, kPeriodic, DIM, SIDE>(pos + (row0 + r0 + lane) * stride,
+                b = (unsigned)bin_row<PosT, kPeriodic, DIM, SIDE, GEO>(pos + (row0 + r0 + lane) * stride,
                                                                   g, nullptr, &dirty, &fg, &hg, &sc);
             side_store((unsigned)sc, valid, r0);
             account(b, valid, r0);
@@ -254,6 +254,20 @@ __global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t*
 }
 
 // ============================================================ launchers
+// The plan's geometry class for the bin kernel (bin_row_fast's GEO): every
+// dimension with the fast wrap and a power-of-two box length, 32-bit index
+// math, not a fine plan -- then kGeoF32 / kGeoF64 by the quotient's type
+// (f32 positions with an f32 box compute in f32, everything else in f64).
+static int geo_kind(const Geom& g, bool pos_f32) {
+    if (g.dim != 3 || g.fine || !g.fast32) return kGeoAny;
+    const bool f32c = pos_f32 && g.compute_f32;
+    for (int d = 0; d < 3; ++d) {
+        if (f32c && !(g.fastf[d] && g.pow2f[d])) return kGeoAny;
+        if (!f32c && !(g.fast[d] && g.pow2[d])) return kGeoAny;
+    }
+    return f32c ? kGeoF32 : kGeoF64;
+}
+
 template <typename PosT, bool kP, typename DestT, int NU, int DIM>
 static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t stride, void* dest,
                               int tile_rows, const Workspace& ws, hipStream_t s,
@@ -261,9 +275,22 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     // nontemporal slab loads/stores always (every A/B favoured them); one
     // slab in flight per wave (two measured slower with the write-back,
     // DESIGN.md §3.3)
+    // the in-box fast path with the geometry at compile time when it is
+    // simple (geo_kind): staged 3-D periodic slabs, the hot configurations
     auto k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideFine>
                 : hg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideHalo>
                      : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideNone>;
+    if constexpr (DIM == 3 && kP && NU > 0) {
+        const int geo = g_tune.bin_geo ? geo_kind(g, sizeof(PosT) == 4) : kGeoAny;
+        if (geo == kGeoF32)
+            k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideFine, kGeoF32>
+                   : hg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideHalo, kGeoF32>
+                        : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideNone, kGeoF32>;
+        else if (geo == kGeoF64)
+            k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideFine, kGeoF64>
+                   : hg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideHalo, kGeoF64>
+                        : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideNone, kGeoF64>;
+    }
     FineGeom f{};
     if (fg) f = *fg;
     HaloGeom h{};

@@ -210,18 +210,27 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
 // n -> 0; the cell number is below nbins.  NaN fails the range test, so the
 // x86 NaN rules never arise here.  Returns false (nothing written) when a
 // coordinate is outside; bin_row then takes the general path.
-template <typename PosT, bool kPeriodic, int DIM, int SIDE>
+// GEO: the plan's geometry at compile time where it is simple (geo_kind):
+// kGeoAny -- read every flag from g; kGeoF32 / kGeoF64 -- every dimension
+// has the fast wrap and a power-of-two box length (x / L == x * (1/L)), the
+// quotient is computed in f32 / f64, and the plan is not a fine plan.  The
+// values are the same; only the per-row flag tests and branches go away.
+constexpr int kGeoAny = 0, kGeoF32 = 1, kGeoF64 = 2;
+
+template <typename PosT, bool kPeriodic, int DIM, int SIDE, int GEO = kGeoAny>
 __device__ __forceinline__ bool bin_row_fast(PosT* row, const Geom& g, bool* dirty,
                                              const FineGeom* fg, const HaloGeom* hg,
                                              long long* cell_out, long long* side) {
-    const bool f32c = sizeof(PosT) == 4 && g.compute_f32;
+    const bool f32c = GEO == kGeoF32 ? true
+                    : GEO == kGeoF64 ? false
+                                     : (sizeof(PosT) == 4 && g.compute_f32);
     PosT in[DIM];
     bool inb = true;
 #pragma unroll
     for (int d = 0; d < DIM; ++d) {
         in[d] = row[d];
-        if (f32c) inb = inb && g.fastf[d] && (float)in[d] >= 0.0f && (float)in[d] < g.Lf[d];
-        else inb = inb && g.fast[d] && (double)in[d] >= 0.0 && (double)in[d] < g.L[d];
+        if (f32c) inb = inb && (GEO != kGeoAny || g.fastf[d]) && (float)in[d] >= 0.0f && (float)in[d] < g.Lf[d];
+        else inb = inb && (GEO != kGeoAny || g.fast[d]) && (double)in[d] >= 0.0 && (double)in[d] < g.L[d];
     }
     if (!inb) return false;
     int cell = 0, sc = 0;
@@ -236,7 +245,7 @@ __device__ __forceinline__ bool bin_row_fast(PosT* row, const Geom& g, bool* dir
                 x = (y == g.twoLf[d]) ? 0.0f : y - g.Lf[d];
                 if (!same_bits((PosT)x, in[d])) { row[d] = (PosT)x; *dirty = true; }
             }
-            const float q = g.pow2f[d] ? x * g.invLf[d] : x / g.Lf[d];
+            const float q = (GEO != kGeoAny || g.pow2f[d]) ? x * g.invLf[d] : x / g.Lf[d];
             k = (int)((double)q * g.nd[d]);
             if (SIDE == kSideFine) kf = (int)((double)q * fg->nd[d]);
             if (SIDE == kSideHalo) xs = (double)x;
@@ -249,14 +258,14 @@ __device__ __forceinline__ bool bin_row_fast(PosT* row, const Geom& g, bool* dir
                 if (!same_bits(w, in[d])) { row[d] = w; *dirty = true; }
                 x = (double)w;
             }
-            const double q = g.pow2[d] ? x * g.invL[d] : x / g.L[d];
+            const double q = (GEO != kGeoAny || g.pow2[d]) ? x * g.invL[d] : x / g.L[d];
             k = (int)(q * g.nd[d]);
             if (SIDE == kSideFine) kf = (int)(q * fg->nd[d]);
             if (SIDE == kSideHalo) xs = x;
         }
         const int n = (int)g.n[d];
         if (k >= n) k -= n;
-        if (g.fine) k %= (int)g.fmod[d];
+        if (GEO == kGeoAny && g.fine) k %= (int)g.fmod[d];
         if (SIDE == kSideFine) {
             const int nf = (int)fg->n[d], f = (int)fg->fmod[d];
             if (kf >= nf) kf -= nf;
@@ -279,14 +288,15 @@ __device__ __forceinline__ bool bin_row_fast(PosT* row, const Geom& g, bool* dir
 // DIM > 0: compile-time dimensionality (the common 1-3); 0: runtime g.dim.
 // SIDE: *side gets the row's fine cell (row-major over fg->fmod) or its face
 // flags (bit 2d: right face of dimension d, bit 2d+1: left face).
-template <typename PosT, bool kPeriodic, int DIM = 0, int SIDE = kSideNone>
+template <typename PosT, bool kPeriodic, int DIM = 0, int SIDE = kSideNone, int GEO = kGeoAny>
 __device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long* idx,
                                              bool* dirty, const FineGeom* fg = nullptr,
                                              const HaloGeom* hg = nullptr,
                                              long long* side = nullptr) {
     if constexpr (DIM > 0) {
         long long c;
-        if (!idx && g.fast32 && bin_row_fast<PosT, kPeriodic, DIM, SIDE>(row, g, dirty, fg, hg, &c, side))
+        if (!idx && (GEO != kGeoAny || g.fast32) &&
+            bin_row_fast<PosT, kPeriodic, DIM, SIDE, GEO>(row, g, dirty, fg, hg, &c, side))
             return c;
     }
     long long cell = 0, sc = 0;

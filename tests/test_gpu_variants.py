@@ -21,8 +21,10 @@ from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _li
 DEFAULTS = {"xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "pack_coop": 1,
             "pack_nt": 0, "many_rows": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1,
             "pack_many": 1, "pack_fine": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
-            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1}
+            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0}
 VARIANTS = [
+    {"bin_geo": 0},
+    {"bin_geo": 0, "bin_skip_clean": 0},
     {"xcd_pack": 1, "xcd_bin": 1},
     {"bin_skip_clean": 0},
     {"tile_rounds": 8},
