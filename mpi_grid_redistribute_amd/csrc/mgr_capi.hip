@@ -772,7 +772,6 @@ int mgr_tune(const char* key, int64_t value) {
     if (!key) return fail(MGR_EINVAL, "null key");
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
-    else if (!strcmp(key, "pack_nt")) mgr::g_tune.pack_nt = (int)value;
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
     else if (!strcmp(key, "rank_rows")) {
         if (value != 0 && value != 2048 && value != 4096)
@@ -805,10 +804,7 @@ int mgr_tune(const char* key, int64_t value) {
         mgr::g_tune.scan_chunk = (int)value;
     }
     else if (!strcmp(key, "prof_mask")) mgr::g_tune.prof_mask = value;
-    else if (!strcmp(key, "pack_rpw")) {
-        if (value < 1 || value > 2) return fail(MGR_EINVAL, "pack_rpw %lld", (long long)value);
-        mgr::g_tune.pack_rpw = (int)value;
-    } else if (!strcmp(key, "scan_spins")) {
+    else if (!strcmp(key, "scan_spins")) {
         if (value < -1 || value > (1 << 30)) return fail(MGR_EINVAL, "scan_spins %lld", (long long)value);
         mgr::g_tune.scan_spins = (int)value;
     } else if (!strcmp(key, "bin_waves")) {

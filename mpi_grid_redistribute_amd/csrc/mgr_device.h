@@ -433,9 +433,14 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Clang vector types, not HIP's uint4/uint2: those are union wrappers that
+// SROA can leave as an alloca, which the backend then parks in LDS (a
+// ds_write/ds_read pair per unit -- measured +15 % on the coop pack).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 template <int W> struct Unit;
-template <> struct Unit<16> { using T = uint4; };
-template <> struct Unit<8> { using T = uint2; };
+template <> struct Unit<16> { using T = u32x4_t; };
+template <> struct Unit<8> { using T = u32x2_t; };
 template <> struct Unit<4> { using T = uint32_t; };
 template <> struct Unit<2> { using T = uint16_t; };
 template <> struct Unit<1> { using T = uint8_t; };
@@ -526,8 +531,6 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t T) {
 
 // Streaming accesses: NT selects the nontemporal (nt) cache policy for data
 // that is read or written exactly once.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 template <bool NT, typename T>
 __device__ __forceinline__ T ld(const T* p) {
     if constexpr (!NT) {

@@ -136,13 +136,11 @@ struct Tune {
     int bin_staged = 1;    // stage 64-row position slabs through LDS
     int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
     int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
-    int pack_nt = 0;       // 1: nontemporal payload loads; 2: loads and stores (small/coop)
     int bin_skip_clean = 1;  // write a position slab back only if a row changed
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
     int xcd_pack = 1;      // ... in the pack kernels
     int pack_fine = 1;     // sorted-image pack for 65..1024 bins (4-byte-multiple rows)
     int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
-    int pack_rpw = 1;      // 64-row rounds per pack wave (1: 1024-row tiles, 2: 2048)
     int bin_waves = 0;     // waves per bin workgroup (1..16; a tile's rounds split over them; 0: auto)
     int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
     int pack_compact = 1;  // selections (2 bins, bin 1 dropped): wave-per-tile compaction

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
 // barrier) to get each bin's base inside the tile.  Unit-transposed moves:
 // lane l moves W-byte units 64k + l of the round, so each load instruction
 // reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
-template <int W, int UPR, bool NT, int RPW, bool NTS>
+template <int W, int UPR, int RPW>
 __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
@@ -118,12 +118,12 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
             for (int k = 0; k < UPR; ++k) {
                 const int u = 64 * k + lane;
                 const int rb = __shfl((int)b[q], u / UPR, 64);
-                if (u < nr[q] * UPR && rb != drop_bin) v[q][k] = ld<NT>(sp + u);
+                if (u < nr[q] * UPR && rb != drop_bin) v[q][k] = sp[u];
             }
         } else {
 #pragma unroll
             for (int k = 0; k < UPR; ++k)
-                if (64 * k + lane < nr[q] * UPR) v[q][k] = ld<NT>(sp + 64 * k + lane);
+                if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
         }
     }
     // rank inside each round; lane l counts bin l
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
             const long long t = __shfl(tgt, r, 64);
             if (u < nr[q] * UPR && t >= 0) {
                 U* o = (t >> 62) ? r_u : d_u;
-                st<NTS>(o + (t & ((1ll << 62) - 1)) * UPR + part, v[q][k]);
+                o[(t & ((1ll << 62) - 1)) * UPR + part] = v[q][k];
             }
         }
     }
@@ -950,8 +950,8 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // <= 64 bins: 1024 rows (64 bins: pack 0.92 vs 1.07 ms at 512: longer
     // same-bin runs); more bins: longer tiles keep the [nbins][tiles]
     // histogram small next to the payload.
-    if (nbins <= 16) return 512 * g_tune.pack_rpw;
-    if (nbins <= 64) return 1024 * g_tune.pack_rpw;
+    if (nbins <= 16) return 512;
+    if (nbins <= 64) return 1024;
     // sorted-image pack: 2048-row tiles (its LDS image), rows of 4-byte multiples
     if (g_tune.pack_fine && nbins <= 1024 && row_bytes <= 64 && row_bytes % 4 == 0)
         return fine_tile_rows();
@@ -986,23 +986,17 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
     // one wave per RPW 64-row rounds of the tile (<= 16 waves)
     const int rpw = tile_rows > 1024 ? 2 : 1;
     const int threads = tile_rows / rpw;
-#define MGR_PCK(NT_, RPW_, NTS_)                                                              \
-    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, NT_, RPW_, NTS_>), dim3((unsigned)ws.T),     \
-                       dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, \
-                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,   \
-                       (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack,  \
-                       sel, ws.scan_err, t_side.src, t_side.dst, t_side.red)
+#define MGR_PCK(RPW_)                                                                         \
+    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_>), dim3((unsigned)ws.T), dim3(threads), 0, \
+                       s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),     \
+                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,    \
+                       redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel, ws.scan_err, \
+                       t_side.src, t_side.dst, t_side.red)
     // selection packs (2 bins, one dropped: the halo's rows to send) skip
     // the loads of dropped rows; elsewhere loads go out before the bins are known
     const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
     t_side.used = t_side.src != nullptr;
-    if (g_tune.pack_nt >= 2) {
-        if (rpw == 2) MGR_PCK(true, 2, true); else MGR_PCK(true, 1, true);
-    } else if (g_tune.pack_nt == 1) {
-        if (rpw == 2) MGR_PCK(true, 2, false); else MGR_PCK(true, 1, false);
-    } else {
-        if (rpw == 2) MGR_PCK(false, 2, false); else MGR_PCK(false, 1, false);
-    }
+    if (rpw == 2) MGR_PCK(2); else MGR_PCK(1);
 #undef MGR_PCK
     return hipGetLastError();
 }
@@ -1014,18 +1008,18 @@ static hipError_t pack_coop_t(const void* src, int64_t row_bytes, int64_t n, con
                                int nb, int drop_bin, int tile_rows, const Workspace& ws,
                                void* dst, int redirect_bin, void* redirect_dst, hipStream_t s) {
 #define MGR_PS(U_) case U_: return pack_coop_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    if (W >= 4) {
+    if constexpr (W >= 4) {
         switch ((int)(row_bytes / W)) {
             MGR_PS(1) MGR_PS(2) MGR_PS(3) MGR_PS(4)
             default: break;
         }
-        if (W <= 8) {
+        if constexpr (W <= 8) {
             switch ((int)(row_bytes / W)) {
                 MGR_PS(5) MGR_PS(6) MGR_PS(7) MGR_PS(8)
                 default: break;
             }
         }
-        if (W == 4) {
+        if constexpr (W == 4) {
             switch ((int)(row_bytes / W)) {
                 MGR_PS(9) MGR_PS(10) MGR_PS(11) MGR_PS(12) MGR_PS(13) MGR_PS(14) MGR_PS(15) MGR_PS(16)
                 default: break;
@@ -1069,13 +1063,13 @@ static hipError_t pack_many_t(const void* src, int64_t row_bytes, int64_t n, con
         MGR_PM(1) MGR_PM(2) MGR_PM(3) MGR_PM(4)
         default: break;
     }
-    if (W <= 8) {
+    if constexpr (W <= 8) {
         switch ((int)(row_bytes / W)) {
             MGR_PM(5) MGR_PM(6) MGR_PM(7) MGR_PM(8)
             default: break;
         }
     }
-    if (W == 4) {
+    if constexpr (W == 4) {
         switch ((int)(row_bytes / W)) {
             MGR_PM(9) MGR_PM(10) MGR_PM(11) MGR_PM(12) MGR_PM(13) MGR_PM(14) MGR_PM(15) MGR_PM(16)
             default: break;

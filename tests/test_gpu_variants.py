@@ -19,7 +19,7 @@ mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
 DEFAULTS = {"xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "pack_coop": 1,
-            "pack_nt": 0, "many_rows": 0, "bin_staged": 1, "tile_rounds": 0, "pack_rpw": 1,
+            "many_rows": 0, "bin_staged": 1, "tile_rounds": 0,
             "pack_many": 1, "pack_fine": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
             "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0}
 VARIANTS = [
@@ -34,11 +34,8 @@ VARIANTS = [
     {"bin_skip_clean": 0, "bin_staged": 0},
     {"bin_waves": 1, "xcd_bin": 1},
     {"xcd_pack": 0},
-    {"pack_rpw": 2},
-    {"pack_nt": 2},
-    {"pack_rpw": 2, "pack_nt": 1},
     {"pack_coop": 0},
-    {"pack_coop": 0, "pack_nt": 2},
+    {"pack_coop": 0, "xcd_pack": 0},
     {"pack_many": 0},
     {"pack_fine": 0},
     {"pack_fine": 0, "many_rows": 1024},
@@ -52,7 +49,7 @@ VARIANTS = [
     {"scan_max_chunks": 4096},
     {"scan_max_chunks": 8, "scan_chunk": 256},
     {"many_super": 16, "xcd_pack": 0},
-    {"pack_img": 1, "tile_rounds": 16, "pack_rpw": 2},
+    {"pack_img": 1, "tile_rounds": 16},
     {"pack_img": 1, "xcd_pack": 0, "tile_rounds": 1},
     {"scan_chunk": 65536},
     {"many_rows": 4096},

@@ -57,9 +57,9 @@ def run(variant):
         out[k] = round(ms / max(cnt, 1), 4)
     out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
     out["pack_GBps"] = round((2 * rb + 1) * N / (out["pack"] / 1e3) / 1e9, 1)
-    for k, v in {"bin_staged": 1, "tile_rounds": 0, "pack_nt": 0, "pack_coop": 1,
+    for k, v in {"bin_staged": 1, "tile_rounds": 0, "pack_coop": 1,
                  "xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1,
-                 "bin_waves": 0, "pack_rpw": 1, "pack_many": 1, "scan_chunk": 2048,
+                 "bin_waves": 0, "pack_many": 1, "scan_chunk": 2048,
                  "pack_img": 1, "many_super": 1, "scan_max_chunks": 1024, "pack_sel": 1,
                  "pack_compact": 1, "many_rows": 0, "pack_fine": 1, "bin_geo": 1}.items():
         _lib.tune(k, v)

@@ -2,7 +2,7 @@
 2^26 uniform particles, 2x2x2): the whole step's time, so effects a kernel
 has on the NEXT kernel (dirty lines it leaves in L2/MALL) show up, which the
 per-kernel A/B (kbench.py) cannot see.  Interleaved repeats, median ms/step.
-Usage: python tools/step_ab.py '[{"pack_nt": 1}, {"xcd_bin": 1}]'"""
+Usage: python tools/step_ab.py '[{"xcd_pack": 0}, {"xcd_bin": 1}]'"""
 import json
 import os
 import sys
@@ -35,7 +35,7 @@ for rep in range(reps):
         torch.cuda.synchronize()
         res[i].append((time.perf_counter() - t0) / steps * 1e3)
         for k in v:
-            _lib.tune(k, {"pack_nt": 0, "xcd_bin": 0, "xcd_pack": 1, "bin_waves": 4}.get(k, 0))
+            _lib.tune(k, {"xcd_bin": 0, "xcd_pack": 1, "bin_waves": 0}.get(k, 0))
     print("rep", rep, [round(res[i][-1], 4) for i in res], flush=True)
 for i, v in enumerate(variants):
     r = sorted(res[i])
