@@ -322,7 +322,7 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
 /* -------------------------------------------------------------- tuning --
  * Kernel-variant knobs for A/B measurement: "bin_staged", "bin_skip_clean",
  * "bin_waves", "bin_geo", "xcd_bin", "pack_coop", "xcd_pack", "tile_rounds",
- * "scan_chunk", "scan_max_chunks", "pack_img", "pack_sel", "pack_compact",
+ * "scan_chunk", "scan_max_chunks", "pack_img", "img_rpw", "pack_sel", "pack_compact",
  * "pack_many", "pack_fine", "many_super", "many_rows", "rank_rows", "scan_spins" (polls
  * per look-back word before the scan gives up; -1 gives up at once, for
  * tests of the failure path) and "prof_mask" (bit k: time profiler kernel id

@@ -773,6 +773,10 @@ int mgr_tune(const char* key, int64_t value) {
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
+    else if (!strcmp(key, "img_rpw")) {
+        if (value != 1 && value != 2) return fail(MGR_EINVAL, "img_rpw %lld (1 or 2)", (long long)value);
+        mgr::g_tune.img_rpw = (int)value;
+    }
     else if (!strcmp(key, "rank_rows")) {
         if (value != 0 && value != 2048 && value != 4096)
             return fail(MGR_EINVAL, "rank_rows %lld (0, 2048 or 4096)", (long long)value);

@@ -150,6 +150,7 @@ struct Tune {
     int scan_max_chunks = 1024;  // one-pass scan: at most this many chunks (look-back depth)
     int scan_spins = 1 << 24;    // one-pass scan: polls per look-back word before giving up
                                  // (-1: give up at once -- tests of the error path)
+    int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
     int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
     int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096
     int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)

@@ -491,7 +491,7 @@ __device__ __forceinline__ void gstore(unsigned long long a, const T& v) {
     *(__attribute__((address_space(1))) T*)a = v;
 }
 
-template <int RB>
+template <int RB, int RPW>
 __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
@@ -500,10 +500,11 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
-    constexpr int RBYTES = 64 * RB;                 // one round, a multiple of 16
+    constexpr int WR = 64 * RPW;                    // rows per wave (RPW consecutive rounds)
+    constexpr int RBYTES = WR * RB;                 // the wave's rows, a multiple of 16
     constexpr int NU = (RBYTES / 16 + 63) / 64;     // 16-byte units per lane
     constexpr int DW = RB / 4;
-    constexpr int WAVE_LDS = RBYTES + 64 * 8 + 64;  // image, per-bin output address, row bins
+    constexpr int WAVE_LDS = RBYTES + 64 * 8 + WR;  // image, per-bin output address, row bins
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int nw = blockDim.x >> 6;
@@ -513,12 +514,17 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     uint8_t* ibin = img + RBYTES + 64 * 8;
     uint32_t* imgw = (uint32_t*)img;
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
-    const int64_t row0 = tile * (int64_t)tile_rows + 64 * w;
-    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
-    const int nbytes = nr * RB;
-    const bool valid = lane < nr;
-    const unsigned b = valid ? (unsigned)dest[row0 + lane] : 0u;
-    const unsigned idv = id_src && valid ? (unsigned)id_src[row0 + lane] : 0u;   // side field
+    const int64_t row0 = tile * (int64_t)tile_rows + (int64_t)WR * w;
+    const int nrows = (int)max((int64_t)0, min((int64_t)WR, n - row0));
+    const int nbytes = nrows * RB;
+    unsigned b[RPW], idv[RPW];
+    bool valid[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        valid[q] = 64 * q + lane < nrows;
+        b[q] = valid[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+        idv[q] = id_src && valid[q] ? (unsigned)id_src[row0 + 64 * q + lane] : 0u;  // side field
+    }
     long long tbase = 0;
     if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
     const uint8_t* __restrict__ sp = src + row0 * RB;
@@ -528,8 +534,14 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
         const int x = 16 * (64 * k + lane);
         bool need = true;
         if (sel) {   // selection: skip units whose rows (at most two, RB > 16) are all dropped
-            const int b0 = __shfl((int)b, min(x / RB, 63), 64);
-            const int b1 = __shfl((int)b, min((x + 15) / RB, 63), 64);
+            const int r0 = min(x / RB, WR - 1), r1 = min((x + 15) / RB, WR - 1);
+            int b0 = 0, b1 = 0;
+#pragma unroll
+            for (int q = 0; q < RPW; ++q) {
+                const int t0 = __shfl((int)b[q], r0 & 63, 64), t1 = __shfl((int)b[q], r1 & 63, 64);
+                if ((r0 >> 6) == q) b0 = t0;
+                if ((r1 >> 6) == q) b1 = t1;
+            }
             need = b0 != drop_bin || b1 != drop_bin;
         }
         if (!need) {
@@ -541,14 +553,21 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
                            x + 12 < nbytes ? q[3] : 0u};
         }
     }
-    // rank inside the round; lane l counts bin l
-    unsigned long long pe = __ballot(valid), mine = pe;
-    for (int i = 0; i < nbits; ++i) {
-        const unsigned long long m = __ballot((b >> i) & 1u);
-        pe &= ((b >> i) & 1u) ? m : ~m;
-        mine &= ((lane >> i) & 1) ? m : ~m;
+    // rank inside each round; lane l counts bin l per round, cnt over the wave
+    unsigned long long pe[RPW];
+    int cq[RPW], cnt = 0;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        unsigned long long p = __ballot(valid[q]), mine = p;
+        for (int i = 0; i < nbits; ++i) {
+            const unsigned long long m = __ballot((b[q] >> i) & 1u);
+            p &= ((b[q] >> i) & 1u) ? m : ~m;
+            mine &= ((lane >> i) & 1) ? m : ~m;
+        }
+        pe[q] = p;
+        cq[q] = __popcll(mine);
+        cnt += cq[q];
     }
-    const int cnt = __popcll(mine);
     s_cnt[w * 64 + lane] = cnt;
 #pragma unroll
     for (int k = 0; k < NU; ++k) {
@@ -558,7 +577,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     __syncthreads();
     if (scan_failed(scan_err)) return;
     for (int j = 0; j < w; ++j) tbase += s_cnt[j * 64 + lane];
-    // round image order: exclusive prefix of the round's bin counts
+    // wave image order: exclusive prefix of the wave's bin counts
     int incl = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -566,27 +585,41 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
         if (lane >= o) incl += y;
     }
     const int excl = incl - cnt;
-    const int slot = __shfl(excl, (int)b, 64) + (valid ? rank_in(pe) : 0);
+    int slot[RPW];
+    int run = excl;   // lane b: bin b's next image slot, round by round
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        slot[q] = __shfl(run, (int)b[q], 64) + (valid[q] ? rank_in(pe[q]) : 0);
+        run += cq[q];
+    }
     if (lane < nb) {
         uint8_t* base = lane == redirect_bin ? redirect_dst : dst;
         gaddr[lane] = lane == drop_bin ? 0ull
                                        : (unsigned long long)(base + (tbase - excl) * (long long)RB);
     }
-    if (id_src) {   // the row's output row: its bin's (tile base - round start) + image slot
-        const long long gr = __shfl(tbase - excl, (int)b, 64) + slot;
-        if (valid && (int)b != drop_bin) ((int)b == redirect_bin ? id_red : id_dst)[gr] = (uint16_t)idv;
-    }
-    uint32_t row[DW];
-    if (valid) {
+    if (id_src) {   // the row's output row: its bin's (tile base - wave image start) + image slot
 #pragma unroll
-        for (int p = 0; p < DW; ++p) row[p] = imgw[lane * DW + p];
+        for (int q = 0; q < RPW; ++q) {
+            const long long gr = __shfl(tbase - excl, (int)b[q], 64) + slot[q];
+            if (valid[q] && (int)b[q] != drop_bin)
+                ((int)b[q] == redirect_bin ? id_red : id_dst)[gr] = (uint16_t)idv[q];
+        }
     }
+    uint32_t row[RPW][DW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q)
+        if (valid[q]) {
+#pragma unroll
+            for (int p = 0; p < DW; ++p) row[q][p] = imgw[(64 * q + lane) * DW + p];
+        }
     wave_sync();
-    if (valid) {
 #pragma unroll
-        for (int p = 0; p < DW; ++p) imgw[slot * DW + p] = row[p];
-        ibin[slot] = (uint8_t)b;
-    }
+    for (int q = 0; q < RPW; ++q)
+        if (valid[q]) {
+#pragma unroll
+            for (int p = 0; p < DW; ++p) imgw[slot[q] * DW + p] = row[q][p];
+            ibin[slot[q]] = (uint8_t)b[q];
+        }
     wave_sync();
 #pragma unroll
     for (int k = 0; k < NU; ++k) {
@@ -1083,9 +1116,15 @@ template <int RB>
 static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                              int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                              void* redirect_dst, hipStream_t s) {
-    const int nw = tile_rows / 64;
-    const int lds = nw * 64 * 4 + nw * (64 * RB + 64 * 8 + 64);
-    auto k = pack_img_kernel<RB>;
+    // img_rpw 64-row rounds per wave when they divide the tile: 2 (A/B, 36-B
+    // records: 0.90-0.92 vs 1.02-1.05 ms per 64M, 4: 1.17 -- a wave's fixed
+    // per-round chain of load, count exchange, LDS permutation and store then
+    // moves twice the rows)
+    int rpw = g_tune.img_rpw;
+    while (rpw > 1 && tile_rows % (64 * rpw)) rpw >>= 1;
+    const int nw = tile_rows / (64 * rpw);
+    const int lds = nw * 64 * 4 + nw * (64 * rpw * RB + 64 * 8 + 64 * rpw);
+    auto k = rpw == 2 ? pack_img_kernel<RB, 2> : pack_img_kernel<RB, 1>;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s,
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,

@@ -21,8 +21,11 @@ from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _li
 DEFAULTS = {"xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "pack_coop": 1,
             "many_rows": 0, "bin_staged": 1, "tile_rounds": 0,
             "pack_many": 1, "pack_fine": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
-            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0}
+            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0, "img_rpw": 2}
 VARIANTS = [
+    {"img_rpw": 1},
+    {"img_rpw": 1, "tile_rounds": 1},
+    {"img_rpw": 2, "tile_rounds": 16, "pack_sel": 0},
     {"bin_geo": 0},
     {"bin_geo": 0, "bin_skip_clean": 0},
     {"xcd_pack": 1, "xcd_bin": 1},
@@ -133,14 +136,16 @@ def test_cellnum_drop_variant(variant):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), r
 
 
+@pytest.mark.parametrize("img_rpw", [1, 2])
 @pytest.mark.parametrize("row_bytes", [12, 20, 24, 28, 36, 40, 44, 52, 56, 60])
 @pytest.mark.parametrize("topo", [[2, 2, 2], [4, 4, 4], [7], [1]])
-def test_image_pack_row_sizes(row_bytes, topo):
+def test_image_pack_row_sizes(row_bytes, topo, img_rpw):
     """pack_img (16-byte image pack) for every row size it takes, ragged n,
     1..64 bins, against the C oracle."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     _lib.tune("pack_img", 2)     # every row size the image pack takes
+    _lib.tune("img_rpw", img_rpw)
     try:
         rng = np.random.default_rng(row_bytes * 31 + len(topo))
         n = 50_003 + 7 * row_bytes
@@ -157,6 +162,7 @@ def test_image_pack_row_sizes(row_bytes, topo):
         assert np.array_equal(out.cpu().numpy(), exp)
     finally:
         _lib.tune("pack_img", DEFAULTS["pack_img"])
+        _lib.tune("img_rpw", DEFAULTS["img_rpw"])
 
 
 @pytest.mark.parametrize("case", ["halo_p8_f64_rec32.npz", "halo_p2_f32_rec36.npz",
