@@ -411,6 +411,29 @@ __device__ __forceinline__ long long seg_start(const int64_t* __restrict__ offse
     return o;
 }
 
+// seg_start for bin min(lane, nb - 1) in two steps: seg_load issues the
+// loads unconditionally (no exec mask, no use of their values), seg_value
+// combines them -- so a kernel can put its payload loads in between and
+// wait for everything once.  Lanes >= nb get a value they must not use.
+struct SegLoad {
+    long long o, own, gap;
+};
+__device__ __forceinline__ SegLoad seg_load(const int64_t* __restrict__ offsets,
+                                            const int64_t* __restrict__ bin_starts, int64_t T,
+                                            int64_t tile, int lane, int nb, int redirect_bin) {
+    const int b = min(lane, nb - 1);
+    SegLoad s{offsets[(int64_t)b * T + tile], 0, 0};
+    if (redirect_bin >= 0) {   // uniform
+        s.own = bin_starts[b];
+        s.gap = bin_starts[redirect_bin + 1] - bin_starts[redirect_bin];
+    }
+    return s;
+}
+__device__ __forceinline__ long long seg_value(const SegLoad& s, int lane, int redirect_bin) {
+    if (redirect_bin < 0) return s.o;
+    return s.o - (lane == redirect_bin ? s.own : (lane > redirect_bin ? s.gap : 0ll));
+}
+
 // A failed scan (ScanCtl::err, mgr_kernels.hip) leaves offsets that must
 // not be written through: every pack kernel checks it before its first
 // store (the word was written by an earlier kernel, a uniform read).

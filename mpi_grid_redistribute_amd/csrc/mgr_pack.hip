@@ -82,12 +82,12 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
 // barrier) to get each bin's base inside the tile.  Unit-transposed moves:
 // lane l moves W-byte units 64k + l of the round, so each load instruction
 // reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
-template <int W, int UPR, int RPW>
+template <int W, int UPR, int RPW, bool SEL>
 __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
     const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     using U = typename Unit<W>::T;
@@ -96,23 +96,28 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
     // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
     const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
-    // issue every load of the wave's rounds first
+    // issue every load of the wave's rounds first, branch-free (indices
+    // clamped into the arrays; rows past n are masked by nr afterwards), so
+    // the first wait -- for the destination bytes -- leaves the payload,
+    // side-field and segment-start loads in flight
     int nr[RPW];
-    unsigned b[RPW];
+    unsigned braw[RPW], b[RPW];
     U v[RPW][UPR];
     unsigned idv[RPW];   // side field: every row's 2-byte id (fine cell), moved alike
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
-        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
-        idv[q] = id_src && lane < nr[q] ? (unsigned)id_src[row0 + 64 * q + lane] : 0u;
+        const int64_t r = min(row0 + 64 * q + lane, n - 1);
+        braw[q] = (unsigned)dest[r];
+        idv[q] = id_src ? (unsigned)id_src[r] : 0u;
     }
-    long long tbase = 0;
-    if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
+    const SegLoad seg = seg_load(offsets, bin_starts, T, tile, lane, nb, redirect_bin);
+    if constexpr (SEL) {
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
-        if (sel) {
+        for (int q = 0; q < RPW; ++q) b[q] = lane < nr[q] ? braw[q] : 0u;
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
             // selection (most rows dropped): load only the units of kept rows
 #pragma unroll
             for (int k = 0; k < UPR; ++k) {
@@ -120,12 +125,19 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
                 const int rb = __shfl((int)b[q], u / UPR, 64);
                 if (u < nr[q] * UPR && rb != drop_bin) v[q][k] = sp[u];
             }
-        } else {
+        }
+    } else {
+        const U* __restrict__ s_u = (const U*)src;
+        const int64_t last = n * UPR - 1;
+#pragma unroll
+        for (int q = 0; q < RPW; ++q)
 #pragma unroll
             for (int k = 0; k < UPR; ++k)
-                if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
-        }
+                v[q][k] = s_u[min((row0 + 64 * q) * UPR + 64 * k + lane, last)];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) b[q] = lane < nr[q] ? braw[q] : 0u;
     }
+    long long tbase = lane < nb ? seg_value(seg, lane, redirect_bin) : 0;
     // rank inside each round; lane l counts bin l
     unsigned long long peers[RPW];
     int cnt[RPW];
@@ -491,12 +503,12 @@ __device__ __forceinline__ void gstore(unsigned long long a, const T& v) {
     *(__attribute__((address_space(1))) T*)a = v;
 }
 
-template <int RB, int RPW>
+template <int RB, int RPW, bool SEL>
 __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
     const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
@@ -517,23 +529,37 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     const int64_t row0 = tile * (int64_t)tile_rows + (int64_t)WR * w;
     const int nrows = (int)max((int64_t)0, min((int64_t)WR, n - row0));
     const int nbytes = nrows * RB;
-    unsigned b[RPW], idv[RPW];
+    // every load issued first, branch-free (clamped indices; rows past n are
+    // masked by valid / nbytes afterwards): the first wait -- for the
+    // destination bytes -- leaves the payload and side loads in flight
+    unsigned braw[RPW], b[RPW], idv[RPW];
     bool valid[RPW];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         valid[q] = 64 * q + lane < nrows;
-        b[q] = valid[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
-        idv[q] = id_src && valid[q] ? (unsigned)id_src[row0 + 64 * q + lane] : 0u;  // side field
+        const int64_t r = min(row0 + 64 * q + lane, n - 1);
+        braw[q] = (unsigned)dest[r];
+        idv[q] = id_src ? (unsigned)id_src[r] : 0u;  // side field
     }
-    long long tbase = 0;
-    if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
+    const SegLoad seg = seg_load(offsets, bin_starts, T, tile, lane, nb, redirect_bin);
     const uint8_t* __restrict__ sp = src + row0 * RB;
     u32x4_t v[NU];
+    if constexpr (!SEL) {
+        // a 16-byte unit that starts inside the array stays inside its page;
+        // units past the wave's rows re-read the array's last one (never stored)
+        const int64_t xmax = ((n * RB - 1) & ~(int64_t)15) - row0 * RB;
 #pragma unroll
-    for (int k = 0; k < NU; ++k) {
+        for (int k = 0; k < NU; ++k)
+            v[k] = *(const u32x4_t*)(sp + min((int64_t)(16 * (64 * k + lane)), xmax));
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) b[q] = valid[q] ? braw[q] : 0u;
+    long long tbase = lane < nb ? seg_value(seg, lane, redirect_bin) : 0;
+#pragma unroll
+    for (int k = 0; k < NU && SEL; ++k) {
         const int x = 16 * (64 * k + lane);
         bool need = true;
-        if (sel) {   // selection: skip units whose rows (at most two, RB > 16) are all dropped
+        {   // selection: skip units whose rows (at most two, RB > 16) are all dropped
             const int r0 = min(x / RB, WR - 1), r1 = min((x + 15) / RB, WR - 1);
             int b0 = 0, b1 = 0;
 #pragma unroll
@@ -1019,17 +1045,21 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
     // one wave per RPW 64-row rounds of the tile (<= 16 waves)
     const int rpw = tile_rows > 1024 ? 2 : 1;
     const int threads = tile_rows / rpw;
-#define MGR_PCK(RPW_)                                                                         \
-    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_>), dim3((unsigned)ws.T), dim3(threads), 0, \
-                       s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),     \
-                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,    \
-                       redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel, ws.scan_err, \
-                       t_side.src, t_side.dst, t_side.red)
+#define MGR_PCK(RPW_, SEL_)                                                                   \
+    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_, SEL_>), dim3((unsigned)ws.T),           \
+                       dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb,  \
+                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,    \
+                       (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack,   \
+                       ws.scan_err, t_side.src, t_side.dst, t_side.red)
     // selection packs (2 bins, one dropped: the halo's rows to send) skip
     // the loads of dropped rows; elsewhere loads go out before the bins are known
-    const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
+    const bool sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
     t_side.used = t_side.src != nullptr;
-    if (rpw == 2) MGR_PCK(2); else MGR_PCK(1);
+    if (sel) {
+        if (rpw == 2) MGR_PCK(2, true); else MGR_PCK(1, true);
+    } else {
+        if (rpw == 2) MGR_PCK(2, false); else MGR_PCK(1, false);
+    }
 #undef MGR_PCK
     return hipGetLastError();
 }
@@ -1124,13 +1154,14 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
     while (rpw > 1 && tile_rows % (64 * rpw)) rpw >>= 1;
     const int nw = tile_rows / (64 * rpw);
     const int lds = nw * 64 * 4 + nw * (64 * rpw * RB + 64 * 8 + 64 * rpw);
-    auto k = rpw == 2 ? pack_img_kernel<RB, 2> : pack_img_kernel<RB, 1>;
+    const bool sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
+    auto k = sel ? (rpw == 2 ? pack_img_kernel<RB, 2, true> : pack_img_kernel<RB, 1, true>)
+                 : (rpw == 2 ? pack_img_kernel<RB, 2, false> : pack_img_kernel<RB, 1, false>);
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s,
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
-                       (uint8_t*)redirect_dst, g_tune.xcd_pack,
-                       g_tune.pack_sel && nb <= 2 && drop_bin >= 0, ws.scan_err, t_side.src,
+                       (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err, t_side.src,
                        t_side.dst, t_side.red);
     t_side.used = t_side.src != nullptr;
     return hipGetLastError();

@@ -66,7 +66,7 @@ def bench(lib, pos, rec, rb, nbins=8, topo=(2, 2, 2)):
 def main():
     pos2, rec2 = mgr.synth_uniform(N, seed=1)
     rec5, pos5 = mgr.synth_wide(N, seed=3)
-    for rep in range(2):
+    for rep in range(int(os.environ.get("AB_REPEAT", 3))):
         for lib in sys.argv[1:]:
             r2 = bench(lib, pos2, rec2.reshape(-1), 32)
             r5 = bench(lib, pos5, rec5.reshape(-1), 36)
