@@ -82,12 +82,15 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
 // barrier) to get each bin's base inside the tile.  Unit-transposed moves:
 // lane l moves W-byte units 64k + l of the round, so each load instruction
 // reads 64*W contiguous bytes; the unit's row gets its slot by shfl.
-template <int W, int UPR, int RPW, bool SEL>
+// (A/B, same box: issuing every load branch-free before the first wait, as
+// the image pack does, made this kernel slower -- 0.86 vs 0.77 ms at config 2
+// -- so the destination bytes are waited for before the payload loads go out.)
+template <int W, int UPR, int RPW>
 __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
     const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
     const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     using U = typename Unit<W>::T;
@@ -96,28 +99,23 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
     // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
     const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
-    // issue every load of the wave's rounds first, branch-free (indices
-    // clamped into the arrays; rows past n are masked by nr afterwards), so
-    // the first wait -- for the destination bytes -- leaves the payload,
-    // side-field and segment-start loads in flight
+    // issue every load of the wave's rounds first
     int nr[RPW];
-    unsigned braw[RPW], b[RPW];
+    unsigned b[RPW];
     U v[RPW][UPR];
     unsigned idv[RPW];   // side field: every row's 2-byte id (fine cell), moved alike
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         nr[q] = (int)max((int64_t)0, min((int64_t)64, n - row0 - 64 * q));
-        const int64_t r = min(row0 + 64 * q + lane, n - 1);
-        braw[q] = (unsigned)dest[r];
-        idv[q] = id_src ? (unsigned)id_src[r] : 0u;
+        b[q] = lane < nr[q] ? (unsigned)dest[row0 + 64 * q + lane] : 0u;
+        idv[q] = id_src && lane < nr[q] ? (unsigned)id_src[row0 + 64 * q + lane] : 0u;
     }
-    const SegLoad seg = seg_load(offsets, bin_starts, T, tile, lane, nb, redirect_bin);
-    if constexpr (SEL) {
+    long long tbase = 0;
+    if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
 #pragma unroll
-        for (int q = 0; q < RPW; ++q) b[q] = lane < nr[q] ? braw[q] : 0u;
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+    for (int q = 0; q < RPW; ++q) {
+        const U* __restrict__ sp = (const U*)src + (row0 + 64 * q) * UPR;
+        if (sel) {
             // selection (most rows dropped): load only the units of kept rows
 #pragma unroll
             for (int k = 0; k < UPR; ++k) {
@@ -125,19 +123,12 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
                 const int rb = __shfl((int)b[q], u / UPR, 64);
                 if (u < nr[q] * UPR && rb != drop_bin) v[q][k] = sp[u];
             }
-        }
-    } else {
-        const U* __restrict__ s_u = (const U*)src;
-        const int64_t last = n * UPR - 1;
-#pragma unroll
-        for (int q = 0; q < RPW; ++q)
+        } else {
 #pragma unroll
             for (int k = 0; k < UPR; ++k)
-                v[q][k] = s_u[min((row0 + 64 * q) * UPR + 64 * k + lane, last)];
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) b[q] = lane < nr[q] ? braw[q] : 0u;
+                if (64 * k + lane < nr[q] * UPR) v[q][k] = sp[64 * k + lane];
+        }
     }
-    long long tbase = lane < nb ? seg_value(seg, lane, redirect_bin) : 0;
     // rank inside each round; lane l counts bin l
     unsigned long long peers[RPW];
     int cnt[RPW];
@@ -1045,21 +1036,17 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
     // one wave per RPW 64-row rounds of the tile (<= 16 waves)
     const int rpw = tile_rows > 1024 ? 2 : 1;
     const int threads = tile_rows / rpw;
-#define MGR_PCK(RPW_, SEL_)                                                                   \
-    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_, SEL_>), dim3((unsigned)ws.T),           \
-                       dim3(threads), 0, s, (const uint8_t*)src, n, (const uint8_t*)dest, nb,  \
-                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,    \
-                       (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack,   \
-                       ws.scan_err, t_side.src, t_side.dst, t_side.red)
+#define MGR_PCK(RPW_)                                                                         \
+    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_>), dim3((unsigned)ws.T), dim3(threads), 0, \
+                       s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),     \
+                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,    \
+                       redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel, ws.scan_err, \
+                       t_side.src, t_side.dst, t_side.red)
     // selection packs (2 bins, one dropped: the halo's rows to send) skip
     // the loads of dropped rows; elsewhere loads go out before the bins are known
-    const bool sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
+    const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
     t_side.used = t_side.src != nullptr;
-    if (sel) {
-        if (rpw == 2) MGR_PCK(2, true); else MGR_PCK(1, true);
-    } else {
-        if (rpw == 2) MGR_PCK(2, false); else MGR_PCK(1, false);
-    }
+    if (rpw == 2) MGR_PCK(2); else MGR_PCK(1);
 #undef MGR_PCK
     return hipGetLastError();
 }
