@@ -400,11 +400,7 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     const int64_t chunk = (ws.T + cpb - 1) / cpb;
     cpb = (ws.T + chunk - 1) / chunk;                 // no empty chunk
     prof_begin(s, K_SCAN);
-    // a chunk of up to 32 counts per thread is read once and kept in
-    // registers (one block scan); longer chunks loop over tiles twice
-    auto k = chunk <= 8 * kBlock    ? scan_onepass_kernel<8>
-             : chunk <= 16 * kBlock ? scan_onepass_kernel<16>
-                                    : scan_onepass_kernel<32>;
+    auto k = chunk <= 8 * kBlock ? scan_onepass_kernel<8> : scan_onepass_kernel<16>;
     hipLaunchKernelGGL(k, dim3((unsigned)(nbins * cpb)), dim3(kBlock), 0, s, ws.counts, ws.T,
                        chunk, (int)cpb, nbins, ws.flags, ws.offsets, ws.bin_starts, bin_counts,
                        g_tune.scan_spins);
