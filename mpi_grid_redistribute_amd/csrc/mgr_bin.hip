@@ -407,25 +407,28 @@ __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __res
 // waves); per tile: every bin's start inside the tile (tile_starts[t][b],
 // tile-major, contiguous) and its count (counts[b * T + t], for mgr_scan).
 // The ranking work leaves the pack, which then only places rows.
-template <int NW>
+// RPW > 0 / NBITS > 0: the rounds per wave and the id bits at compile time
+// (the ranked tiles of mgr_ranked_tile_rows, 512 cells): unrolled rounds in
+// named registers and an unrolled ballot match; 0: read at run time.
+template <int NW, int RPW, int NBITS>
 __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     const uint16_t* __restrict__ ids, int64_t n, int nbins, int nbits,
     int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ ranks,
     uint16_t* __restrict__ tile_starts, uint8_t* __restrict__ dest8,
     uint64_t* __restrict__ scan_flags) {
-    constexpr int NT = NW * 64, RPW_MAX = 4096 / 64 / NW;
+    constexpr int NT = NW * 64, RPW_MAX = RPW > 0 ? RPW : 4096 / 64 / NW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint16_t* wt = (uint16_t*)smem;   // [NW][nbins]
     __shared__ int s_wsum[NW];
     clear_scan_flags(scan_flags);
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const int64_t tile = xcd_tile(blockIdx.x, T);
-    const int rpw = tile_rows / 64 / NW;
+    const int rpw = RPW > 0 ? RPW : tile_rows / 64 / NW;
     for (int i = tid; i < NW * nbins; i += NT) wt[i] = 0;
     unsigned b[RPW_MAX];
 #pragma unroll
     for (int q = 0; q < RPW_MAX; ++q) {
-        if (q >= rpw) break;
+        if (RPW == 0 && q >= rpw) break;
         const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
         b[q] = row < n ? (unsigned)ids[row] : 0u;
     }
@@ -433,11 +436,11 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     int rk[RPW_MAX];
 #pragma unroll
     for (int q = 0; q < RPW_MAX; ++q) {
-        if (q >= rpw) break;
+        if (RPW == 0 && q >= rpw) break;
         const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
         const bool valid = row < n;
         if (dest8 && valid) dest8[row] = (uint8_t)b[q];
-        const unsigned long long peers = match_bin(b[q], valid, nbits);
+        const unsigned long long peers = match_bin_t<NBITS>(b[q], valid, nbits);
         const int r = rank_in(peers);
         const int before = valid ? (int)wt[w * nbins + b[q]] : 0;
         wave_sync();
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     }
 #pragma unroll
     for (int q = 0; q < RPW_MAX; ++q) {
-        if (q >= rpw) break;
+        if (RPW == 0 && q >= rpw) break;
         const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
         if (row < n) ranks[row] = (uint16_t)(wt[w * nbins + b[q]] + rk[q]);
     }
@@ -498,7 +501,10 @@ hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_r
     // 4 waves (16 waves measured 0.57 vs 0.31 ms at 64M rows, 512 bins)
     const int nw = kWaves;
     const int lds = align16(nw * nbins * 2);
-    auto k = rank_ids_kernel<kWaves>;
+    const bool b9 = nbits_for(nbins) == 9;   // 257..512 cells (8x8x8)
+    auto k = tile_rows == 4096 ? (b9 ? rank_ids_kernel<kWaves, 16, 9> : rank_ids_kernel<kWaves, 16, 0>)
+           : tile_rows == 2048 ? (b9 ? rank_ids_kernel<kWaves, 8, 9> : rank_ids_kernel<kWaves, 8, 0>)
+                               : rank_ids_kernel<kWaves, 0, 0>;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s, ids, n, nbins,
                        nbits_for(nbins), ws.counts, ws.T, tile_rows, ranks, tile_starts, dest8,

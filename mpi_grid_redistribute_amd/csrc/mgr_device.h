@@ -329,6 +329,23 @@ __device__ __forceinline__ unsigned long long match_bin(unsigned b, bool valid, 
     return valid ? peers : 0ull;
 }
 
+// match_bin with the bit count at compile time (NBITS > 0: unrolled).
+template <int NBITS>
+__device__ __forceinline__ unsigned long long match_bin_t(unsigned b, bool valid, int nbits) {
+    if constexpr (NBITS == 0) {
+        return match_bin(b, valid, nbits);
+    } else {
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int i = 0; i < NBITS; ++i) {
+            const bool bit = (b >> i) & 1u;
+            const unsigned long long m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        return valid ? peers : 0ull;
+    }
+}
+
 __device__ __forceinline__ int rank_in(unsigned long long peers) {
     const unsigned lo = (unsigned)peers, hi = (unsigned)(peers >> 32);
     return __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
