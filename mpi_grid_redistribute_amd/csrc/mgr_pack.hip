@@ -1000,7 +1000,12 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // <= 64 bins: 1024 rows (64 bins: pack 0.92 vs 1.07 ms at 512: longer
     // same-bin runs); more bins: longer tiles keep the [nbins][tiles]
     // histogram small next to the payload.
-    if (nbins <= 16) return 512;
+    // rows the image pack takes (4-byte, not 16-byte multiples, 24..60 B, e.g.
+    // config 5's 36-B records): 1024-row tiles (2 rounds x 8 waves per image
+    // workgroup; A/B at 36 B: bin 0.382 vs 0.418, scan 0.014 vs 0.023, pack
+    // 0.850 vs 0.856 ms per 64M)
+    const bool img = row_bytes % 4 == 0 && row_bytes % 16 != 0 && row_bytes >= 24 && row_bytes <= 60;
+    if (nbins <= 16) return img && g_tune.img_rpw == 2 ? 1024 : 512;
     if (nbins <= 64) return 1024;
     // sorted-image pack: 2048-row tiles (its LDS image), rows of 4-byte multiples
     if (g_tune.pack_fine && nbins <= 1024 && row_bytes <= 64 && row_bytes % 4 == 0)
