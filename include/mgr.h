@@ -115,13 +115,14 @@ int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int6
 int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* pos, int pos_dtype,
                        int64_t n, int64_t row_stride, int periodic, void* dest,
                        uint16_t* fine_ids, int tile_rows, void* workspace, void* stream);
-/* Tile histogram of n uint16 bin ids (< nbins) for
- * mgr_scan.  The ids are the destination array of the following mgr_pack
- * when mgr_dest_bytes(nbins) == 2; for <= 256 bins they are also written as
- * bytes to dest (n bytes), the array mgr_pack then takes (dest is unused,
- * may be NULL, above 256 bins).                                            */
+/* Tile histogram of n uint16 bin ids (< nbins) for mgr_scan, and the ids as
+ * the destination array of the following mgr_pack (dest: n entries of
+ * mgr_dest_bytes(nbins) bytes).  An id >= nbins (e.g. of another fine grid)
+ * is clamped to nbins - 1 -- no table is indexed out of range -- and sets
+ * *bad_ids nonzero (bad_ids: a caller-zeroed device word, or NULL); the
+ * caller then treats the counts as failed (-1), like a failed scan.        */
 int mgr_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, void* dest,
-                  void* workspace, void* stream);
+                  uint32_t* bad_ids, void* workspace, void* stream);
 
 /* redist.py:169-198 (redistribute_by_cell_number): caller-supplied rank
  * ids (MGR_I32/MGR_I64/MGR_F32/MGR_F64); ids outside [0, nbins) -- and
@@ -191,7 +192,7 @@ int mgr_pack_ids(const void* src, int64_t row_bytes, int64_t n, const void* dest
  * when the ranked path does not take these rows.                          */
 int mgr_ranked_tile_rows(int64_t row_bytes, int nbins);
 int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint16_t* ranks,
-                 uint16_t* tile_starts, void* workspace, void* stream);
+                 uint16_t* tile_starts, uint32_t* bad_ids, void* workspace, void* stream);
 int mgr_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
                     const uint16_t* ranks, const uint16_t* tile_starts, int nbins, int tile_rows,
                     const void* workspace, void* dst, void* stream);

@@ -38,8 +38,8 @@ SIGNATURES = {
     "mgr_dest_bytes": (_I, [_I]),
     "mgr_bin_count": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I, _P, _P]),
     "mgr_bin_count_fine": (_I, [_P, _P, _P, _I, _I64, _I64, _I, _P, _P, _I, _P, _P]),
-    "mgr_count_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P]),
-    "mgr_rank_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P, _P]),
+    "mgr_count_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P, _P]),
+    "mgr_rank_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P, _P, _P]),
     "mgr_pack_ranked": (_I, [_P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, _P]),
     "mgr_cell_ids": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P]),
     "mgr_bin_ids": (_I, [_P, _P, _I, _I64, _P, _I, _P, _P]),
@@ -122,10 +122,6 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
-        # MGR_TUNE="key=value,..." (A/B measurement of kernel variants)
-        for kv in filter(None, os.environ.get("MGR_TUNE", "").split(",")):
-            k, v = kv.split("=")
-            check(lib.mgr_tune(k.strip().encode(), int(v)), f"MGR_TUNE {kv}")
     return _lib
 
 

@@ -51,13 +51,66 @@ def row_exchange_arrays(size, row_bytes, send_counts, send_offsets, recv_counts,
             arr(send_offsets), arr(recv_counts), arr(recv_offsets), 1)
 
 
+class Traffic:
+    """Bytes one rank moved to and received from OTHER ranks (its xGMI traffic):
+    per peer and direction, from the exchange's real layout -- every field's
+    rows (side fields included), the count messages and the halo's
+    point-to-point messages.  Messages to self never leave the GPU and are
+    not counted."""
+
+    def __init__(self, size, rank):
+        self.rank = int(rank)
+        self.send = np.zeros(int(size), dtype=np.int64)
+        self.recv = np.zeros(int(size), dtype=np.int64)
+
+    def add(self, kind, peer, nbytes):
+        peer, nbytes = int(peer), int(nbytes)
+        if peer == self.rank or nbytes <= 0:
+            return
+        (self.send if kind == "send" else self.recv)[peer] += nbytes
+
+    def add_rows(self, row_bytes, send_counts, recv_counts):
+        """One row exchange: send_counts[p] / recv_counts[p] rows of every
+        field (row_bytes[f] bytes each) to / from peer p."""
+        rb = int(sum(int(x) for x in row_bytes))
+        for p in range(len(self.send)):
+            self.add("send", p, int(send_counts[p]) * rb)
+            self.add("recv", p, int(recv_counts[p]) * rb)
+
+    def as_dict(self):
+        return {"send_bytes": int(self.send.sum()), "recv_bytes": int(self.recv.sum()),
+                "send_peers": int((self.send > 0).sum()), "recv_peers": int((self.recv > 0).sum()),
+                "send_per_peer": self.send.tolist(), "recv_per_peer": self.recv.tolist()}
+
+
 class Transport:
     """Interface.  ``skips_self`` True means the transport never touches the
-    self segment, so the pack may write it straight into the output."""
+    self segment, so the pack may write it straight into the output.
+    ``traffic`` accumulates the off-rank bytes since the last
+    ``reset_traffic()`` (MPIGridRedistributor resets it per call)."""
 
     rank = 0
     size = 1
     skips_self = True
+    traffic = None
+
+    def reset_traffic(self):
+        self.traffic = Traffic(self.size, self.rank)
+        return self.traffic
+
+    def note(self, kind, peer, nbytes):
+        if self.traffic is None:
+            self.reset_traffic()
+        self.traffic.add(kind, peer, nbytes)
+
+    def note_rows(self, row_bytes, send_counts, recv_counts):
+        if self.traffic is None:
+            self.reset_traffic()
+        self.traffic.add_rows(row_bytes, send_counts, recv_counts)
+
+    def note_p2p(self, ops):
+        for k, p, t in ops:
+            self.note(k, p, t.numel())
 
     def Get_rank(self):  # mpi4py duck type (redist.py:41)
         return self.rank

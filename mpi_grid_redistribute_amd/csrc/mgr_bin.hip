@@ -375,12 +375,17 @@ hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, in
 // destination-major counts[b * T + tile] for mgr_scan; the ids themselves
 // are the pack's destination array (<= 256 bins: copied to the 1-byte
 // destination array dest8 the pack then reads).
+// Ids >= nbins (the caller's, e.g. of another fine grid) are clamped to
+// nbins - 1 -- every table index stays in range -- and reported through
+// *bad (nonzero), which the host turns into a raised error / -1 counts.
+template <typename DestT>
 __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __restrict__ ids,
                                                            int64_t n, int nbins,
                                                            int32_t* __restrict__ counts, int64_t T,
                                                            int tile_rows,
                                                            uint64_t* __restrict__ scan_flags,
-                                                           uint8_t* __restrict__ dest8) {
+                                                           DestT* __restrict__ dest,
+                                                           uint32_t* __restrict__ bad) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     int32_t* hist = (int32_t*)smem;
     clear_scan_flags(scan_flags);
@@ -391,11 +396,14 @@ __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __res
     __syncthreads();
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
+    bool oob = false;
     for (int i = threadIdx.x; i < rows; i += kBlock) {
-        const unsigned v = ids[row0 + i];
+        unsigned v = ids[row0 + i];
+        if (v >= (unsigned)nbins) { v = nbins - 1; oob = true; }
         atomicAdd(&hist[v], 1);
-        if (dest8) dest8[row0 + i] = (uint8_t)v;
+        dest[row0 + i] = (DestT)v;
     }
+    if (__any(oob) && lane_id() == 0 && bad) atomicOr(bad, 1u);
     __syncthreads();
     for (int b = threadIdx.x; b < nbins; b += kBlock) counts[(int64_t)b * T + tile] = hist[b];
 }
@@ -410,12 +418,18 @@ __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __res
 // RPW > 0 / NBITS > 0: the rounds per wave and the id bits at compile time
 // (the ranked tiles of mgr_ranked_tile_rows, 512 cells): unrolled rounds in
 // named registers and an unrolled ballot match; 0: read at run time.
-template <int NW, int RPW, int NBITS>
+// HALF (4 waves, 4096-row tiles): ranks and starts per half tile (waves 0-1
+// = rows 0..2047, waves 2-3 = rows 2048..4095) for the half-tile pack
+// (pack_ranked_half_kernel): a row's rank among its half's rows of its bin,
+// and per half h and bin b one uint32 hinfo[2 tile + h][b] = (start of b in
+// the half's sorted image) | (rows of b in the earlier half) << 16.  The
+// tile histogram for mgr_scan is the same.
+template <int NW, int RPW, int NBITS, bool HALF = false>
 __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     const uint16_t* __restrict__ ids, int64_t n, int nbins, int nbits,
     int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ ranks,
     uint16_t* __restrict__ tile_starts, uint8_t* __restrict__ dest8,
-    uint64_t* __restrict__ scan_flags) {
+    uint64_t* __restrict__ scan_flags, uint32_t* __restrict__ bad) {
     constexpr int NT = NW * 64, RPW_MAX = RPW > 0 ? RPW : 4096 / 64 / NW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint16_t* wt = (uint16_t*)smem;   // [NW][nbins]
@@ -426,12 +440,19 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     const int rpw = RPW > 0 ? RPW : tile_rows / 64 / NW;
     for (int i = tid; i < NW * nbins; i += NT) wt[i] = 0;
     unsigned b[RPW_MAX];
+    bool oob = false;   // ids >= nbins: clamped, reported through *bad
 #pragma unroll
     for (int q = 0; q < RPW_MAX; ++q) {
         if (RPW == 0 && q >= rpw) break;
         const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
         b[q] = row < n ? (unsigned)ids[row] : 0u;
     }
+#pragma unroll
+    for (int q = 0; q < RPW_MAX; ++q) {
+        if (RPW == 0 && q >= rpw) break;
+        if (b[q] >= (unsigned)nbins) { b[q] = nbins - 1; oob = true; }
+    }
+    if (__any(oob) && lane == 0 && bad) atomicOr(bad, 1u);
     __syncthreads();
     int rk[RPW_MAX];
 #pragma unroll
@@ -454,17 +475,29 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     int carry = 0;
     for (int k = 0; k * NT < nbins; ++k) {
         const int bb = k * NT + tid;
-        int run = 0;
+        int run = 0;   // HALF: the two halves' counts packed (each <= 2048)
+        int c0h = 0;
         if (bb < nbins) {
             int c[NW];
 #pragma unroll
             for (int ww = 0; ww < NW; ++ww) c[ww] = wt[ww * nbins + bb];
+            if constexpr (HALF) {
+                static_assert(NW == 4, "half tiles: waves 0-1 and 2-3");
+                wt[0 * nbins + bb] = 0;
+                wt[1 * nbins + bb] = (uint16_t)c[0];
+                wt[2 * nbins + bb] = 0;
+                wt[3 * nbins + bb] = (uint16_t)c[2];
+                c0h = c[0] + c[1];
+                run = c0h | ((c[2] + c[3]) << 16);
+                counts[(int64_t)bb * T + tile] = c0h + c[2] + c[3];
+            } else {
 #pragma unroll
-            for (int ww = 0; ww < NW; ++ww) {
-                wt[ww * nbins + bb] = (uint16_t)run;
-                run += c[ww];
+                for (int ww = 0; ww < NW; ++ww) {
+                    wt[ww * nbins + bb] = (uint16_t)run;
+                    run += c[ww];
+                }
+                counts[(int64_t)bb * T + tile] = run;
             }
-            counts[(int64_t)bb * T + tile] = run;
         }
         int incl = run;
 #pragma unroll
@@ -481,7 +514,16 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
             wpre += ww < w ? x : 0;
             wall += x;
         }
-        if (bb < nbins) tile_starts[tile * nbins + bb] = (uint16_t)(carry + wpre + incl - run);
+        if constexpr (HALF) {
+            const unsigned p = (unsigned)(carry + wpre + incl - run);
+            uint32_t* hinfo = (uint32_t*)tile_starts;
+            if (bb < nbins) {
+                hinfo[(2 * tile) * nbins + bb] = p & 0xFFFFu;
+                hinfo[(2 * tile + 1) * nbins + bb] = (p >> 16) | ((unsigned)c0h << 16);
+            }
+        } else {
+            if (bb < nbins) tile_starts[tile * nbins + bb] = (uint16_t)(carry + wpre + incl - run);
+        }
         carry += wall;
         __syncthreads();
     }
@@ -495,7 +537,7 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
 
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                            const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
-                           uint8_t* dest8, hipStream_t s) {
+                           uint8_t* dest8, uint32_t* bad, hipStream_t s, bool half) {
     if (n <= 0) return hipSuccess;
     prof_begin(s, K_COUNT_IDS);
     // 4 waves (16 waves measured 0.57 vs 0.31 ms at 64M rows, 512 bins)
@@ -505,22 +547,32 @@ hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_r
     auto k = tile_rows == 4096 ? (b9 ? rank_ids_kernel<kWaves, 16, 9> : rank_ids_kernel<kWaves, 16, 0>)
            : tile_rows == 2048 ? (b9 ? rank_ids_kernel<kWaves, 8, 9> : rank_ids_kernel<kWaves, 8, 0>)
                                : rank_ids_kernel<kWaves, 0, 0>;
+    if (half) {
+        if (tile_rows != 4096) return hipErrorNotSupported;
+        k = b9 ? rank_ids_kernel<kWaves, 16, 9, true> : rank_ids_kernel<kWaves, 16, 0, true>;
+    }
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s, ids, n, nbins,
                        nbits_for(nbins), ws.counts, ws.T, tile_rows, ranks, tile_starts, dest8,
-                       ws.flags);
+                       ws.flags, bad);
     prof_end(s, K_COUNT_IDS);
     return hipGetLastError();
 }
 
 hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
-                            const Workspace& ws, uint8_t* dest8, hipStream_t s) {
+                            const Workspace& ws, void* dest, uint32_t* bad, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     prof_begin(s, K_COUNT_IDS);
     const int lds = align16(nbins * 4);
-    ensure_lds(count_ids_kernel, lds);
-    hipLaunchKernelGGL(count_ids_kernel, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lds, s, ids, n,
-                       nbins, ws.counts, ws.T, tile_rows, ws.flags, dest8);
+    if (dest_bytes(nbins) == 1) {
+        ensure_lds(count_ids_kernel<uint8_t>, lds);
+        hipLaunchKernelGGL(count_ids_kernel<uint8_t>, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lds,
+                           s, ids, n, nbins, ws.counts, ws.T, tile_rows, ws.flags, (uint8_t*)dest, bad);
+    } else {
+        ensure_lds(count_ids_kernel<uint16_t>, lds);
+        hipLaunchKernelGGL(count_ids_kernel<uint16_t>, dim3((unsigned)ws.T), dim3(kBlock), (size_t)lds,
+                           s, ids, n, nbins, ws.counts, ws.T, tile_rows, ws.flags, (uint16_t*)dest, bad);
+    }
     prof_end(s, K_COUNT_IDS);
     return hipGetLastError();
 }

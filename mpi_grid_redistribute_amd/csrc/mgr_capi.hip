@@ -372,23 +372,19 @@ int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* ro
 }
 
 int mgr_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, void* dest,
-                  void* workspace, void* stream) {
+                  uint32_t* bad_ids, void* workspace, void* stream) {
     int rc = check_tile(tile_rows);
     if (rc) return rc;
     if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
-    if (n > 0 && (!ids || !workspace)) return fail(MGR_EINVAL, "null argument");
-    if (n > 0 && mgr::dest_bytes(nbins) == 1 && !dest)
-        return fail(MGR_EINVAL, "%d bins: the 1-byte destination array is required", nbins);
+    if (n > 0 && (!ids || !workspace || !dest)) return fail(MGR_EINVAL, "null argument");
     const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
-    HIP_OK(mgr::launch_count_ids(ids, n, nbins, tile_rows, ws,
-                                 mgr::dest_bytes(nbins) == 1 ? (uint8_t*)dest : nullptr,
-                                 (hipStream_t)stream));
+    HIP_OK(mgr::launch_count_ids(ids, n, nbins, tile_rows, ws, dest, bad_ids, (hipStream_t)stream));
     return MGR_OK;
 }
 
 int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint16_t* ranks,
-                 uint16_t* tile_starts, void* workspace, void* stream) {
+                 uint16_t* tile_starts, uint32_t* bad_ids, void* workspace, void* stream) {
     int rc = check_tile(tile_rows);
     if (rc) return rc;
     if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
@@ -397,8 +393,8 @@ int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint1
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (n > 0 && (!ids || !ranks || !tile_starts || !workspace)) return fail(MGR_EINVAL, "null argument");
     const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
-    HIP_OK(mgr::launch_rank_ids(ids, n, nbins, tile_rows, ws, ranks, tile_starts, nullptr,
-                                (hipStream_t)stream));
+    HIP_OK(mgr::launch_rank_ids(ids, n, nbins, tile_rows, ws, ranks, tile_starts, nullptr, bad_ids,
+                                (hipStream_t)stream, mgr::ranked_half(nbins, tile_rows, n)));
     return MGR_OK;
 }
 
@@ -773,6 +769,9 @@ int mgr_tune(const char* key, int64_t value) {
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
+    else if (!strcmp(key, "ranked_rows")) mgr::g_tune.ranked_rows = (int)value;
+    else if (!strcmp(key, "ranked_walk")) mgr::g_tune.ranked_walk = (int)value;
+    else if (!strcmp(key, "ranked_ko")) mgr::g_tune.ranked_ko = (int)value;
     else if (!strcmp(key, "img_rpw")) {
         if (value != 1 && value != 2) return fail(MGR_EINVAL, "img_rpw %lld (1 or 2)", (long long)value);
         mgr::g_tune.img_rpw = (int)value;
@@ -791,7 +790,6 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
     else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
     else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
-    else if (!strcmp(key, "pack_fine")) mgr::g_tune.pack_fine = (int)value;
     else if (!strcmp(key, "pack_img")) mgr::g_tune.pack_img = (int)value;
     else if (!strcmp(key, "pack_sel")) mgr::g_tune.pack_sel = (int)value;
     else if (!strcmp(key, "pack_compact")) mgr::g_tune.pack_compact = (int)value;

@@ -569,6 +569,17 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t T) {
     return bid;
 }
 
+// xcd_tile in chunks of C tiles: XCD label x takes chunk x of every group of
+// 8 C consecutive tiles, so all XCDs stream through one region of the input
+// at a time (C <= 1: xcd_tile's one run per XCD).
+__device__ __forceinline__ int64_t xcd_tile_c(int64_t bid, int64_t T, int C) {
+    if (C <= 1) return xcd_tile(bid, T);
+    const int64_t g = 8 * (int64_t)C;
+    if (bid >= (T / g) * g) return bid;
+    const int64_t within = bid % g;
+    return bid - within + (within & 7) * C + (within >> 3);
+}
+
 // Streaming accesses: NT selects the nontemporal (nt) cache policy for data
 // that is read or written exactly once.
 template <bool NT, typename T>

@@ -102,10 +102,12 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
                             int64_t n, const uint16_t* flags, int nsets, const int* bits,
                             int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s);
 hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
-                            const Workspace& ws, uint8_t* dest8, hipStream_t s);
+                            const Workspace& ws, void* dest, uint32_t* bad, hipStream_t s);
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                            const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
-                           uint8_t* dest8, hipStream_t s);
+                           uint8_t* dest8, uint32_t* bad, hipStream_t s, bool half);
+// the ranked sort takes half tiles (rank_ids HALF + pack_ranked_half_kernel)
+bool ranked_half(int nbins, int tile_rows, int64_t n);
 hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
                               const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
                               int tile_rows, const Workspace& ws, void* dst, hipStream_t s);
@@ -138,8 +140,7 @@ struct Tune {
     int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
     int bin_skip_clean = 1;  // write a position slab back only if a row changed
     int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
-    int xcd_pack = 1;      // ... in the pack kernels
-    int pack_fine = 1;     // sorted-image pack for 65..1024 bins (4-byte-multiple rows)
+    int xcd_pack = 16;     // ... in the pack kernels: tiles dealt in chunks of 16 per XCD (1: one run per XCD)
     int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
     int bin_waves = 0;     // waves per bin workgroup (1..16; a tile's rounds split over them; 0: auto)
     int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
@@ -152,6 +153,9 @@ struct Tune {
                                  // (-1: give up at once -- tests of the error path)
     int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
     int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
+    int ranked_rows = 0;   // ranked pack: 0 16-byte units, 1 row-wise read-back, 2 units, unrolled
+    int ranked_ko = 0;     // A/B knockouts of the ranked pack (timing only, wrong output)
+    int ranked_walk = 0;   // ranked pack tile walk: 0 one region per XCD, 1 all XCDs in one region
     int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096
     int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)
     int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)

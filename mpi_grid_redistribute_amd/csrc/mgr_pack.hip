@@ -96,7 +96,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kCoopMaxRounds][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t tile = xcd ? xcd_tile_c(blockIdx.x, T, xcd) : (int64_t)blockIdx.x;
     // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
     const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
     // issue every load of the wave's rounds first
@@ -490,7 +490,7 @@ typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Store through an address held as an integer: a global-address-space
 // pointer, so the compiler emits global_store (a plain pointer would be flat).
 template <typename T>
-__device__ __forceinline__ void gstore(unsigned long long a, const T& v) {
+__device__ __forceinline__ void gstore(unsigned long long a, T v) {
     *(__attribute__((address_space(1))) T*)a = v;
 }
 
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     unsigned long long* gaddr = (unsigned long long*)(img + RBYTES);
     uint8_t* ibin = img + RBYTES + 64 * 8;
     uint32_t* imgw = (uint32_t*)img;
-    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t tile = xcd ? xcd_tile_c(blockIdx.x, T, xcd) : (int64_t)blockIdx.x;
     const int64_t row0 = tile * (int64_t)tile_rows + (int64_t)WR * w;
     const int nrows = (int)max((int64_t)0, min((int64_t)WR, n - row0));
     const int nbytes = nrows * RB;
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     long long* s_off = (long long*)smem;                       // [nb] running bin bases
     uint16_t* tab = (uint16_t*)(smem + align16(nb * 8));       // [R][nb]
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = xcd ? xcd_tile(blockIdx.x, T) : (int64_t)blockIdx.x;
+    const int64_t tile = xcd ? xcd_tile_c(blockIdx.x, T, xcd) : (int64_t)blockIdx.x;
     if (scan_failed(scan_err)) return;
     for (int bb = threadIdx.x; bb < nb; bb += blockDim.x)
         s_off[bb] = seg_start(offsets, bin_starts, T, tile, bb, redirect_bin);
@@ -755,28 +755,10 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     }
 }
 
-// Sorted-image pack for many destinations (65..1024 bins: the 512 fine cells
-// of config 5) and rows of RB bytes (a 4-byte multiple <= 64).
-//
-// Why: with hundreds of bins a round's 64 rows go to ~60 places, so a pack
-// that stores each round straight to its slots (pack_many_kernel) issues
-// store instructions whose 64 lanes touch ~60 different cache lines -- the
-// address pipeline, not HBM, bounds it, and runs of ~4 rows leave
-// half-written lines behind.  Here a workgroup sorts its whole tile by bin
-// in LDS first (stable: wave-private running counts per bin, a prefix over
-// the waves, a scan over the bins) and then streams the sorted image out in
-// 16-byte units, so one store instruction writes 1 KiB of a few contiguous
-// runs.  Persistent: one 1024-thread workgroup per CU (the image fills most
-// of the LDS) walks its XCD's tiles, the 32 workgroups of an XCD on 32
-// adjacent tiles at a time (the lines their runs share meet in one L2), and
-// the next tile's rows are loaded into registers while the current image is
-// stored.
-//
-// LDS: image [TR * RB] | bin of every image row u16 [TR] | wave-private
-// counts u16 [16][nb] | per-bin output base (u64) [nb] | tile bin start [nb].
 typedef unsigned int u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
 typedef unsigned int u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 
+// One row of NDW dwords (4-byte aligned) into registers: 16-byte loads and a tail.
 template <int NDW>
 __device__ __forceinline__ void load_row_dw(const uint8_t* __restrict__ p, uint32_t (&v)[NDW]) {
     int i = 0;
@@ -796,187 +778,20 @@ __device__ __forceinline__ void load_row_dw(const uint8_t* __restrict__ p, uint3
     }
 }
 
-constexpr int kFineTR = 2048;      // rows per tile (32 rounds)
-constexpr int kFineWaves = 16;     // 1024 threads, 2 rounds per wave
-static int fine_tile_rows() { return kFineTR; }
-
-__host__ __device__ inline int fine_lds_bytes(int rb, int nb) {
-    return align16(kFineTR * rb) + align16(kFineTR * 2) + align16(kFineWaves * nb * 2) + nb * 8 +
-           nb * 4;
-}
-
-template <int RB, typename DestT>
-__global__ __launch_bounds__(1024) void pack_fine_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const DestT* __restrict__ dest, int nb,
-    int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, const uint32_t* __restrict__ scan_err) {
-    static_assert(RB % 4 == 0 && RB <= 64, "fine pack row size");
-    constexpr int TR = kFineTR, NW = kFineWaves, RPW = TR / 64 / NW;
-    constexpr int NDW = RB / 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* img = (uint32_t*)smem;
-    uint8_t* p = smem + align16(TR * RB);
-    uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
-    uint16_t* wtab = (uint16_t*)p;                 p += align16(NW * nb * 2);
-    unsigned long long* gaddr = (unsigned long long*)p;  p += nb * 8;
-    int* lstart = (int*)p;
-    __shared__ int s_wsum[NW];
-    if (scan_failed(scan_err)) return;
-    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    // this workgroup's tiles: XCD x = blockIdx % 8 owns tiles [x*per, (x+1)*per);
-    // its G/8 workgroups take them G/8 at a time, adjacent ones together
-    const int64_t per = (T + 7) >> 3;
-    const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3);
-    const int64_t first = (int64_t)(blockIdx.x & 7) * per, last = min(T, first + per);
-    // thread tid < nb owns bin tid: its base correction for the redirect
-    // (tile-independent, seg_start) and its output buffer
-    const int mb = min(tid, nb - 1);
-    long long adj = 0;
-    if (redirect_bin >= 0) {
-        if (mb == redirect_bin) adj = bin_starts[mb];
-        else if (mb > redirect_bin) adj = bin_starts[redirect_bin + 1] - bin_starts[redirect_bin];
-    }
-    uint8_t* const obase = mb == redirect_bin ? redirect_dst : dst;
-    for (int i = tid; i < NW * nb; i += 1024) wtab[i] = 0;
-
-    // Everything a tile needs from HBM -- its rows, their bins, the tile's
-    // segment start of bin tid -- in one register set; two sets, so the next
-    // tile's loads are in flight a whole tile ahead.  The loads are
-    // unconditional (row index clamped to the last row, tile to the last
-    // tile): no loaded register is merged across a branch, which would make
-    // the compiler wait for it (and every older store) on the spot.
-    struct Set {
-        uint32_t v[RPW][NDW];
-        unsigned b[RPW];
-        long long seg;
-    };
-    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
-        t = min(t, last - 1);
-        S.seg = offsets[(int64_t)mb * T + t];
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
-            S.b[q] = (unsigned)dest[row];
-            load_row_dw<NDW>(src + row * RB, S.v[q]);
-        }
-    };
-    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
-        const int tr = (int)min((int64_t)TR, n - t * TR);   // rows of this tile
-        // 1. wave-private running counts (wtab zeroed at the end of the last
-        //    tile): a row's rank among its wave's rows of its bin
-        int lr[RPW];
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const bool valid = (w * RPW + q) * 64 + lane < tr;
-            const unsigned long long peers = match_bin(S.b[q], valid, nbits);
-            const int rk = rank_in(peers);
-            const int before = valid ? (int)wtab[w * nb + S.b[q]] : 0;
-            wave_sync();
-            if (valid && rk == 0) wtab[w * nb + S.b[q]] = (uint16_t)(before + __popcll(peers));
-            wave_sync();
-            lr[q] = before + rk;
-        }
-        __syncthreads();
-        // 2. per bin: exclusive prefix over the waves (the 16 counts read
-        //    first: independent LDS reads), then the bins' starts in the tile
-        int total = 0;
-        if (tid < nb) {
-#pragma unroll
-            for (int w0 = 0; w0 < NW; w0 += 4) {
-                int c[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) c[k] = wtab[(w0 + k) * nb + tid];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    wtab[(w0 + k) * nb + tid] = (uint16_t)total;
-                    total += c[k];
-                }
-            }
-        }
-        int incl = total;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63) s_wsum[w] = incl;
-        __syncthreads();
-        int wpre = 0;
-#pragma unroll
-        for (int ww = 0; ww < NW; ++ww) wpre += ww < w ? s_wsum[ww] : 0;
-        if (tid < nb) {
-            const int ls = wpre + incl - total;
-            lstart[tid] = ls;
-            gaddr[tid] = tid == drop_bin
-                             ? 0ull
-                             : (unsigned long long)(obase + (S.seg - adj - ls) * (long long)RB);
-        }
-        __syncthreads();
-        // 3. rows into the sorted image
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            if ((w * RPW + q) * 64 + lane < tr) {
-                const int lpos = lstart[S.b[q]] + wtab[w * nb + S.b[q]] + lr[q];
-#pragma unroll
-                for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
-                ibin[lpos] = (uint16_t)S.b[q];
-            }
-        }
-        __syncthreads();
-        // 4. stream the image out in 16-byte units; zero the counts for the
-        //    next tile on the way
-        for (int i = tid; i < NW * nb; i += 1024) wtab[i] = 0;
-        const int nbytes = tr * RB;
-        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
-            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
-            const int bf = ibin[x / RB];
-            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
-                const unsigned long long a = gaddr[bf];
-                if (a) gstore<u32x4_a4>(a + x, q);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    if (xd < nbytes) {
-                        const unsigned long long a = gaddr[ibin[xd / RB]];
-                        if (a) gstore<uint32_t>(a + xd, q[d]);
-                    }
-                }
-            }
-        }
-        __syncthreads();   // the image, ibin and gaddr are reused by the next tile
-    };
-    Set A, B;
-    int64_t t = first + kx;
-    if (t >= last) return;
-    load(A, t);
-    __syncthreads();   // wtab zeroed
-    for (;;) {
-        load(B, t + gx);
-        process(A, t);
-        t += gx;
-        if (t >= last) break;
-        load(A, t + gx);
-        process(B, t);
-        t += gx;
-        if (t >= last) break;
-    }
-}
+constexpr int kFineTR = 2048;      // ranked tiles when a 4096-row image does not fit
+constexpr int kFineWaves = 16;     // ranked pack: 1024 threads
 
 // ============================================================ launchers
-// The 2-byte side field of the pack in progress (mgr_pack_ids: the fine
-// cells travelling with config-5 rows).  launch_pack sets it for the
-// duration of one call on the calling thread; the coop and image launchers
-// take it into their kernel and mark it consumed, other paths leave it to a
-// second (2-byte-row) pack.
+// The 2-byte side field of a pack (mgr_pack_ids: the fine cells or halo
+// flags travelling with the rows), handed down the launchers explicitly
+// (NULL: none).  The coop and image launchers take it into their kernel and
+// mark it used; other paths leave it to a second (2-byte-row) pack.
 struct SideField {
     const uint16_t* src = nullptr;
     uint16_t* dst = nullptr;
     uint16_t* red = nullptr;
     bool used = false;
 };
-static thread_local SideField t_side;
 
 // pack_many_kernel: super-rounds of 64 * R rows (the uint16 [R][nbins] LDS
 // table stays <= 128 KiB at 4096 rows and 1024 bins), many_super super-rounds
@@ -1007,9 +822,6 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     const bool img = row_bytes % 4 == 0 && row_bytes % 16 != 0 && row_bytes >= 24 && row_bytes <= 60;
     if (nbins <= 16) return img && g_tune.img_rpw == 2 ? 1024 : 512;
     if (nbins <= 64) return 1024;
-    // sorted-image pack: 2048-row tiles (its LDS image), rows of 4-byte multiples
-    if (g_tune.pack_fine && nbins <= 1024 && row_bytes <= 64 && row_bytes % 4 == 0)
-        return fine_tile_rows();
     if (g_tune.pack_many && nbins <= 1024 && row_bytes <= 64) return many_tile_rows(nbins);
     int r = 16;
     while (r < 4096 / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
@@ -1036,7 +848,7 @@ static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const vo
 template <int W, int UPR>
 static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
-                              void* redirect_dst, hipStream_t s) {
+                              void* redirect_dst, hipStream_t s, SideField* side) {
     if (!g_tune.pack_coop || tile_rows > 2048) return hipErrorNotSupported;
     // one wave per RPW 64-row rounds of the tile (<= 16 waves)
     const int rpw = tile_rows > 1024 ? 2 : 1;
@@ -1046,11 +858,12 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
                        s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),     \
                        drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,    \
                        redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel, ws.scan_err, \
-                       t_side.src, t_side.dst, t_side.red)
+                       side ? side->src : nullptr, side ? side->dst : nullptr,         \
+                       side ? side->red : nullptr)
     // selection packs (2 bins, one dropped: the halo's rows to send) skip
     // the loads of dropped rows; elsewhere loads go out before the bins are known
     const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
-    t_side.used = t_side.src != nullptr;
+    if (side) side->used = side->src != nullptr;
     if (rpw == 2) MGR_PCK(2); else MGR_PCK(1);
 #undef MGR_PCK
     return hipGetLastError();
@@ -1061,8 +874,9 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
 template <int W>
 static hipError_t pack_coop_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                                int nb, int drop_bin, int tile_rows, const Workspace& ws,
-                               void* dst, int redirect_bin, void* redirect_dst, hipStream_t s) {
-#define MGR_PS(U_) case U_: return pack_coop_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+                               void* dst, int redirect_bin, void* redirect_dst, hipStream_t s,
+                               SideField* side) {
+#define MGR_PS(U_) case U_: return pack_coop_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
     if constexpr (W >= 4) {
         switch ((int)(row_bytes / W)) {
             MGR_PS(1) MGR_PS(2) MGR_PS(3) MGR_PS(4)
@@ -1137,7 +951,7 @@ static hipError_t pack_many_t(const void* src, int64_t row_bytes, int64_t n, con
 template <int RB>
 static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                              int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
-                             void* redirect_dst, hipStream_t s) {
+                             void* redirect_dst, hipStream_t s, SideField* side) {
     // img_rpw 64-row rounds per wave when they divide the tile: 2 (A/B, 36-B
     // records: 0.90-0.92 vs 1.02-1.05 ms per 64M, 4: 1.17 -- a wave's fixed
     // per-round chain of load, count exchange, LDS permutation and store then
@@ -1153,9 +967,10 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s,
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
-                       (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err, t_side.src,
-                       t_side.dst, t_side.red);
-    t_side.used = t_side.src != nullptr;
+                       (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err,
+                       side ? side->src : nullptr, side ? side->dst : nullptr,
+                       side ? side->red : nullptr);
+    if (side) side->used = side->src != nullptr;
     return hipGetLastError();
 }
 
@@ -1171,33 +986,151 @@ static int device_cus() {
     return g_cus;
 }
 
-template <int RB, typename DestT>
-static hipError_t pack_fine_t(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
-                              const Workspace& ws, void* dst, int redirect_bin, void* redirect_dst,
-                              hipStream_t s) {
-    auto k = pack_fine_kernel<RB, DestT>;
-    const int lds = fine_lds_bytes(RB, nb);
-    if (lds > 160 * 1024) return hipErrorNotSupported;
-    ensure_lds(k, lds);
-    // one workgroup per CU (the LDS holds one image), a multiple of 8 (XCDs)
-    int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
-    const int64_t need = (ws.T + 7) / 8 * 8;
-    if (grid > need) grid = need;
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s, (const uint8_t*)src, n,
-                       (const DestT*)dest, nb, nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts,
-                       ws.T, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, ws.scan_err);
-    return hipGetLastError();
+// Ranked sorted-image pack (mgr_pack_ranked), the stable sort of 65..1024
+// bins (config 5's fine cells): every row's rank inside (tile, bin) and every
+// tile's bin starts come from mgr_rank_ids, so a tile is: load (a tile
+// ahead), rows into the LDS image at tile_start[bin] + rank, stream the image
+// out in 16-byte units (a unit inside one bin's run is one 16-byte store to
+// the run's place, a unit straddling two runs goes dword by dword).
+// Persistent: one 1024-thread workgroup per CU (the image fills most of the
+// LDS) walks its XCD's tiles, the workgroups of an XCD on adjacent tiles at a
+// time (the lines their runs share meet in one L2).  No ballots, no per-tile
+// count table, three barriers per tile.
+template <int RB, int TR, bool UNR>
+__global__ __launch_bounds__(1024) void pack_ranked_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
+    const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
+    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err, int walk, int ko) {
+    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
+    constexpr int NW = kFineWaves, RPW = TR / 64 / NW;
+    constexpr int NDW = RB / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* img = (uint32_t*)smem;
+    uint8_t* p = smem + align16(TR * RB);
+    uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
+    unsigned long long* gaddr = (unsigned long long*)p;  p += nb * 8;
+    uint16_t* lstart = (uint16_t*)p;
+    if (scan_failed(scan_err)) return;
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    // tile walk: walk 0 -- XCD x owns tiles [x*per, (x+1)*per), its gx
+    // workgroups on gx adjacent tiles at a time; walk 1 -- all 8 gx
+    // workgroups on 8 gx adjacent tiles at a time (one region of the input)
+    const int64_t per = (T + 7) >> 3;
+    const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3), xx = (int)(blockIdx.x & 7);
+    const int64_t first = walk ? (int64_t)xx * gx + kx : (int64_t)xx * per + kx;
+    const int64_t stride = walk ? 8 * (int64_t)gx : gx;
+    const int64_t last = walk ? T : min(T, (int64_t)xx * per + per);
+    const int mb = min(tid, nb - 1);
+    struct Set {
+        uint32_t v[RPW][NDW];
+        unsigned b[RPW];
+        unsigned rk[RPW];
+        long long seg;
+        unsigned ls;
+    };
+    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        t = min(t, last - 1);
+        S.seg = offsets[(int64_t)mb * T + t];
+        S.ls = tile_starts[t * nb + mb];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
+            S.b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));   // ids >= nb: clamped (mgr_rank_ids reports them)
+            S.rk[q] = ranks[row];
+            load_row_dw<NDW>(src + row * RB, S.v[q]);
+        }
+    };
+    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        const int tr = (int)min((int64_t)TR, n - t * TR);
+        if (tid < nb) {
+            lstart[tid] = (uint16_t)S.ls;
+            gaddr[tid] = (unsigned long long)(dst + (S.seg - (long long)S.ls) * (long long)RB);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            if ((w * RPW + q) * 64 + lane < tr) {
+                const int lpos = lstart[S.b[q]] + S.rk[q];
+                if (ko & 1) {   // A/B knockout 1: rows not written to the image
+                    ibin[lpos] = (uint16_t)S.b[q];
+                    if (S.v[q][0] == 0x9E3779B9u && S.v[q][NDW - 1] == 0x7F4A7C15u) img[lpos * NDW] = 1u;
+                    continue;
+                }
+#pragma unroll
+                for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
+                ibin[lpos] = (uint16_t)S.b[q];
+            }
+        }
+        __syncthreads();
+        const int nbytes = tr * RB;
+        auto unit = [&](int x) __attribute__((always_inline)) {
+            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
+            const int bf = ibin[x / RB];
+            if (ko & 4) return;   // A/B knockout: no stores
+            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+                gstore<u32x4_a4>(gaddr[bf] + x, q);
+            } else if (!(ko & 2)) {   // A/B knockout 2: straddling units not stored
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
+                }
+            }
+        };
+        if constexpr (UNR) {
+            // unrolled: no store loop whose preheader would wait (vmcnt 0)
+            // for the next tile's loads already in flight
+            constexpr int NU = (TR * RB / 16 + 1023) / 1024;
+#pragma unroll
+            for (int k = 0; k < NU; ++k) {
+                int x = 16 * (tid + 1024 * k);
+                asm volatile("" : "+v"(x));   // computed per tile, not hoisted (registers)
+                if (x < nbytes) unit(x);
+            }
+        } else {
+            for (int x = 16 * tid; x < nbytes; x += 16 * 1024) unit(x);
+        }
+        __syncthreads();   // the image, ibin, lstart and gaddr are reused by the next tile
+    };
+    Set A, B;
+    int64_t t = first;
+    if (t >= last) return;
+    load(A, t);
+    for (;;) {
+        load(B, t + stride);
+        process(A, t);
+        t += stride;
+        if (t >= last) break;
+        load(A, t + stride);
+        process(B, t);
+        t += stride;
+        if (t >= last) break;
+    }
 }
 
-// 65..1024 bins, rows of 4-byte multiples <= 64 bytes, every base 4-byte
-// aligned: the sorted-image pack.
-// Ranked sorted-image pack (mgr_pack_ranked): pack_fine_kernel without its
-// ranking -- every row's rank inside (tile, bin) and every tile's bin starts
-// come from mgr_rank_ids -- so a tile is: load (a tile ahead), rows into the
-// LDS image at tile_start[bin] + rank, stream the image out.  No ballots, no
-// per-tile count table, three barriers per tile.
+template <int NDW>
+__device__ __forceinline__ void store_row_dw(unsigned long long a, const uint32_t (&v)[NDW]) {
+    int i = 0;
+#pragma unroll
+    for (; i + 4 <= NDW; i += 4) gstore<u32x4_a4>(a + 4 * i, u32x4_a4{v[i], v[i + 1], v[i + 2], v[i + 3]});
+    if constexpr (NDW % 4 == 3) gstore<u32x3_a4>(a + 4 * i, u32x3_a4{v[i], v[i + 1], v[i + 2]});
+    else if constexpr (NDW % 4 == 2) gstore<u32x2_a4>(a + 4 * i, u32x2_a4{v[i], v[i + 1]});
+    else if constexpr (NDW % 4 == 1) gstore<uint32_t>(a + 4 * i, v[i]);
+}
+
+// Ranked pack, row-wise read-back (round 3).  Same tile walk and LDS image
+// as pack_ranked_kernel, but the image leaves row by row: lane l of a wave
+// takes sorted row j (consecutive j per wave, so a store instruction writes
+// the wave's rows of each run back to back), reads its dwords (stride RB/4,
+// conflict-free), and stores the row whole to obase[bin] + j.  Every access
+// is branch-free: rows past the tile end re-read and re-store the tile's
+// last row (identical bytes to the same place), so each wave issues the
+// same number of stores for every tile and the next tile's loads (issued a
+// tile ahead) stay in flight across them -- no data-dependent dword path,
+// no per-unit run lookups.
 template <int RB, int TR>
-__global__ __launch_bounds__(1024) void pack_ranked_kernel(
+__global__ __launch_bounds__(1024) void pack_ranked_rows_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
     const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
     const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
@@ -1209,7 +1142,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     uint32_t* img = (uint32_t*)smem;
     uint8_t* p = smem + align16(TR * RB);
     uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
-    unsigned long long* gaddr = (unsigned long long*)p;  p += nb * 8;
+    long long* obase = (long long*)p;              p += nb * 8;
     uint16_t* lstart = (uint16_t*)p;
     if (scan_failed(scan_err)) return;
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
@@ -1231,7 +1164,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
             const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
-            S.b[q] = ids[row];
+            S.b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));   // ids >= nb: clamped (mgr_rank_ids reports them)
             S.rk[q] = ranks[row];
             load_row_dw<NDW>(src + row * RB, S.v[q]);
         }
@@ -1240,34 +1173,29 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         const int tr = (int)min((int64_t)TR, n - t * TR);
         if (tid < nb) {
             lstart[tid] = (uint16_t)S.ls;
-            gaddr[tid] = (unsigned long long)(dst + (S.seg - (long long)S.ls) * (long long)RB);
+            obase[tid] = S.seg - (long long)S.ls;
+        }
+        __syncthreads();
+        // rows into the sorted image (rows past n were clamped to row n - 1:
+        // the same bytes to the same slot)
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int lpos = lstart[S.b[q]] + S.rk[q];
+#pragma unroll
+            for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
+            ibin[lpos] = (uint16_t)S.b[q];
         }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
-            if ((w * RPW + q) * 64 + lane < tr) {
-                const int lpos = lstart[S.b[q]] + S.rk[q];
+            const int j = min(w * (64 * RPW) + 64 * q + lane, tr - 1);
+            const long long o = obase[ibin[j]] + j;
+            uint32_t row[NDW];
 #pragma unroll
-                for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
-                ibin[lpos] = (uint16_t)S.b[q];
-            }
+            for (int i = 0; i < NDW; ++i) row[i] = img[j * NDW + i];
+            store_row_dw<NDW>((unsigned long long)(dst + o * RB), row);
         }
-        __syncthreads();
-        const int nbytes = tr * RB;
-        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
-            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
-            const int bf = ibin[x / RB];
-            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
-                gstore<u32x4_a4>(gaddr[bf] + x, q);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
-                }
-            }
-        }
-        __syncthreads();   // the image, ibin, lstart and gaddr are reused by the next tile
+        __syncthreads();   // the image, ibin, lstart and obase are reused by the next tile
     };
     Set A, B;
     int64_t t = first + kx;
@@ -1283,6 +1211,94 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         t += gx;
         if (t >= last) break;
     }
+}
+
+// Half-tile ranked pack (round 3): the 4096-row scan tiles are packed as two
+// independent 2048-row halves (mgr_rank_ids in half mode ranks each half on
+// its own), one 512-thread workgroup per half, not persistent.  A half's
+// LDS (image + bins + tables, <= 80 KiB for rows of <= 36 B) lets two
+// workgroups share a CU, so one streams its rows in while the other stores
+// its image out -- the overlap a single persistent workgroup per CU did not
+// get (its store phase waited for the next tile's loads, profiles/round3).
+// hinfo[half][b] = start of bin b in the half's sorted image | (rows of b in
+// the tile's earlier half) << 16; a row's output = offsets[b][tile] + that
+// count + its rank in the half.
+constexpr int kHalfRows = 2048;
+constexpr int kHalfThreads = 512;
+
+bool ranked_half(int nbins, int tile_rows, int64_t n) {
+    return g_tune.ranked_rows == 3 && tile_rows == 4096 && n < ((int64_t)1 << 31) && nbins <= 1024;
+}
+
+template <int RB>
+__global__ __launch_bounds__(kHalfThreads) void pack_ranked_half_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
+    const uint16_t* __restrict__ ranks, const uint32_t* __restrict__ hinfo, int nb,
+    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err, int xcd) {
+    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
+    constexpr int HR = kHalfRows, NT = kHalfThreads, RPT = HR / NT;   // rows per thread
+    constexpr int NDW = RB / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* img = (uint32_t*)smem;
+    uint8_t* p = smem + align16(HR * RB);
+    uint16_t* ibin = (uint16_t*)p;                 p += align16(HR * 2);
+    int* obase = (int*)p;                          p += align16(nb * 4);
+    uint16_t* lstart = (uint16_t*)p;
+    if (scan_failed(scan_err)) return;
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const int64_t half = xcd ? xcd_tile_c(blockIdx.x, 2 * T, xcd) : (int64_t)blockIdx.x;
+    const int64_t t = half >> 1, row0 = half * HR;
+    if (row0 >= n) return;
+    const int tr = (int)min((int64_t)HR, n - row0);
+    if (tid < nb) {
+        const uint32_t hi = hinfo[half * nb + tid];
+        lstart[tid] = (uint16_t)(hi & 0xFFFFu);
+        obase[tid] = (int)(offsets[(int64_t)tid * T + t] + (long long)(hi >> 16) - (long long)(hi & 0xFFFFu));
+    }
+    unsigned b[RPT], rk[RPT];
+    uint32_t v[RPT][NDW];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        // rows past n: the half's last row again (same bytes to the same slot)
+        const int64_t row = min(row0 + (int64_t)(w * RPT + q) * 64 + lane, n - 1);
+        b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));
+        rk[q] = ranks[row];
+        load_row_dw<NDW>(src + row * RB, v[q]);
+    }
+    for (int i = tid + 512; i < nb; i += NT) {   // > 512 bins
+        const uint32_t hi = hinfo[half * nb + i];
+        lstart[i] = (uint16_t)(hi & 0xFFFFu);
+        obase[i] = (int)(offsets[(int64_t)i * T + t] + (long long)(hi >> 16) - (long long)(hi & 0xFFFFu));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int lpos = lstart[b[q]] + rk[q];
+#pragma unroll
+        for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = v[q][i];
+        ibin[lpos] = (uint16_t)b[q];
+    }
+    __syncthreads();
+    const int nbytes = tr * RB;
+    for (int x = 16 * tid; x < nbytes; x += 16 * NT) {
+        const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
+        const int bf = ibin[x / RB];
+        if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+            gstore<u32x4_a4>((unsigned long long)(dst + (int64_t)obase[bf] * RB + x), q);
+        } else {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int xd = x + 4 * d;
+                if (xd < nbytes)
+                    gstore<uint32_t>((unsigned long long)(dst + (int64_t)obase[ibin[xd / RB]] * RB + xd), q[d]);
+            }
+        }
+    }
+}
+
+static int ranked_half_lds_bytes(int64_t row_bytes, int nbins) {
+    return align16(kHalfRows * (int)row_bytes) + align16(kHalfRows * 2) + align16(nbins * 4) + nbins * 2;
 }
 
 // LDS of the ranked pack: the tile image, its row bins, per-bin output
@@ -1308,6 +1324,29 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if ((tile_rows != kFineTR && tile_rows != 4096) || row_bytes % 4 || row_bytes > 64 ||
         ((uintptr_t)src & 3) || ((uintptr_t)dst & 3))
         return hipErrorNotSupported;
+    if (ranked_half(nbins, tile_rows, n)) {
+        const int hl = ranked_half_lds_bytes(row_bytes, nbins);
+        prof_begin(s, K_PACK_FINE);
+        hipError_t e = hipErrorNotSupported;
+#define MGR_PH(RB_)                                                                           \
+        case RB_: {                                                                           \
+            auto k = pack_ranked_half_kernel<RB_>;                                            \
+            ensure_lds(k, hl);                                                                \
+            hipLaunchKernelGGL(k, dim3((unsigned)(2 * ws.T)), dim3(kHalfThreads), (size_t)hl, s, \
+                               (const uint8_t*)src, n, ids, ranks, (const uint32_t*)tile_starts, \
+                               nbins, ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,           \
+                               g_tune.xcd_pack);                                              \
+            e = hipGetLastError();                                                            \
+        } break;
+        switch ((int)row_bytes) {
+            MGR_PH(4) MGR_PH(8) MGR_PH(12) MGR_PH(16) MGR_PH(20) MGR_PH(24) MGR_PH(28) MGR_PH(32)
+            MGR_PH(36) MGR_PH(40) MGR_PH(44) MGR_PH(48) MGR_PH(52) MGR_PH(56) MGR_PH(60) MGR_PH(64)
+            default: break;
+        }
+#undef MGR_PH
+        prof_end(s, K_PACK_FINE);
+        return e;
+    }
     const int lds = ranked_lds_bytes(tile_rows, row_bytes, nbins);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
@@ -1317,11 +1356,21 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     hipError_t e = hipErrorNotSupported;
 #define MGR_PRT(RB_, TR_)                                                                     \
     {                                                                                         \
-        auto k = pack_ranked_kernel<RB_, TR_>;                                                \
-        ensure_lds(k, lds);                                                                   \
-        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,               \
-                           (const uint8_t*)src, n, ids, ranks, tile_starts, nbins, ws.offsets, \
-                           ws.T, (uint8_t*)dst, ws.scan_err);                                  \
+        if (g_tune.ranked_rows == 1) {                                                        \
+            auto k = pack_ranked_rows_kernel<RB_, TR_>;                                       \
+            ensure_lds(k, lds);                                                               \
+            hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,           \
+                               (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,        \
+                               ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err);                 \
+        } else {                                                                              \
+            auto k = g_tune.ranked_rows == 2 ? pack_ranked_kernel<RB_, TR_, true>             \
+                                             : pack_ranked_kernel<RB_, TR_, false>;           \
+            ensure_lds(k, lds);                                                               \
+            hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,           \
+                               (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,        \
+                               ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,                  \
+                               g_tune.ranked_walk, g_tune.ranked_ko);                         \
+        }                                                                                     \
         e = hipGetLastError();                                                                \
     }
 #define MGR_PR(RB_)                                                                           \
@@ -1347,36 +1396,12 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     return e;
 }
 
-static hipError_t pack_fine(const void* src, int64_t row_bytes, int64_t n, const void* dest,
-                            int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                            int redirect_bin, void* redirect_dst, hipStream_t s) {
-    uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
-    if (redirect_dst) a |= (uintptr_t)redirect_dst;
-    if (!g_tune.pack_fine || nb <= 64 || nb > 1024 || (a & 3) || row_bytes > 64 ||
-        tile_rows != kFineTR)
-        return hipErrorNotSupported;
-    const bool d8 = dest_bytes(nb) == 1;
-#define MGR_PF(RB_)                                                                              \
-    case RB_:                                                                                    \
-        return d8 ? pack_fine_t<RB_, uint8_t>(src, n, dest, nb, drop_bin, ws, dst, redirect_bin, \
-                                              redirect_dst, s)                                   \
-                  : pack_fine_t<RB_, uint16_t>(src, n, dest, nb, drop_bin, ws, dst, redirect_bin, \
-                                               redirect_dst, s);
-    switch ((int)row_bytes) {
-        MGR_PF(4) MGR_PF(8) MGR_PF(12) MGR_PF(16) MGR_PF(20) MGR_PF(24) MGR_PF(28) MGR_PF(32)
-        MGR_PF(36) MGR_PF(40) MGR_PF(44) MGR_PF(48) MGR_PF(52) MGR_PF(56) MGR_PF(60) MGR_PF(64)
-        default: break;
-    }
-#undef MGR_PF
-    return hipErrorNotSupported;
-}
-
 // Rows of 24..60 (pack_img 2: 12..60) bytes, 4-byte multiples but not 16-byte ones: the
 // image pack (16-byte global accesses) when the source is 16-byte aligned,
 // the outputs 4-byte aligned, <= 64 bins and <= 16 waves per tile.
 static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                            int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                           int redirect_bin, void* redirect_dst, hipStream_t s) {
+                           int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side) {
     uintptr_t a = (uintptr_t)dst | (uintptr_t)row_bytes;
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
     // pack_img 1: rows of >= 24 bytes (A/B: 36 B 0.90 vs 1.05 ms, 40 B 0.97 vs
@@ -1387,7 +1412,7 @@ static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const 
         row_bytes < min_rb || row_bytes > 60 || nb > 64 || tile_rows > 1024 ||
         dest_bytes(nb) != 1)
         return hipErrorNotSupported;
-#define MGR_PI(RB_) case RB_: return pack_img_t<RB_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+#define MGR_PI(RB_) case RB_: return pack_img_t<RB_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
     switch ((int)row_bytes) {
         MGR_PI(12) MGR_PI(20) MGR_PI(24) MGR_PI(28) MGR_PI(36) MGR_PI(40) MGR_PI(44)
         MGR_PI(52) MGR_PI(56) MGR_PI(60)
@@ -1400,7 +1425,7 @@ static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const 
 template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                         int redirect_bin, void* redirect_dst, hipStream_t s) {
+                         int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side) {
     if constexpr (W >= 4) {
         if (g_tune.pack_many && nb > 64 && nb <= 1024 && row_bytes <= 64 &&
             tile_rows == many_tile_rows(nb)) {
@@ -1413,13 +1438,13 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
     if constexpr (W == 2) {   // 2-byte rows (the fine cells travelling with config-5 rows)
         if (nb <= 64 && row_bytes == 2) {
             const hipError_t e = pack_coop_u<2, 1>(src, n, dest, nb, drop_bin, tile_rows, ws, dst,
-                                                   redirect_bin, redirect_dst, s);
+                                                   redirect_bin, redirect_dst, s, nullptr);
             if (e != hipErrorNotSupported) return e;
         }
     }
     if (nb <= 64 && row_bytes <= 64 && W >= 4) {
         const hipError_t e = pack_coop_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
-                                             ws, dst, redirect_bin, redirect_dst, s);
+                                             ws, dst, redirect_bin, redirect_dst, s, side);
         if (e != hipErrorNotSupported) return e;
     }
     const bool wide = row_bytes > 256;
@@ -1433,35 +1458,32 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
 static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n,
                                    const void* dest, int nbins, int drop_bin, int tile_rows,
                                    const Workspace& ws, void* dst, int redirect_bin,
-                                   void* redirect_dst, hipStream_t s);
+                                   void* redirect_dst, hipStream_t s, SideField* side);
 
 hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                        int nbins, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                        int redirect_bin, void* redirect_dst, hipStream_t s, const uint16_t* ids_src,
                        uint16_t* ids_dst, uint16_t* ids_red) {
     if (n <= 0) return hipSuccess;
-    t_side = SideField{ids_src, ids_dst, ids_red, false};
+    SideField side{ids_src, ids_dst, ids_red, false};
     hipError_t e = launch_pack_rows(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
-                                    redirect_bin, redirect_dst, s);
-    const bool rest = ids_src && !t_side.used;
-    t_side = SideField{};
+                                    redirect_bin, redirect_dst, s, ids_src ? &side : nullptr);
+    const bool rest = ids_src && !side.used;
     if (e != hipSuccess || !rest) return e;
     // the kernel that moved the rows cannot carry the ids: a 2-byte-row pack
     return launch_pack_rows(ids_src, 2, n, dest, nbins, drop_bin, tile_rows, ws, ids_dst,
-                            redirect_bin, ids_red, s);
+                            redirect_bin, ids_red, s, nullptr);
 }
 
 static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n,
                                    const void* dest, int nbins, int drop_bin, int tile_rows,
                                    const Workspace& ws, void* dst, int redirect_bin,
-                                   void* redirect_dst, hipStream_t s) {
+                                   void* redirect_dst, hipStream_t s, SideField* side) {
     // Widest unit dividing the row and every base address.
     uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)row_bytes;
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
-    // profiler: the many-bin sorted-image pack and narrow (< 4-byte) rows apart
-    const int kid = (g_tune.pack_fine && nbins > 64 && nbins <= 1024 && tile_rows == kFineTR)
-                        ? K_PACK_FINE
-                        : (row_bytes < 4 ? K_PACK_NARROW : K_PACK);
+    // profiler: narrow (< 4-byte) rows apart
+    const int kid = row_bytes < 4 ? K_PACK_NARROW : K_PACK;
     prof_begin(s, kid);
     hipError_t e = hipErrorNotSupported;
     if (g_tune.pack_compact && nbins == 2 && drop_bin == 1 && redirect_bin < 0) {
@@ -1471,20 +1493,17 @@ static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n
         else e = compact_t<1>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
     }
     if (e == hipErrorNotSupported)
-        e = pack_fine(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
-                      redirect_dst, s);
-    if (e == hipErrorNotSupported)
         e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
-                     redirect_dst, s);
+                     redirect_dst, s, side);
     if (e != hipErrorNotSupported) {
         prof_end(s, kid);
         return e;
     }
-    if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
-    else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
+    if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
+    else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
+    else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
+    else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
+    else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
     prof_end(s, kid);
     return e;
 }

@@ -71,6 +71,9 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
     moved by one kernel, e.g. rows with their fine cells).  Returns (outs, layout); outs are new flat uint8
     tensors of (total_recv + extra) * row_bytes[f] bytes (>= 1 byte)."""
     sc, rc = transport.exchange_counts(bin_counts)
+    for p in range(len(sc)):   # the count row: one int64 each way per peer
+        transport.note("send", p, 8)
+        transport.note("recv", p, 8)
     check_counts(sc, rc)
     lay = plan_layout(sc, rc, rank, transport.skips_self)
     extra = int(extra_rows(lay.total_recv)) if extra_rows is not None else 0
@@ -92,4 +95,5 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
             pack(f, sends[f], redirect, outs[f] if lay.redirect_self else None, offs[f])
     transport.exchange_rows(sends, outs, list(row_bytes), sc, lay.send_offsets, rc,
                             lay.recv_offsets)
+    transport.note_rows(row_bytes, sc, rc)
     return outs, lay

@@ -59,6 +59,13 @@ from . import _lib
 from .comm import excl_cumsum
 
 
+def _p2p(transport, ops):
+    """One batch of point-to-point messages, its off-rank bytes counted in
+    the transport's traffic."""
+    transport.note_p2p(ops)
+    transport.p2p(ops)
+
+
 def neighbours(R, d, periodic):
     """Right/left neighbour ranks of R's cell in dimension d and whether each
     side sends (redist.py:248-267, quirk :287 -- the left send's flag is the
@@ -223,7 +230,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                 ("recv", b, recv_l[2 * d:2 * d + 1].view(torch.uint8)),
                 ("send", b, send_l[2 * d + 1:2 * d + 2].view(torch.uint8)),
                 ("recv", a, recv_l[2 * d + 1:2 * d + 2].view(torch.uint8))]
-    transport.p2p(ops)
+    _p2p(transport, ops)
     ls, rl = sel.to_host([send_l, recv_l])                   # host sync 1
 
     # the append-only overload store: data (+ positions) + flags
@@ -314,7 +321,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                 send_g[0].zero_()
             if not keep_b:
                 send_g[1].zero_()
-            transport.p2p([("send", a, send_g[0:1].view(torch.uint8)),
+            _p2p(transport, [("send", a, send_g[0:1].view(torch.uint8)),
                            ("recv", b, recv_g[0:1].view(torch.uint8)),
                            ("send", b, send_g[1:2].view(torch.uint8)),
                            ("recv", a, recv_g[1:2].view(torch.uint8))])
@@ -362,7 +369,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                     ops.append(("recv", frm, store(f, at, rl_)))
                 if rg_:
                     ops.append(("recv", frm, store(f, at + rl_, rg_)))
-        transport.p2p(ops)
+        _p2p(transport, ops)
         m = new_m
     if not m:
         empty = torch.empty(0, dtype=torch.uint8, device=dev)

@@ -32,7 +32,6 @@ Documented divergences from the reference:
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -74,62 +73,75 @@ class _Plan:
             pass
 
 
-def _as_ids(fine_ids, n, dev):
-    """uint16 device ids of n rows (torch int16/uint16 tensor or numpy array)."""
-    t = fine_ids if isinstance(fine_ids, torch.Tensor) else torch.from_numpy(
-        np.ascontiguousarray(np.asarray(fine_ids).astype(np.uint16)).view(np.int16))
-    if t.dtype not in (torch.int16, torch.uint16):
-        raise TypeError(f"fine_ids must be 16-bit (got {t.dtype})")
-    t = t.to(dev).contiguous().reshape(-1)
+def _as_ids(fine_ids, n, dev, nbins):
+    """uint16 device ids of n rows (torch int16/uint16 tensor or numpy array),
+    every id < nbins.  Host ids are range-checked before the cast (a negative
+    or >= 65536 id would wrap); device ids are checked by the kernels
+    (mgr_rank_ids / mgr_count_ids clamp them and flag the call, whose counts
+    then read -1)."""
+    if isinstance(fine_ids, torch.Tensor):
+        t = fine_ids
+        if t.dtype not in (torch.int16, torch.uint16):
+            raise TypeError(f"fine_ids must be 16-bit (got {t.dtype})")
+        t = t.to(dev).contiguous().reshape(-1)   # range: flagged by the kernels
+    else:
+        a = np.asarray(fine_ids).reshape(-1)
+        if a.dtype.kind not in "iu":
+            raise TypeError(f"fine_ids must be integers (got {a.dtype})")
+        if a.size and (int(a.min()) < 0 or int(a.max()) >= nbins):
+            raise ValueError(f"fine_ids out of range [0, {nbins})")
+        t = torch.from_numpy(np.ascontiguousarray(a.astype(np.uint16)).view(np.int16)).to(dev)
     if t.numel() != n:
         raise ValueError(f"fine_ids has {t.numel()} entries for {n} rows")
     return t
 
 
-_FINE_RANKED = os.environ.get("MGR_FINE_RANKED", "1") != "0"   # A/B measurement only
-
-
-def _sort_by_ids(fields, ids, n, nb, dev, scratch=None):
-    """count (mgr_count_ids) -> scan -> stable pack of every field by the
-    uint16 ids (the fine cells).  Returns ([sorted flat fields], counts)."""
+def _sort_by_ids(fields, ids, n, nb, dev, scratch=None, check_ids=True):
+    """Stable sort of every field by the uint16 ids (the fine cells): rank
+    (mgr_rank_ids) or count (mgr_count_ids) -> scan -> pack.  Returns ([sorted
+    flat fields], counts).  ``check_ids``: ids from the caller (not from this
+    library's binning) -- an id >= nb is clamped by the kernels and turns the
+    counts into -1 (the failed-scan convention: host results raise)."""
     hint = max([f.row_bytes for f in fields] + [1])
-    small = _lib.load().mgr_dest_bytes(int(nb)) == 1   # <= 256 bins: 1-byte dest array
     s = _lib.stream_handle()
     counts = torch.empty(nb, dtype=torch.int64, device=dev)
-    # 65..1024 fine cells, 4-byte-multiple rows: ranks computed once, the
-    # ranked pack only places rows (mgr_rank_ids + mgr_pack_ranked), on its
-    # own tiles (mgr_ranked_tile_rows)
+    bad = torch.zeros(1, dtype=torch.int32, device=dev) if check_ids else None
+    # <= 1024 fine cells, 4-byte-multiple rows <= 64 B on 4-byte-aligned
+    # storage: ranks computed once, the ranked pack only places rows
+    # (mgr_rank_ids + mgr_pack_ranked), on its own tiles (mgr_ranked_tile_rows);
+    # other rows: count + scan + the generic stable pack
     rtr = int(_lib.load().mgr_ranked_tile_rows(int(hint), int(nb)))
-    ranked = (_FINE_RANKED and 64 < nb <= 1024 and rtr > 0
-              and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64 for f in fields))
-    tile_rows, ws, d8 = _scratch(n, nb, hint, dev, scratch, dest=small and not ranked,
-                                 tag="_fine", tile_rows=rtr if ranked else None)
+    ranked = (rtr > 0 and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64
+                              and f.flat.data_ptr() % 4 == 0 for f in fields))
+    tile_rows, ws, dest = _scratch(n, nb, hint, dev, scratch, dest=not ranked,
+                                   tag="_fine", tile_rows=rtr if ranked else None)
+    outs = []
     if ranked:
         T = (n + tile_rows - 1) // tile_rows
         get = scratch.get if scratch is not None else (
             lambda name, nbytes: torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev))
         ranks = get("ranks_fine", 2 * max(n, 1))
-        tstarts = get("tstarts_fine", 2 * max(T * nb, 1))
+        tstarts = get("tstarts_fine", 8 * max(T * nb, 1))   # u16 starts, or u32 x 2 halves
         _lib.call("mgr_rank_ids", _lib.ptr(ids), n, nb, tile_rows, _lib.ptr(ranks),
-                  _lib.ptr(tstarts), _lib.ptr(ws), s)
+                  _lib.ptr(tstarts), _lib.ptr(bad), _lib.ptr(ws), s)
         _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
-        outs = []
         for f in fields:
             o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
             _lib.call("mgr_pack_ranked", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(ids),
                       _lib.ptr(ranks), _lib.ptr(tstarts), nb, tile_rows, _lib.ptr(ws),
                       _lib.ptr(o), s)
             outs.append(o)
-        return outs, counts
-    dest = d8 if small else ids
-    _lib.call("mgr_count_ids", _lib.ptr(ids), n, nb, tile_rows, _lib.ptr(d8), _lib.ptr(ws), s)
-    _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
-    outs = []
-    for f in fields:
-        o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
-        _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
-                  tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
-        outs.append(o)
+    else:
+        _lib.call("mgr_count_ids", _lib.ptr(ids), n, nb, tile_rows, _lib.ptr(dest),
+                  _lib.ptr(bad), _lib.ptr(ws), s)
+        _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+        for f in fields:
+            o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
+            _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
+                      tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
+            outs.append(o)
+    if bad is not None:
+        counts.masked_fill_(bad.ne(0), -1)
     return outs, counts
 
 
@@ -146,10 +158,12 @@ def _offsets_like(data, counts, dev):
     return offsets.cpu() if isinstance(data, torch.Tensor) else offsets.cpu().numpy()
 
 
-def _fine_sort(plan, dim, dev, data, position, return_positions, fine_ids=None):
-    """bin (fine plan, no wrap) -> scan -> stable pack of data (and
-    positions); with ``fine_ids`` (computed at the source, mgr_bin_count_fine)
-    no binning: count -> scan -> pack by the ids."""
+def _fine_sort(plan, coarse, dim, dev, data, position, return_positions, fine_ids=None):
+    """The fine cells of the rows -- ``fine_ids`` as given (computed at the
+    source), else one read of the positions (mgr_bin_count_fine against the
+    coarse plan, periodic=0: no wrap, no write-back; the fine cell is the fine
+    plan's binning by construction, mgr_device.h bin_coord) -- then the
+    stable sort by them (_sort_by_ids)."""
     rows = Rows(data, dev)
     pos = Positions(position, dim, dev, data_rows=rows)
     if pos.n != rows.n:
@@ -157,22 +171,18 @@ def _fine_sort(plan, dim, dev, data, position, return_positions, fine_ids=None):
     n, nb = rows.n, plan.nbins
     prow = Rows(position, dev) if return_positions else None
     fields = [rows] + ([prow] if prow else [])
-    if fine_ids is not None:
-        outs, counts = _sort_by_ids(fields, _as_ids(fine_ids, n, dev), n, nb, dev)
-    else:
+    check = fine_ids is not None
+    if fine_ids is None:
+        ids = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
         hint = max(rows.row_bytes, prow.row_bytes if prow else 1)
-        tile_rows, ws, dest = _scratch(n, nb, hint, dev)
-        s = _lib.stream_handle()
-        counts = torch.empty(nb, dtype=torch.int64, device=dev)
-        _lib.call("mgr_bin_count", plan.h, ctypes.c_void_p(pos.addr), pos.code, n, pos.stride, 0,
-                  _lib.ptr(dest), tile_rows, _lib.ptr(ws), s)
-        _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
-        outs = []
-        for f in fields:
-            o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
-            _lib.call("mgr_pack", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(dest), nb, -1,
-                      tile_rows, _lib.ptr(ws), _lib.ptr(o), -1, None, s)
-            outs.append(o)
+        tile_rows, ws, dest = _scratch(n, coarse.nbins, hint, dev)
+        _lib.call("mgr_bin_count_fine", coarse.h, plan.h, ctypes.c_void_p(pos.addr), pos.code, n,
+                  pos.stride, 0, _lib.ptr(dest), _lib.ptr(ids), tile_rows, _lib.ptr(ws),
+                  _lib.stream_handle())
+        ids = ids[:n]
+    else:
+        ids = _as_ids(fine_ids, n, dev, nb)
+    outs, counts = _sort_by_ids(fields, ids, n, nb, dev, check_ids=check)
     res = [f.wrap(o, n) for f, o in zip(fields, outs)]
     return tuple(res) + (_offsets_like(data, counts, dev),)
 
@@ -334,6 +344,7 @@ class MPIGridRedistributor:
         stably sorted by fine cell with their offsets, = ``fine_cell_sort``
         of the plain result, computed from fine cells binned at the source."""
         self._check_host_alias(data, position)
+        self.comm.reset_traffic()
         rows = Rows(data, self._dev)
         pos = Positions(position, self.dim, self._dev, data_rows=rows)
         if pos.n != rows.n:
@@ -458,7 +469,8 @@ class MPIGridRedistributor:
         recv[0].row_bytes = rows.row_bytes
         if return_positions:
             recv[1].row_bytes = fields[2].row_bytes
-        sorted_, counts = _sort_by_ids(recv, ids, m, fplan.nbins, self._dev, self._scratch)
+        sorted_, counts = _sort_by_ids(recv, ids, m, fplan.nbins, self._dev, self._scratch,
+                                       check_ids=False)   # binned here: in range
         res = [rows.wrap(sorted_[0], m)]
         if return_positions:
             res.append(fields[2].wrap(sorted_[1], m))
@@ -471,6 +483,7 @@ class MPIGridRedistributor:
         (already redistributed).  ``return_positions`` (ignored by the
         reference) returns (data, positions)."""
         self._check_halo(overload_lengths)
+        self.comm.reset_traffic()
         rows = Rows(data, self._dev)
         prow = Rows(position, self._dev)
         if not (isinstance(position, (np.ndarray, torch.Tensor)) and position.ndim == 2
@@ -512,7 +525,8 @@ class MPIGridRedistributor:
         (uint16, ``GridPartitioner.partition_device(..., fine_cells=...)`` /
         mgr_bin_count_fine); the rows are then not binned again."""
         plan = self._fine_plan(fine_cells)
-        return _fine_sort(plan, self.dim, self._dev, data, position, return_positions, fine_ids)
+        return _fine_sort(plan, self._plan, self.dim, self._dev, data, position,
+                          return_positions, fine_ids)
 
     def get_cell_number_from_indexes_host(self, indexes, periodic=True):
         """redist.py:73-85 on the host (neighbour ranks of the halo exchange)."""
@@ -543,6 +557,7 @@ class MPIGridRedistributor:
     def redistribute_by_cell_number(self, data, rank_to_send):
         """redist.py:169-200: send row i to rank ``rank_to_send[i]``; ids
         outside [0, size) are dropped (S6)."""
+        self.comm.reset_traffic()
         rows = Rows(data, self._dev)
         ids, code = id_array(rank_to_send, self._dev)
         if ids.numel() != rows.n:
@@ -592,6 +607,16 @@ class MPIGridRedistributor:
                              self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
                              pack_all=pack_all if side_ids else None)
         return outs, lay.total_recv
+
+    @property
+    def last_traffic(self):
+        """Off-rank bytes of the last redistribution call on this rank
+        (comm.Traffic.as_dict): sent to / received from every other rank,
+        computed from the exchange's real layout -- every field's rows, side
+        fields (fine cells, halo flags), count messages and the halo's
+        messages included.  bench.py's xGMI figures come from it."""
+        t = self.comm.traffic
+        return t.as_dict() if t is not None else None
 
     # ------------------------------------------------------------ helpers
     def stack_position(self, xyz_list):

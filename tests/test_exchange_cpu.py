@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mpi_grid_redistribute_amd.comm import MpiHostComm, TorchDistComm
+from mpi_grid_redistribute_amd.comm import MpiHostComm, TorchDistComm, Transport
 from mpi_grid_redistribute_amd.exchange import exchange
 from oracle import c_oracle
 from oracle import redist_oracle as ro
@@ -141,7 +141,7 @@ class _SimWorld:
         self.lock = threading.Lock()
 
 
-class SimRcclComm:
+class SimRcclComm(Transport):
     """RcclComm's host side (counts all-to-all, the arrays it hands to
     mgr_exchange_rows: comm.row_exchange_arrays) with the device transfers
     replaced by executing mgr_exchange_schedule's operation list on host
@@ -182,6 +182,7 @@ class SimRcclComm:
         lib.mgr_exchange_schedule(self.rank, self.size, len(sends), rb, sc, so, rc, ro_, skip,
                                   ops, n)
         ops = ops[:n]
+        self.sched = [(o.kind, o.peer, o.bytes) for o in ops]
         assert all(o.kind != _lib.MGR_XOP_COPY for o in ops)      # skip_self: no self copy
         assert all(o.peer != self.rank for o in ops)
         w = self.world
@@ -238,8 +239,22 @@ def test_rccl_schedule_exchange(size, empty_rank, drop):
             (pack0 if f == 0 else pack1)(f, snd, redirect_bin, out, out_offset)
 
         t = SimRcclComm(world, r)
+        t.reset_traffic()
         outs, lay = exchange(t, [rb, 4], counts, r, "cpu", pack)
         assert lay.total_send == int(counts.sum()) - int(counts[r])   # no self rows in the buffer
+        # xGMI accounting: the bytes RCCL moves per peer and direction (the
+        # operation list) + one int64 count each way per peer, both fields
+        from mpi_grid_redistribute_amd import _lib
+        want_s, want_r = np.zeros(size, np.int64), np.zeros(size, np.int64)
+        for kind, peer, nbytes in t.sched:
+            (want_s if kind == _lib.MGR_XOP_SEND else want_r)[peer] += nbytes
+        for p in range(size):
+            if p != r:
+                want_s[p] += 8
+                want_r[p] += 8
+        assert t.traffic.send.tolist() == want_s.tolist()
+        assert t.traffic.recv.tolist() == want_r.tolist()
+        assert t.traffic.send[r] == 0 and t.traffic.recv[r] == 0   # the self rows never travel
         return outs[0][: lay.total_recv * rb].numpy().copy(), outs[1][: lay.total_recv * 4].numpy()
 
     outs = run_ranks(size, fn)

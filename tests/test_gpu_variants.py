@@ -18,10 +18,11 @@ pytestmark = pytest.mark.gpu
 mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
-DEFAULTS = {"xcd_pack": 1, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 4, "pack_coop": 1,
+DEFAULTS = {"xcd_pack": 16, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 0, "pack_coop": 1,
             "many_rows": 0, "bin_staged": 1, "tile_rounds": 0,
-            "pack_many": 1, "pack_fine": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
-            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0, "img_rpw": 2}
+            "pack_many": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
+            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0,
+            "img_rpw": 2, "ranked_rows": 0, "ranked_walk": 0}
 VARIANTS = [
     {"img_rpw": 1},
     {"img_rpw": 1, "tile_rounds": 1},
@@ -40,8 +41,11 @@ VARIANTS = [
     {"pack_coop": 0},
     {"pack_coop": 0, "xcd_pack": 0},
     {"pack_many": 0},
-    {"pack_fine": 0},
-    {"pack_fine": 0, "many_rows": 1024},
+    {"xcd_pack": 4},
+    {"xcd_pack": 64, "tile_rounds": 1},
+    {"ranked_rows": 1},
+    {"ranked_rows": 2, "ranked_walk": 1},
+    {"rank_rows": 2048, "ranked_rows": 2},
     {"tile_rounds": 1},
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},

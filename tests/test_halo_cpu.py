@@ -219,3 +219,37 @@ def test_halo_capacity_clamped():
     assert halo_capacity(R, m, [0.0, 0.0, 0.0]) == 4096
     small = halo_capacity(R, m, [0.05, 0.05, 0.05])
     assert int(m * ((1.2 ** 3) - 1)) < small < big
+
+
+@pytest.mark.parametrize("case", ["halo_p8_f64_rec32.npz", "halo_p27_333_ids.npz",
+                                  "halo_direct_p6_321_nonperiodic.npz"])
+def test_threaded_halo_traffic(case):
+    """xGMI accounting of the halo's messages (Transport.traffic): what rank r
+    counts as sent to p is what p counts as received from r, nothing is
+    counted to self, and the bytes are the rows each rank actually received
+    (the halo store grew by them) times the fields' row bytes."""
+    f = G.load(case)
+    size = int(f["size"])
+
+    def fn(comm, r):
+        t = MpiHostComm(comm)
+        t.reset_traffic()
+        out = run_rank(f, case, t, r, carry_pos=True)
+        return out, t.traffic
+
+    res = run_ranks(size, fn)
+    send = np.array([tr.send for _, tr in res])
+    recv = np.array([tr.recv for _, tr in res])
+    assert np.array_equal(send, recv.T)
+    assert not np.diag(send).any() and not np.diag(recv).any()
+    if case.startswith("halo_direct_"):
+        return   # a grid extent of 1: rows of that dimension never leave the rank
+    local, local_pos, _ = local_inputs(f, case)
+    dim = len(f["topology"])
+    for r in range(size):
+        d, lp = local[r], local_pos[r]
+        m = len(res[r][0]) - len(d)                       # halo rows received
+        rb = d.dtype.itemsize * int(np.prod(d.shape[1:], dtype=np.int64)) \
+            + lp.dtype.itemsize * lp.shape[1] + 2          # data + positions + face flags
+        extra = int(recv[r].sum()) - m * rb                # the 8-byte count messages
+        assert extra % 8 == 0 and 0 < extra <= 8 * 4 * dim, (r, extra)
