@@ -239,25 +239,27 @@ int mgr_bin_count_halo(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n
                        int64_t row_stride, int periodic, void* dest, uint16_t* flags,
                        const double* cell_length, const double* overload_lengths, int tile_rows,
                        void* workspace, void* stream);
-/* Multi-selection: set k = the rows whose flag bit bits[k] is set (nsets <=
- * 16; a row may be in several sets), all sets in one pass.  mgr_msel_count
+/* Multi-selection: set k = the rows whose flags hold every bit of masks[k]
+ * (nonzero uint16 masks, nsets <= 32; one bit: a face of the halo, several:
+ * an edge or corner region; a row may be in several sets), all sets in one
+ * pass.  mgr_msel_count
  * writes the per-(set, tile) counts for mgr_scan(n, nsets, ...) (bin_counts
  * = the set sizes); then mgr_msel_pack writes one field's selected rows (any
  * width): set k's rows, in row order, to dsts[k] (nsets device pointers; NULL
  * = set k not written).  The halo's sends of a dimension and direction
  * (redist.py:271-275) go straight to a neighbour's staging buffer or, for a
  * self-neighbour, into the halo store.                                    */
-int mgr_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits, int tile_rows,
+int mgr_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* masks, int tile_rows,
                    void* workspace, void* stream);
 int mgr_msel_pack(const void* src, int64_t row_bytes, int64_t n, const uint16_t* flags,
-                  int nsets, const int* bits, int tile_rows, const void* workspace,
+                  int nsets, const int* masks, int tile_rows, const void* workspace,
                   void* const* dsts, void* stream);
 /* mgr_msel_pack of nfields (1..3) fields of the same rows in one pass (the
  * flags read and the sets listed once): srcs[f] rows of row_bytes[f]; set k
  * of field f goes to dsts[f * nsets + k]; field 0's NULLs decide which sets
  * are written.                                                            */
 int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
-                         const uint16_t* flags, int nsets, const int* bits, int tile_rows,
+                         const uint16_t* flags, int nsets, const int* masks, int tile_rows,
                          const void* workspace, void* const* dsts, void* stream);
 
 /* ------------------------------------------------------------ exchange --

@@ -139,6 +139,12 @@ class Transport:
     def barrier(self):
         pass
 
+    def any_failed(self, failed):
+        """Global agreement on a local failure flag (True if any rank failed):
+        lets every rank raise together where a failure would otherwise reach
+        only some peers (the halo's neighbour-only count messages)."""
+        return bool(failed)
+
 
 def _self_pairs(ops, rank):
     """The k-th non-empty send to ``rank`` feeds its k-th non-empty receive."""
@@ -258,6 +264,11 @@ class RcclComm(Transport):
     def barrier(self):
         self.allreduce_max([0.0])
 
+    def any_failed(self, failed):
+        if self.size == 1:
+            return bool(failed)
+        return bool(self.allreduce_max([1.0 if failed else 0.0])[0] > 0)
+
 
 class MpiHostComm(Transport):
     """Any mpi4py-like communicator: counts and rows move with its lowercase
@@ -316,6 +327,9 @@ class MpiHostComm(Transport):
     def barrier(self):
         self.comm.alltoall([0] * self.size)
 
+    def any_failed(self, failed):
+        return any(bool(x) for x in self.comm.alltoall([bool(failed)] * self.size))
+
 
 class TorchDistComm(Transport):
     """torch.distributed all_to_all_single (gloo for CPU tests, nccl on GPUs).
@@ -365,6 +379,13 @@ class TorchDistComm(Transport):
 
     def barrier(self):
         self.dist.barrier(group=self.group)
+
+    def any_failed(self, failed):
+        t = torch.tensor([1 if failed else 0], dtype=torch.int64)
+        if self.dist.get_backend(self.group) == "nccl":
+            t = t.cuda()
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return bool(t.item())
 
 
 def as_transport(comm):

@@ -418,13 +418,7 @@ __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __res
 // RPW > 0 / NBITS > 0: the rounds per wave and the id bits at compile time
 // (the ranked tiles of mgr_ranked_tile_rows, 512 cells): unrolled rounds in
 // named registers and an unrolled ballot match; 0: read at run time.
-// HALF (4 waves, 4096-row tiles): ranks and starts per half tile (waves 0-1
-// = rows 0..2047, waves 2-3 = rows 2048..4095) for the half-tile pack
-// (pack_ranked_half_kernel): a row's rank among its half's rows of its bin,
-// and per half h and bin b one uint32 hinfo[2 tile + h][b] = (start of b in
-// the half's sorted image) | (rows of b in the earlier half) << 16.  The
-// tile histogram for mgr_scan is the same.
-template <int NW, int RPW, int NBITS, bool HALF = false>
+template <int NW, int RPW, int NBITS>
 __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     const uint16_t* __restrict__ ids, int64_t n, int nbins, int nbits,
     int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ ranks,
@@ -475,29 +469,17 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     int carry = 0;
     for (int k = 0; k * NT < nbins; ++k) {
         const int bb = k * NT + tid;
-        int run = 0;   // HALF: the two halves' counts packed (each <= 2048)
-        int c0h = 0;
+        int run = 0;
         if (bb < nbins) {
             int c[NW];
 #pragma unroll
             for (int ww = 0; ww < NW; ++ww) c[ww] = wt[ww * nbins + bb];
-            if constexpr (HALF) {
-                static_assert(NW == 4, "half tiles: waves 0-1 and 2-3");
-                wt[0 * nbins + bb] = 0;
-                wt[1 * nbins + bb] = (uint16_t)c[0];
-                wt[2 * nbins + bb] = 0;
-                wt[3 * nbins + bb] = (uint16_t)c[2];
-                c0h = c[0] + c[1];
-                run = c0h | ((c[2] + c[3]) << 16);
-                counts[(int64_t)bb * T + tile] = c0h + c[2] + c[3];
-            } else {
 #pragma unroll
-                for (int ww = 0; ww < NW; ++ww) {
-                    wt[ww * nbins + bb] = (uint16_t)run;
-                    run += c[ww];
-                }
-                counts[(int64_t)bb * T + tile] = run;
+            for (int ww = 0; ww < NW; ++ww) {
+                wt[ww * nbins + bb] = (uint16_t)run;
+                run += c[ww];
             }
+            counts[(int64_t)bb * T + tile] = run;
         }
         int incl = run;
 #pragma unroll
@@ -514,16 +496,7 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
             wpre += ww < w ? x : 0;
             wall += x;
         }
-        if constexpr (HALF) {
-            const unsigned p = (unsigned)(carry + wpre + incl - run);
-            uint32_t* hinfo = (uint32_t*)tile_starts;
-            if (bb < nbins) {
-                hinfo[(2 * tile) * nbins + bb] = p & 0xFFFFu;
-                hinfo[(2 * tile + 1) * nbins + bb] = (p >> 16) | ((unsigned)c0h << 16);
-            }
-        } else {
-            if (bb < nbins) tile_starts[tile * nbins + bb] = (uint16_t)(carry + wpre + incl - run);
-        }
+        if (bb < nbins) tile_starts[tile * nbins + bb] = (uint16_t)(carry + wpre + incl - run);
         carry += wall;
         __syncthreads();
     }
@@ -537,7 +510,7 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
 
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                            const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
-                           uint8_t* dest8, uint32_t* bad, hipStream_t s, bool half) {
+                           uint8_t* dest8, uint32_t* bad, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     prof_begin(s, K_COUNT_IDS);
     // 4 waves (16 waves measured 0.57 vs 0.31 ms at 64M rows, 512 bins)
@@ -547,10 +520,6 @@ hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_r
     auto k = tile_rows == 4096 ? (b9 ? rank_ids_kernel<kWaves, 16, 9> : rank_ids_kernel<kWaves, 16, 0>)
            : tile_rows == 2048 ? (b9 ? rank_ids_kernel<kWaves, 8, 9> : rank_ids_kernel<kWaves, 8, 0>)
                                : rank_ids_kernel<kWaves, 0, 0>;
-    if (half) {
-        if (tile_rows != 4096) return hipErrorNotSupported;
-        k = b9 ? rank_ids_kernel<kWaves, 16, 9, true> : rank_ids_kernel<kWaves, 16, 0, true>;
-    }
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s, ids, n, nbins,
                        nbits_for(nbins), ws.counts, ws.T, tile_rows, ranks, tile_starts, dest8,

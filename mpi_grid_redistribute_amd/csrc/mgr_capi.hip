@@ -327,36 +327,37 @@ int mgr_bin_count_halo(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n
     return MGR_OK;
 }
 
-static int check_sets(int nsets, const int* bits) {
-    if (nsets < 1 || nsets > 16 || !bits) return fail(MGR_EINVAL, "nsets %d (1..16)", nsets);
+static int check_sets(int nsets, const int* masks) {
+    if (nsets < 1 || nsets > mgr::kMaxSets || !masks)
+        return fail(MGR_EINVAL, "nsets %d (1..%d)", nsets, mgr::kMaxSets);
     for (int k = 0; k < nsets; ++k)
-        if (bits[k] < 0 || bits[k] > 15) return fail(MGR_EINVAL, "set %d: flag bit %d", k, bits[k]);
+        if (masks[k] < 1 || masks[k] > 0xFFFF) return fail(MGR_EINVAL, "set %d: flag mask %d", k, masks[k]);
     return MGR_OK;
 }
 
-int mgr_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits, int tile_rows,
+int mgr_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* masks, int tile_rows,
                    void* workspace, void* stream) {
     int rc = check_tile(tile_rows);
-    if (rc || (rc = check_sets(nsets, bits))) return rc;
+    if (rc || (rc = check_sets(nsets, masks))) return rc;
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (n > 0 && (!flags || !workspace)) return fail(MGR_EINVAL, "null argument");
     const mgr::Workspace ws = mgr::carve(workspace, n, nsets, tile_rows);
-    HIP_OK(mgr::launch_msel_count(flags, n, nsets, bits, tile_rows, ws, (hipStream_t)stream));
+    HIP_OK(mgr::launch_msel_count(flags, n, nsets, masks, tile_rows, ws, (hipStream_t)stream));
     return MGR_OK;
 }
 
 int mgr_msel_pack(const void* src, int64_t row_bytes, int64_t n, const uint16_t* flags,
-                  int nsets, const int* bits, int tile_rows, const void* workspace,
+                  int nsets, const int* masks, int tile_rows, const void* workspace,
                   void* const* dsts, void* stream) {
-    return mgr_msel_pack_fields(1, &src, &row_bytes, n, flags, nsets, bits, tile_rows, workspace,
+    return mgr_msel_pack_fields(1, &src, &row_bytes, n, flags, nsets, masks, tile_rows, workspace,
                                 dsts, stream);
 }
 
 int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
-                         const uint16_t* flags, int nsets, const int* bits, int tile_rows,
+                         const uint16_t* flags, int nsets, const int* masks, int tile_rows,
                          const void* workspace, void* const* dsts, void* stream) {
     int rc = check_tile(tile_rows);
-    if (rc || (rc = check_sets(nsets, bits))) return rc;
+    if (rc || (rc = check_sets(nsets, masks))) return rc;
     if (nfields < 1 || nfields > 3 || !srcs || !row_bytes)
         return fail(MGR_EINVAL, "nfields %d (1..3)", nfields);
     for (int f = 0; f < nfields; ++f)
@@ -366,7 +367,7 @@ int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* ro
         if (!srcs[f]) return fail(MGR_EINVAL, "null argument");
     if (n <= 0) return MGR_OK;
     const mgr::Workspace ws = mgr::carve((void*)workspace, n, nsets, tile_rows);
-    HIP_OK(mgr::launch_msel_pack(nfields, srcs, row_bytes, n, flags, nsets, bits, tile_rows, ws,
+    HIP_OK(mgr::launch_msel_pack(nfields, srcs, row_bytes, n, flags, nsets, masks, tile_rows, ws,
                                  dsts, (hipStream_t)stream));
     return MGR_OK;
 }
@@ -394,7 +395,7 @@ int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint1
     if (n > 0 && (!ids || !ranks || !tile_starts || !workspace)) return fail(MGR_EINVAL, "null argument");
     const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
     HIP_OK(mgr::launch_rank_ids(ids, n, nbins, tile_rows, ws, ranks, tile_starts, nullptr, bad_ids,
-                                (hipStream_t)stream, mgr::ranked_half(nbins, tile_rows, n)));
+                                (hipStream_t)stream));
     return MGR_OK;
 }
 
@@ -771,7 +772,6 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
     else if (!strcmp(key, "ranked_rows")) mgr::g_tune.ranked_rows = (int)value;
     else if (!strcmp(key, "ranked_walk")) mgr::g_tune.ranked_walk = (int)value;
-    else if (!strcmp(key, "ranked_ko")) mgr::g_tune.ranked_ko = (int)value;
     else if (!strcmp(key, "img_rpw")) {
         if (value != 1 && value != 2) return fail(MGR_EINVAL, "img_rpw %lld (1 or 2)", (long long)value);
         mgr::g_tune.img_rpw = (int)value;

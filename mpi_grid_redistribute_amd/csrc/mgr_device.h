@@ -536,7 +536,22 @@ __device__ __forceinline__ uint32_t set_mask(const uint32_t (&fw)[kSelWords], in
     return m;
 }
 
-__device__ __forceinline__ int set_bit(uint64_t bits, int k) { return (int)((bits >> (4 * k)) & 15u); }
+// Selection sets by flag mask: set k = the rows whose flags hold every bit of
+// masks.m[k] (one bit: a face; several: an edge or corner region of the halo).
+struct SetMasks {
+    uint16_t m[kMaxSets];
+};
+
+// bit j of the result: the lane's row j has every flag bit of mask
+__device__ __forceinline__ uint32_t set_mask_m(const uint32_t (&fw)[kSelWords], unsigned mask) {
+    uint32_t r = 0xFFFFu;
+    while (mask) {
+        const int b = __builtin_ctz(mask);
+        mask &= mask - 1u;
+        r &= set_mask(fw, b);
+    }
+    return r;
+}
 
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll

@@ -14,6 +14,7 @@ constexpr int kMaxTileRows = 65536;      // many-bin pack tiles (super-rounds of
 constexpr int kCoopMaxRounds = 64;       // cooperative pack tiles <= 4096 rows
 constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
 constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups) at most
+constexpr int kMaxSets = 32;             // multi-selection sets per pass (halo pieces <= 26)
 
 // One-pass scan control words, right behind the kScanFlags chunk words and
 // zeroed with them by every count producer.
@@ -96,18 +97,16 @@ hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, in
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
                             hipStream_t s, const FineGeom* fg = nullptr,
                             uint16_t* side_out = nullptr, const HaloGeom* hg = nullptr);
-hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits,
+hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* masks,
                              int tile_rows, const Workspace& ws, hipStream_t s);
 hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
-                            int64_t n, const uint16_t* flags, int nsets, const int* bits,
+                            int64_t n, const uint16_t* flags, int nsets, const int* masks,
                             int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s);
 hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                             const Workspace& ws, void* dest, uint32_t* bad, hipStream_t s);
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                            const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
-                           uint8_t* dest8, uint32_t* bad, hipStream_t s, bool half);
-// the ranked sort takes half tiles (rank_ids HALF + pack_ranked_half_kernel)
-bool ranked_half(int nbins, int tile_rows, int64_t n);
+                           uint8_t* dest8, uint32_t* bad, hipStream_t s);
 hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
                               const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
                               int tile_rows, const Workspace& ws, void* dst, hipStream_t s);
@@ -153,8 +152,7 @@ struct Tune {
                                  // (-1: give up at once -- tests of the error path)
     int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
     int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
-    int ranked_rows = 0;   // ranked pack: 0 16-byte units, 1 row-wise read-back, 2 units, unrolled
-    int ranked_ko = 0;     // A/B knockouts of the ranked pack (timing only, wrong output)
+    int ranked_rows = 0;   // ranked pack store phase: 0 rolled loop, 2 unrolled
     int ranked_walk = 0;   // ranked pack tile walk: 0 one region per XCD, 1 all XCDs in one region
     int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096
     int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)

@@ -264,13 +264,13 @@ __global__ __launch_bounds__(kBlock) void select_count_kernel(const uint16_t* __
 }
 
 // Multi-selection counts (the halo's sends, redist.py:271-275, all at once):
-// set s selects the rows whose flag bit bits[s] is set -- a row may be in
-// several sets (near an edge or a corner).  Wave-private tiles of tile_rows
-// rows read in kSelChunk-row chunks (chunk_flags); counts[s * T + tile] for
-// mgr_scan with nbins = nsets, whose offsets then lay the sets out one after
-// the other, each in row order.
+// set s selects the rows whose flags hold every bit of masks.m[s] -- a row
+// may be in several sets (near an edge or a corner).  Wave-private tiles of
+// tile_rows rows read in kSelChunk-row chunks (chunk_flags); counts[s * T +
+// tile] for mgr_scan with nbins = nsets, whose offsets then lay the sets out
+// one after the other, each in row order.
 __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __restrict__ flags,
-                                                            int64_t n, int nsets, uint64_t bits,
+                                                            int64_t n, int nsets, SetMasks masks,
                                                             int32_t* __restrict__ counts,
                                                             int64_t T, int tile_rows,
                                                             uint64_t* __restrict__ scan_flags) {
@@ -280,33 +280,33 @@ __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __re
     if (tile >= T) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
-    int c[16];
+    int c[kMaxSets];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) c[k] = 0;
+    for (int k = 0; k < kMaxSets; ++k) c[k] = 0;
     for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
         uint32_t fw[kSelWords];
         chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (k < nsets) c[k] += __popc(set_mask(fw, set_bit(bits, k)));
+        for (int k = 0; k < kMaxSets; ++k)
+            if (k < nsets) c[k] += __popc(set_mask_m(fw, masks.m[k]));
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < kMaxSets; ++k) {
         if (k >= nsets) break;
         const int t = wave_sum(c[k]);
         if (lane == 0) counts[(int64_t)k * T + tile] = t;
     }
 }
 
-hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* bits,
+hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const int* masks,
                              int tile_rows, const Workspace& ws, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    uint64_t sb = 0;
-    for (int k = 0; k < nsets; ++k) sb |= (uint64_t)(bits[k] & 15) << (4 * k);
+    SetMasks sm{};
+    for (int k = 0; k < nsets; ++k) sm.m[k] = (uint16_t)masks[k];
     const int64_t grid = (ws.T + kWaves - 1) / kWaves;
     prof_begin(s, K_HALO);
     hipLaunchKernelGGL(msel_count_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, flags, n,
-                       nsets, sb, ws.counts, ws.T, tile_rows, ws.flags);
+                       nsets, sm, ws.counts, ws.T, tile_rows, ws.flags);
     prof_end(s, K_HALO);
     return hipGetLastError();
 }

@@ -262,7 +262,7 @@ struct SelFields {
     const uint8_t* src[kSelFields];
     int64_t row_bytes[kSelFields];
     int wlog[kSelFields];                 // log2 of the copy unit
-    uint8_t* dst[kSelFields][16];
+    uint8_t* dst[kSelFields][kMaxSets];
 };
 
 template <int W>
@@ -305,13 +305,13 @@ __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_
 }
 
 __global__ __launch_bounds__(256) void msel_pack_kernel(
-    SelFields fs, int nf, int64_t n, const uint16_t* __restrict__ flags, int nsets, uint64_t bits,
+    SelFields fs, int nf, int64_t n, const uint16_t* __restrict__ flags, int nsets, SetMasks masks,
     const int64_t* __restrict__ offsets, const int64_t* __restrict__ set_starts, int64_t T,
     int tile_rows, const uint32_t* __restrict__ scan_err) {
     __shared__ uint16_t list_s[4][kSelCap];
-    __shared__ uint8_t* dst_s[4][kSelFields][16];
-    __shared__ long long at_s[4][16];    // next output row of every set
-    __shared__ int start_s[4][16], cnt_s[4][16];
+    __shared__ uint8_t* dst_s[4][kSelFields][kMaxSets];
+    __shared__ long long at_s[4][kMaxSets];    // next output row of every set
+    __shared__ int start_s[4][kMaxSets], cnt_s[4][kMaxSets];
     const int w = threadIdx.x >> 6, lane = lane_id();
     const int64_t tile = (int64_t)blockIdx.x * 4 + w;
     if (tile >= T || scan_failed(scan_err)) return;
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
     int* cnt = cnt_s[w];
     uint32_t live = 0;   // sets with a destination (in field 0: all fields alike)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < kMaxSets; ++k) {
         if (k >= nsets) break;
         if (fs.dst[0][k]) live |= 1u << k;
         if (lane == k) {
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         int fill = 0;
         for (int k = 0; k < nsets; ++k) {
             if (!((live >> k) & 1u)) continue;
-            uint32_t m = set_mask(fw, set_bit(bits, k));
+            uint32_t m = set_mask_m(fw, masks.m[k]);
             int total;
             int pos = wave_excl(__popc(m), &total);
             if (!total) continue;
@@ -385,12 +385,13 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
 }
 
 hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
-                            int64_t n, const uint16_t* flags, int nsets, const int* bits,
+                            int64_t n, const uint16_t* flags, int nsets, const int* masks,
                             int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    if (nfields < 1 || nfields > kSelFields) return hipErrorInvalidValue;
-    uint64_t sb = 0;
-    for (int k = 0; k < nsets; ++k) sb |= (uint64_t)(bits[k] & 15) << (4 * k);
+    if (nfields < 1 || nfields > kSelFields || nsets < 1 || nsets > kMaxSets)
+        return hipErrorInvalidValue;
+    SetMasks sb{};
+    for (int k = 0; k < nsets; ++k) sb.m[k] = (uint16_t)masks[k];
     SelFields fs{};
     for (int f = 0; f < nfields; ++f) {
         fs.src[f] = (const uint8_t*)srcs[f];
@@ -492,6 +493,38 @@ typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <typename T>
 __device__ __forceinline__ void gstore(unsigned long long a, T v) {
     *(__attribute__((address_space(1))) T*)a = v;
+}
+
+// One 16-byte unit (image bytes [x, x + 16)) of a destination-sorted LDS
+// image to its output: a bin's rows are one run of the image, and the unit's
+// bytes go to gaddr[bin] + x.  A unit inside one run is one 16-byte store;
+// a unit straddling two runs goes dword by dword.  For rows wider than 16 B
+// a unit covers at most two rows (x / RB and (x + 15) / RB), so both run
+// addresses are fetched up front, side by side -- no LDS lookup per dword on
+// the straddling path (the lookups were a chain of dependent LDS reads per
+// dword).  DROP: a zero address is a dropped bin, not written.
+template <int RB, bool DROP, typename BinT>
+__device__ __forceinline__ void store_img_unit(const uint8_t* __restrict__ img,
+                                               const BinT* ibin,
+                                               const unsigned long long* gaddr, int x,
+                                               int nbytes) {
+    const u32x4_t q = *(const u32x4_t*)(img + x);
+    const int r0 = x / RB, r1 = min(x + 15, nbytes - 1) / RB;
+    const int bf = ibin[r0], bl = ibin[r1];
+    const unsigned long long af = gaddr[bf], al = gaddr[bl];
+    if (x + 16 <= nbytes && bf == bl) {
+        if (!DROP || af) gstore<u32x4_a4>(af + x, q);
+        return;
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int xd = x + 4 * d;
+        if (xd >= nbytes) break;
+        unsigned long long a;
+        if constexpr (RB > 16) a = xd < (r0 + 1) * RB ? af : al;
+        else a = gaddr[ibin[xd / RB]];   // narrow rows: up to 4 rows in a unit
+        if (!DROP || a) gstore<uint32_t>(a + xd, q[d]);
+    }
 }
 
 template <int RB, int RPW, bool SEL>
@@ -641,24 +674,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
 #pragma unroll
     for (int k = 0; k < NU; ++k) {
         const int x = 16 * (64 * k + lane);
-        if (x < nbytes) {
-            const u32x4_t q = *(const u32x4_t*)(img + x);
-            const int bf = ibin[x / RB];
-            const int last = min(x + 15, nbytes - 1);
-            if (x + 16 <= nbytes && ibin[last / RB] == bf) {
-                const unsigned long long a = gaddr[bf];
-                if (a) gstore<u32x4_a4>(a + x, q);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    if (xd < nbytes) {
-                        const unsigned long long a = gaddr[ibin[xd / RB]];
-                        if (a) gstore<uint32_t>(a + xd, q[d]);
-                    }
-                }
-            }
-        }
+        if (x < nbytes) store_img_unit<RB, true>(img, ibin, gaddr, x, nbytes);
     }
 }
 
@@ -1001,7 +1017,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
     const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
     const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err, int walk, int ko) {
+    const uint32_t* __restrict__ scan_err, int walk) {
     static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
     constexpr int NW = kFineWaves, RPW = TR / 64 / NW;
     constexpr int NDW = RB / 4;
@@ -1052,11 +1068,6 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         for (int q = 0; q < RPW; ++q) {
             if ((w * RPW + q) * 64 + lane < tr) {
                 const int lpos = lstart[S.b[q]] + S.rk[q];
-                if (ko & 1) {   // A/B knockout 1: rows not written to the image
-                    ibin[lpos] = (uint16_t)S.b[q];
-                    if (S.v[q][0] == 0x9E3779B9u && S.v[q][NDW - 1] == 0x7F4A7C15u) img[lpos * NDW] = 1u;
-                    continue;
-                }
 #pragma unroll
                 for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
                 ibin[lpos] = (uint16_t)S.b[q];
@@ -1065,18 +1076,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         __syncthreads();
         const int nbytes = tr * RB;
         auto unit = [&](int x) __attribute__((always_inline)) {
-            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
-            const int bf = ibin[x / RB];
-            if (ko & 4) return;   // A/B knockout: no stores
-            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
-                gstore<u32x4_a4>(gaddr[bf] + x, q);
-            } else if (!(ko & 2)) {   // A/B knockout 2: straddling units not stored
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
-                }
-            }
+            store_img_unit<RB, false>((const uint8_t*)img, ibin, gaddr, x, nbytes);
         };
         if constexpr (UNR) {
             // unrolled: no store loop whose preheader would wait (vmcnt 0)
@@ -1109,198 +1109,6 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
-template <int NDW>
-__device__ __forceinline__ void store_row_dw(unsigned long long a, const uint32_t (&v)[NDW]) {
-    int i = 0;
-#pragma unroll
-    for (; i + 4 <= NDW; i += 4) gstore<u32x4_a4>(a + 4 * i, u32x4_a4{v[i], v[i + 1], v[i + 2], v[i + 3]});
-    if constexpr (NDW % 4 == 3) gstore<u32x3_a4>(a + 4 * i, u32x3_a4{v[i], v[i + 1], v[i + 2]});
-    else if constexpr (NDW % 4 == 2) gstore<u32x2_a4>(a + 4 * i, u32x2_a4{v[i], v[i + 1]});
-    else if constexpr (NDW % 4 == 1) gstore<uint32_t>(a + 4 * i, v[i]);
-}
-
-// Ranked pack, row-wise read-back (round 3).  Same tile walk and LDS image
-// as pack_ranked_kernel, but the image leaves row by row: lane l of a wave
-// takes sorted row j (consecutive j per wave, so a store instruction writes
-// the wave's rows of each run back to back), reads its dwords (stride RB/4,
-// conflict-free), and stores the row whole to obase[bin] + j.  Every access
-// is branch-free: rows past the tile end re-read and re-store the tile's
-// last row (identical bytes to the same place), so each wave issues the
-// same number of stores for every tile and the next tile's loads (issued a
-// tile ahead) stay in flight across them -- no data-dependent dword path,
-// no per-unit run lookups.
-template <int RB, int TR>
-__global__ __launch_bounds__(1024) void pack_ranked_rows_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
-    const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
-    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err) {
-    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
-    constexpr int NW = kFineWaves, RPW = TR / 64 / NW;
-    constexpr int NDW = RB / 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* img = (uint32_t*)smem;
-    uint8_t* p = smem + align16(TR * RB);
-    uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
-    long long* obase = (long long*)p;              p += nb * 8;
-    uint16_t* lstart = (uint16_t*)p;
-    if (scan_failed(scan_err)) return;
-    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const int64_t per = (T + 7) >> 3;
-    const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3);
-    const int64_t first = (int64_t)(blockIdx.x & 7) * per, last = min(T, first + per);
-    const int mb = min(tid, nb - 1);
-    struct Set {
-        uint32_t v[RPW][NDW];
-        unsigned b[RPW];
-        unsigned rk[RPW];
-        long long seg;
-        unsigned ls;
-    };
-    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
-        t = min(t, last - 1);
-        S.seg = offsets[(int64_t)mb * T + t];
-        S.ls = tile_starts[t * nb + mb];
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
-            S.b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));   // ids >= nb: clamped (mgr_rank_ids reports them)
-            S.rk[q] = ranks[row];
-            load_row_dw<NDW>(src + row * RB, S.v[q]);
-        }
-    };
-    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
-        const int tr = (int)min((int64_t)TR, n - t * TR);
-        if (tid < nb) {
-            lstart[tid] = (uint16_t)S.ls;
-            obase[tid] = S.seg - (long long)S.ls;
-        }
-        __syncthreads();
-        // rows into the sorted image (rows past n were clamped to row n - 1:
-        // the same bytes to the same slot)
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const int lpos = lstart[S.b[q]] + S.rk[q];
-#pragma unroll
-            for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = S.v[q][i];
-            ibin[lpos] = (uint16_t)S.b[q];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const int j = min(w * (64 * RPW) + 64 * q + lane, tr - 1);
-            const long long o = obase[ibin[j]] + j;
-            uint32_t row[NDW];
-#pragma unroll
-            for (int i = 0; i < NDW; ++i) row[i] = img[j * NDW + i];
-            store_row_dw<NDW>((unsigned long long)(dst + o * RB), row);
-        }
-        __syncthreads();   // the image, ibin, lstart and obase are reused by the next tile
-    };
-    Set A, B;
-    int64_t t = first + kx;
-    if (t >= last) return;
-    load(A, t);
-    for (;;) {
-        load(B, t + gx);
-        process(A, t);
-        t += gx;
-        if (t >= last) break;
-        load(A, t + gx);
-        process(B, t);
-        t += gx;
-        if (t >= last) break;
-    }
-}
-
-// Half-tile ranked pack (round 3): the 4096-row scan tiles are packed as two
-// independent 2048-row halves (mgr_rank_ids in half mode ranks each half on
-// its own), one 512-thread workgroup per half, not persistent.  A half's
-// LDS (image + bins + tables, <= 80 KiB for rows of <= 36 B) lets two
-// workgroups share a CU, so one streams its rows in while the other stores
-// its image out -- the overlap a single persistent workgroup per CU did not
-// get (its store phase waited for the next tile's loads, profiles/round3).
-// hinfo[half][b] = start of bin b in the half's sorted image | (rows of b in
-// the tile's earlier half) << 16; a row's output = offsets[b][tile] + that
-// count + its rank in the half.
-constexpr int kHalfRows = 2048;
-constexpr int kHalfThreads = 512;
-
-bool ranked_half(int nbins, int tile_rows, int64_t n) {
-    return g_tune.ranked_rows == 3 && tile_rows == 4096 && n < ((int64_t)1 << 31) && nbins <= 1024;
-}
-
-template <int RB>
-__global__ __launch_bounds__(kHalfThreads) void pack_ranked_half_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
-    const uint16_t* __restrict__ ranks, const uint32_t* __restrict__ hinfo, int nb,
-    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err, int xcd) {
-    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
-    constexpr int HR = kHalfRows, NT = kHalfThreads, RPT = HR / NT;   // rows per thread
-    constexpr int NDW = RB / 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* img = (uint32_t*)smem;
-    uint8_t* p = smem + align16(HR * RB);
-    uint16_t* ibin = (uint16_t*)p;                 p += align16(HR * 2);
-    int* obase = (int*)p;                          p += align16(nb * 4);
-    uint16_t* lstart = (uint16_t*)p;
-    if (scan_failed(scan_err)) return;
-    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const int64_t half = xcd ? xcd_tile_c(blockIdx.x, 2 * T, xcd) : (int64_t)blockIdx.x;
-    const int64_t t = half >> 1, row0 = half * HR;
-    if (row0 >= n) return;
-    const int tr = (int)min((int64_t)HR, n - row0);
-    if (tid < nb) {
-        const uint32_t hi = hinfo[half * nb + tid];
-        lstart[tid] = (uint16_t)(hi & 0xFFFFu);
-        obase[tid] = (int)(offsets[(int64_t)tid * T + t] + (long long)(hi >> 16) - (long long)(hi & 0xFFFFu));
-    }
-    unsigned b[RPT], rk[RPT];
-    uint32_t v[RPT][NDW];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        // rows past n: the half's last row again (same bytes to the same slot)
-        const int64_t row = min(row0 + (int64_t)(w * RPT + q) * 64 + lane, n - 1);
-        b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));
-        rk[q] = ranks[row];
-        load_row_dw<NDW>(src + row * RB, v[q]);
-    }
-    for (int i = tid + 512; i < nb; i += NT) {   // > 512 bins
-        const uint32_t hi = hinfo[half * nb + i];
-        lstart[i] = (uint16_t)(hi & 0xFFFFu);
-        obase[i] = (int)(offsets[(int64_t)i * T + t] + (long long)(hi >> 16) - (long long)(hi & 0xFFFFu));
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int lpos = lstart[b[q]] + rk[q];
-#pragma unroll
-        for (int i = 0; i < NDW; ++i) img[lpos * NDW + i] = v[q][i];
-        ibin[lpos] = (uint16_t)b[q];
-    }
-    __syncthreads();
-    const int nbytes = tr * RB;
-    for (int x = 16 * tid; x < nbytes; x += 16 * NT) {
-        const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
-        const int bf = ibin[x / RB];
-        if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
-            gstore<u32x4_a4>((unsigned long long)(dst + (int64_t)obase[bf] * RB + x), q);
-        } else {
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const int xd = x + 4 * d;
-                if (xd < nbytes)
-                    gstore<uint32_t>((unsigned long long)(dst + (int64_t)obase[ibin[xd / RB]] * RB + xd), q[d]);
-            }
-        }
-    }
-}
-
-static int ranked_half_lds_bytes(int64_t row_bytes, int nbins) {
-    return align16(kHalfRows * (int)row_bytes) + align16(kHalfRows * 2) + align16(nbins * 4) + nbins * 2;
-}
-
 // LDS of the ranked pack: the tile image, its row bins, per-bin output
 // addresses and tile starts.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
@@ -1324,29 +1132,6 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if ((tile_rows != kFineTR && tile_rows != 4096) || row_bytes % 4 || row_bytes > 64 ||
         ((uintptr_t)src & 3) || ((uintptr_t)dst & 3))
         return hipErrorNotSupported;
-    if (ranked_half(nbins, tile_rows, n)) {
-        const int hl = ranked_half_lds_bytes(row_bytes, nbins);
-        prof_begin(s, K_PACK_FINE);
-        hipError_t e = hipErrorNotSupported;
-#define MGR_PH(RB_)                                                                           \
-        case RB_: {                                                                           \
-            auto k = pack_ranked_half_kernel<RB_>;                                            \
-            ensure_lds(k, hl);                                                                \
-            hipLaunchKernelGGL(k, dim3((unsigned)(2 * ws.T)), dim3(kHalfThreads), (size_t)hl, s, \
-                               (const uint8_t*)src, n, ids, ranks, (const uint32_t*)tile_starts, \
-                               nbins, ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,           \
-                               g_tune.xcd_pack);                                              \
-            e = hipGetLastError();                                                            \
-        } break;
-        switch ((int)row_bytes) {
-            MGR_PH(4) MGR_PH(8) MGR_PH(12) MGR_PH(16) MGR_PH(20) MGR_PH(24) MGR_PH(28) MGR_PH(32)
-            MGR_PH(36) MGR_PH(40) MGR_PH(44) MGR_PH(48) MGR_PH(52) MGR_PH(56) MGR_PH(60) MGR_PH(64)
-            default: break;
-        }
-#undef MGR_PH
-        prof_end(s, K_PACK_FINE);
-        return e;
-    }
     const int lds = ranked_lds_bytes(tile_rows, row_bytes, nbins);
     if (lds > 160 * 1024) return hipErrorNotSupported;
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
@@ -1356,20 +1141,14 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     hipError_t e = hipErrorNotSupported;
 #define MGR_PRT(RB_, TR_)                                                                     \
     {                                                                                         \
-        if (g_tune.ranked_rows == 1) {                                                        \
-            auto k = pack_ranked_rows_kernel<RB_, TR_>;                                       \
-            ensure_lds(k, lds);                                                               \
-            hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,           \
-                               (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,        \
-                               ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err);                 \
-        } else {                                                                              \
+        {                                                                                     \
             auto k = g_tune.ranked_rows == 2 ? pack_ranked_kernel<RB_, TR_, true>             \
                                              : pack_ranked_kernel<RB_, TR_, false>;           \
             ensure_lds(k, lds);                                                               \
             hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,           \
                                (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,        \
                                ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,                  \
-                               g_tune.ranked_walk, g_tune.ranked_ko);                         \
+                               g_tune.ranked_walk);                                           \
         }                                                                                     \
         e = hipGetLastError();                                                                \
     }

@@ -57,6 +57,7 @@ import torch
 
 from . import _lib
 from .comm import excl_cumsum
+from .exchange import check_counts
 
 
 def _p2p(transport, ops):
@@ -64,6 +65,63 @@ def _p2p(transport, ops):
     the transport's traffic."""
     transport.note_p2p(ops)
     transport.p2p(ops)
+
+
+def _agree_counts(transport, sent, received):
+    """check_counts on every rank at once: a -1 count (a selection scan that
+    gave up) reaches only the neighbours of the failed rank, so the ranks
+    agree on the flag first and all raise, none left waiting in a message."""
+    failed = (np.asarray(sent) < 0).any() or (np.asarray(received) < 0).any()
+    if transport.any_failed(failed):
+        check_counts(sent, received)
+        check_counts([-1], [])     # a peer failed: raise here too
+
+
+def self_halo_pieces(dim):
+    """The overload rows of a rank that is its own neighbour in every
+    dimension (one rank; periodic), as pieces in store order: piece = the
+    local rows whose flags hold every bit of its mask, in row order.  The
+    reference's loop (redist.py:246-306) on sets of local rows: per dimension
+    to_a = local rows beyond the right face, then the buffer's; to_b the same
+    at the left face; the rank receives its own to_a as from_b and its own
+    to_b as from_a, and buffer = concat(buffer, from_a, from_b) (:305-306).
+    3^dim - 1 pieces: the faces, edges and corners of the halo."""
+    buf = []
+    for d in range(dim):
+        a, b = 1 << (2 * d), 1 << (2 * d + 1)
+        to_a = [a] + [m | a for m in buf]
+        to_b = [b] + [m | b for m in buf]
+        buf = buf + to_b + to_a
+    return buf
+
+
+def _self_halo(transport, sel, srcs, rbs, flags, n, dim, carry_pos, arena, dev):
+    """exchange_overload when every neighbour is this rank: all pieces are
+    known from the local rows' flags, so one selection pass counts them all
+    and one multi-set pack writes every row straight to each of its pieces
+    in the store -- the local rows are read once, not once per dimension,
+    and nothing is staged or received."""
+    pieces = self_halo_pieces(dim)
+    h, cnt = sel.msel_masks(flags, n, pieces, "_self")
+    counts = sel.to_host([cnt])[0]
+    _agree_counts(transport, counts, [])                    # the one host sync
+    total = int(counts.sum())
+    F = len(rbs)
+    if arena is not None and total <= arena[3]:
+        st, base, in_arena = [arena[0]] + ([arena[1]] if carry_pos else []), arena[2], True
+    else:
+        st = [torch.empty(max(total, 1) * rb, dtype=torch.uint8, device=dev) for rb in rbs]
+        base, in_arena = 0, False
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    dsts = [[st[f][(base + int(offs[k])) * rbs[f]:(base + int(offs[k + 1])) * rbs[f]]
+             if counts[k] else None for k in range(len(pieces))] for f in range(F)]
+    if total:
+        sel.msel_pack_fields(h, srcs, rbs, dsts, total)
+    if not total:
+        empty = torch.empty(0, dtype=torch.uint8, device=dev)
+        return empty, (empty if carry_pos else None), 0, in_arena
+    out = [st[f][base * rbs[f]:(base + total) * rbs[f]] for f in range(F)]
+    return out[0], (out[1] if carry_pos else None), total, in_arena
 
 
 def neighbours(R, d, periodic):
@@ -135,12 +193,16 @@ class DeviceSelect:
     def msel(self, flags, n, bits, tag):
         """Counts of the sets {rows with flag bit bits[k]} -> (handle, device
         int64 counts [len(bits)])."""
+        return self.msel_masks(flags, n, [1 << int(b) for b in bits], tag)
+
+    def msel_masks(self, flags, n, masks, tag):
+        """Counts of the sets {rows whose flags hold every bit of masks[k]}."""
         lib = _lib.load()
         tile_rows = SELECT_TILE_ROWS
-        k = len(bits)
+        k = len(masks)
         ws = self._buf("msel_ws" + tag, int(lib.mgr_workspace_bytes(int(n), k, tile_rows)))
         counts = torch.empty(k, dtype=torch.int64, device=self.dev)
-        cb = (ctypes.c_int * k)(*bits)
+        cb = (ctypes.c_int * k)(*[int(m) for m in masks])
         s = _lib.stream_handle()
         _lib.call("mgr_msel_count", _lib.ptr(flags), n, k, cb, tile_rows, _lib.ptr(ws), s)
         _lib.alg_add("halo", 2 * n)                        # the flags, read once
@@ -211,6 +273,9 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
     me = transport.rank
     nb = [neighbours(R, d, periodic) for d in range(dim)]
     selfd = [a == me and b == me for a, b, _, _ in nb]
+    if dim <= 3 and all(selfd) and all(ka and kb for _, _, ka, kb in nb):
+        return _self_halo(transport, sel, srcs[:F - 1], rbs[:F - 1], flags, n, dim, carry_pos,
+                          arena, dev)
 
     # 1. the local rows' counts of every dimension's two selections, one pass
     S = 2 * dim
@@ -232,6 +297,9 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                 ("recv", a, recv_l[2 * d + 1:2 * d + 2].view(torch.uint8))]
     _p2p(transport, ops)
     ls, rl = sel.to_host([send_l, recv_l])                   # host sync 1
+    # a failed selection scan reports -1 counts (here or, through the count
+    # messages, at a neighbour): every rank agrees and raises together
+    _agree_counts(transport, ls, rl)
 
     # the append-only overload store: data (+ positions) + flags
     st = [None] * F
@@ -326,6 +394,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                            ("send", b, send_g[1:2].view(torch.uint8)),
                            ("recv", a, recv_g[1:2].view(torch.uint8))])
             gc, rg = sel.to_host([send_g, recv_g])            # host sync per dimension
+            _agree_counts(transport, gc, rg)
         nla, nlb = local_pieces(d)
         nga, ngb = int(gc[0]), int(gc[1])
         # what it receives: from_b (step 1) and from_a (step 2), each a local

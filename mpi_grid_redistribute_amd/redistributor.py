@@ -200,7 +200,10 @@ class Scratch:
     """Reusable device buffers of one redistributor (workspace, destination
     bytes, send buffers): grown geometrically, never shrunk, so repeated
     calls with varying sizes (skewed counts) stop allocating after the first
-    few.  Stream-ordered reuse: calls on one stream run in order."""
+    few.  Buffers are kept per CUDA stream (the current stream at the call):
+    calls on one stream run in order and reuse them safely; a call on another
+    stream gets buffers of its own, so calls overlapping on two streams never
+    share a workspace or a send buffer."""
 
     GROWTH = 1.25
 
@@ -210,13 +213,14 @@ class Scratch:
 
     def get(self, name, nbytes):
         nbytes = max(int(nbytes), 1)
-        b = self.bufs.get(name)
+        key = (name, torch.cuda.current_stream(self.dev).cuda_stream)
+        b = self.bufs.get(key)
         if b is None or b.numel() < nbytes:
             if b is not None:
                 nbytes = max(nbytes, int(b.numel() * self.GROWTH))
             del b
-            self.bufs.pop(name, None)
-            b = self.bufs[name] = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            self.bufs.pop(key, None)
+            b = self.bufs[key] = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
         return b
 
     def release(self):

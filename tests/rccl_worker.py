@@ -158,6 +158,109 @@ def case_fine_fused(mgr, comm, fine, seed):
         "fine-sorted positions"
 
 
+REC36 = np.dtype([("pos", "f4", 3), ("vel", "f4", 3), ("mass", "f4"), ("id", "i8")])
+
+
+def case_fine_rec36(mgr, comm, fine, seed, as_torch):
+    """BASELINE config 5's exact layout over RCCL: 36-byte records (f32 pos +
+    vel + mass + i64 id), the position the f32 view into the record (the
+    image pack moves the records, the fine cell travels as a u16 side field),
+    fine_cells + return_positions, skewed sizes with an empty rank -- against
+    the oracle's redistribution + fine_cell_ids + stable sort."""
+    topo = TOPO[WORLD]
+    sizes = [int(np.random.default_rng(seed + r).integers(5_000, 60_000)) for r in range(WORLD)]
+    sizes[0] = 0
+    data = []
+    for r, n in enumerate(sizes):
+        rng = np.random.default_rng(seed + 100 + r)
+        rec = np.zeros(n, dtype=REC36)
+        rec["pos"] = rng.uniform(-0.5, 1.5, (n, 3)).astype(np.float32)
+        rec["vel"] = rng.standard_normal((n, 3)).astype(np.float32)
+        rec["mass"] = rng.random(n).astype(np.float32)
+        rec["id"] = np.arange(n) + 1_000_000 * r
+        data.append(rec)
+    pos_o = [np.ascontiguousarray(d["pos"]) for d in data]
+    data_o = [d.copy() for d in data]
+    loc = ro.redistribute_by_position_all_ranks(topo, BOX, WORLD, data_o, [p.copy() for p in pos_o])
+    # the position is a view into the records: the in-place wrap (S1) shows
+    # in the records that travel, so the expected rows carry wrapped positions
+    geos = [ro.Geometry(topo, BOX, WORLD, r) for r in range(WORLD)]
+    wrapped = [p.copy() for p in pos_o]
+    dests = [ro.cell_number_from_position(g, w) for g, w in zip(geos, wrapped)]
+    lpos = ro.redistribute_by_cell_number_all_ranks(WORLD, wrapped, dests)[RANK]
+    src = [d.copy() for d in data]
+    for r in range(WORLD):
+        src[r]["pos"] = wrapped[r]
+    exp_rows = ro.redistribute_by_cell_number_all_ranks(WORLD, src, dests)[RANK]
+    fid = ro.fine_cell_ids(topo, fine, BOX, lpos)
+    exp, exp_off = ro.fine_cell_sort(exp_rows, fid, int(np.prod(fine)))
+    assert len(loc[RANK]) == len(exp_rows)
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    d = data[RANK]
+    if as_torch:
+        raw = torch.from_numpy(d.view(np.uint8).reshape(len(d), 36).copy()).cuda()
+        got, gpos, off = R.redistribute_by_position(raw, raw.view(torch.float32)[:, :3],
+                                                    fine_cells=fine, return_positions=True)
+        off = off.cpu().numpy()
+    else:
+        got, gpos, off = R.redistribute_by_position(d, d["pos"], fine_cells=fine,
+                                                    return_positions=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(as_bytes(got), as_bytes(exp)), "fine-sorted 36-byte records"
+    assert np.array_equal(np.asarray(off), exp_off), "fine offsets"
+    want_pos = np.ascontiguousarray(lpos[np.argsort(fid, kind="stable")])
+    assert np.array_equal(as_bytes(gpos), as_bytes(want_pos)), "fine-sorted positions"
+
+
+def clustered_inputs(seed, sizes, halos=64):
+    """Config-4-style input: per rank, Gaussian halos (centres anywhere in the
+    box, sigma 0.01-0.05, tails leaving the box -> wrapped) plus 20 % uniform
+    background."""
+    pos, data = [], []
+    crng = np.random.default_rng(seed)
+    centres = crng.random((halos, 3))
+    sig = crng.uniform(0.01, 0.05, halos)
+    wts = crng.pareto(1.5, halos) + 0.1
+    wts /= wts.sum()
+    for r, n in enumerate(sizes):
+        rng = np.random.default_rng(seed + 1 + r)
+        h = rng.choice(halos, n, p=wts)
+        p = centres[h] + rng.standard_normal((n, 3)) * sig[h][:, None]
+        bg = rng.random(n) < 0.2
+        p[bg] = rng.random((int(bg.sum()), 3))
+        pos.append(p)
+        data.append(records(n, r, rng))
+    return pos, data
+
+
+def case_clustered(mgr, comm, seed, as_torch):
+    """Heavily skewed counts (Gaussian halos, config 4) with an empty rank,
+    over RCCL, against the oracle."""
+    topo = TOPO[WORLD]
+    sizes = [int(np.random.default_rng(seed + 50 + r).integers(20_000, 80_000))
+             for r in range(WORLD)]
+    sizes[WORLD // 2] = 0
+    pos, data = clustered_inputs(seed, sizes)
+    pos_o = [p.copy() for p in pos]
+    exp = ro.redistribute_by_position_all_ranks(topo, BOX, WORLD, data, pos_o)[RANK]
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    d, p = data[RANK], pos[RANK]
+    if as_torch:
+        d = torch.from_numpy(d.view(np.uint8).reshape(len(d), 32)).cuda()
+        p = torch.from_numpy(p).cuda()
+    out = R.redistribute_by_position(d, p)
+    torch.cuda.synchronize()
+    assert np.array_equal(as_bytes(out), as_bytes(exp)), "clustered output"
+    assert np.array_equal(as_bytes(p), as_bytes(pos_o[RANK])), "wrapped positions"
+    t = R.last_traffic   # xGMI accounting: only rows that left this rank
+    sc = np.bincount(ro.cell_number_from_position(ro.Geometry(topo, BOX, WORLD, RANK),
+                                                  pos[RANK].copy() if not as_torch
+                                                  else p.cpu().numpy().copy()),
+                     minlength=WORLD)
+    sent = sum(int(sc[q]) * 32 + 8 for q in range(WORLD) if q != RANK)
+    assert t["send_bytes"] == sent, (t["send_bytes"], sent)
+
+
 def case_halo_random(mgr, comm, ol, return_positions, seed):
     """The halo over RCCL at larger sizes (flags from the bin kernel, the
     multi-selection packs, grouped p2p): against the oracle; with
@@ -251,6 +354,11 @@ def main():
             ("scan_failure", lambda: case_scan_failure(mgr, comm)),
             ("fine_fused_888", lambda: case_fine_fused(mgr, comm, [8, 8, 8], 21)),
             ("fine_fused_234", lambda: case_fine_fused(mgr, comm, [2, 3, 4], 22)),
+            ("fine_rec36_888", lambda: case_fine_rec36(mgr, comm, [8, 8, 8], 31, False)),
+            ("fine_rec36_888_torch", lambda: case_fine_rec36(mgr, comm, [8, 8, 8], 32, True)),
+            ("fine_rec36_245", lambda: case_fine_rec36(mgr, comm, [2, 4, 5], 33, True)),
+            ("clustered_empty_rank", lambda: case_clustered(mgr, comm, 41, False)),
+            ("clustered_torch", lambda: case_clustered(mgr, comm, 42, True)),
             ("halo_random", lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], False, 23)),
             ("halo_random_positions",
              lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], True, 24)),

@@ -94,12 +94,15 @@ def test_msel_validation(lib):
     any launch."""
     buf = ctypes.create_string_buffer(64)
     p = ctypes.cast(buf, ctypes.c_void_p)
-    bits = (ctypes.c_int * 2)(0, 1)
-    bad = (ctypes.c_int * 2)(0, 16)
+    bits = (ctypes.c_int * 2)(1, 2)                                    # flag masks
+    bad = (ctypes.c_int * 2)(1, 1 << 16)
     assert lib.mgr_msel_count(p, 5, 0, bits, 4096, p, None) < 0        # no sets
     assert b"nsets" in lib.mgr_last_error()
-    assert lib.mgr_msel_count(p, 5, 2, bad, 4096, p, None) < 0         # flag bit 16
-    assert b"flag bit" in lib.mgr_last_error()
+    assert lib.mgr_msel_count(p, 5, 33, bits, 4096, p, None) < 0       # > 32 sets
+    assert lib.mgr_msel_count(p, 5, 2, bad, 4096, p, None) < 0         # mask beyond 16 bits
+    assert b"flag mask" in lib.mgr_last_error()
+    zero = (ctypes.c_int * 2)(0, 1)
+    assert lib.mgr_msel_count(p, 5, 2, zero, 4096, p, None) < 0        # empty mask
     assert lib.mgr_msel_count(p, 5, 2, bits, 100, p, None) < 0         # tile not a multiple of 64
     assert lib.mgr_msel_pack(p, 0, 5, p, 2, bits, 4096, p, p, None) < 0  # row_bytes < 1
     assert b"row_bytes" in lib.mgr_last_error()

@@ -136,6 +136,25 @@ def test_single_rank_scan_failure_raises():
         _lib.tune("scan_spins", 1 << 24)
 
 
+def test_halo_scan_failure_raises():
+    """The halo's selection scans (mgr_msel_count + mgr_scan) failing: the -1
+    counts are checked at the halo's first host sync and raise, instead of
+    turning into negative slices and mismatched messages."""
+    rng = np.random.default_rng(8)
+    n = 200_000
+    pos = rng.random((n, 3))
+    data = np.arange(n)
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    _lib.tune("scan_spins", -1)
+    try:
+        with pytest.raises(_lib.MgrError, match="scan failed"):
+            R.exchange_overload_by_position(data, pos, [0.1, 0.1, 0.1])
+    finally:
+        _lib.tune("scan_spins", 1 << 24)
+    out = R.exchange_overload_by_position(data, pos, [0.1, 0.1, 0.1])
+    assert len(out) > 0
+
+
 def test_no_device_allocation_after_warmup():
     """Skewed inputs of changing size on repeated calls: after warm-up the
     redistributor reuses its scratch (workspace, destination bytes, send

@@ -270,3 +270,61 @@ def test_halo_overload_beyond_cell_length():
     outs = run_ranks(size, fn)
     for r in range(size):
         assert G.same_bytes(outs[r], exp[r]), r
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3])
+@pytest.mark.parametrize("n", [4097, 300_001])
+def test_msel_masks_self_pieces(dim, n):
+    """Selections by flag MASK (a row is in set k when its flags hold every
+    bit of masks[k]): the 3^dim - 1 face / edge / corner pieces of the
+    one-rank halo, up to 26 sets, every set's rows in order, set after set."""
+    from mpi_grid_redistribute_amd.halo import DeviceSelect, self_halo_pieces
+    rng = np.random.default_rng(n + dim)
+    flags = np.zeros(n, dtype=np.uint16)
+    for b in range(2 * dim):   # each face ~15 % of the rows, left/right exclusive
+        flags |= ((rng.random(n) < 0.15).astype(np.uint16) << b)
+    for d in range(dim):
+        both = ((flags >> (2 * d)) & 3) == 3
+        flags[both] &= np.uint16(~(1 << (2 * d + 1)) & 0xFFFF)
+    masks = self_halo_pieces(dim)
+    assert len(masks) == 3 ** dim - 1
+    rb = 36
+    a = rng.integers(0, 256, (n, rb), dtype=np.uint8)
+    sel = DeviceSelect(torch.device("cuda"))
+    fl = torch.from_numpy(flags.view(np.int16)).cuda()
+    h, cnt = sel.msel_masks(fl, n, masks, "_t")
+    want = [a[(flags & m) == m] for m in masks]
+    tot = sum(len(w) for w in want)
+    dst = torch.full((tot * rb + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    starts = np.concatenate([[0], np.cumsum([len(w_) for w_ in want])])
+    src = torch.from_numpy(a.reshape(-1)).cuda()
+    sel.msel_pack_fields(h, [src], [rb], [[dst[starts[k] * rb:starts[k + 1] * rb]
+                                           if len(want[k]) else None for k in range(len(masks))]])
+    torch.cuda.synchronize()
+    assert cnt.cpu().tolist() == [len(w) for w in want]
+    out = dst.cpu().numpy()
+    np.testing.assert_array_equal(out[:tot * rb], np.concatenate(want).reshape(-1))
+    assert (out[tot * rb:] == 0xAB).all()
+
+
+def test_one_rank_halo_vs_oracle():
+    """The one-rank halo (every neighbour is this rank: one selection pass,
+    one multi-set pack) against the oracle, f64 and f32 positions, with and
+    without returned positions."""
+    rng = np.random.default_rng(5)
+    for dt, rp in ((np.float64, False), (np.float32, True)):
+        n = 250_000
+        pos = rng.uniform(-0.2, 1.2, (n, 3)).astype(dt)
+        data = np.zeros(n, dtype=[("x", "f8"), ("y", "f8"), ("z", "f8"), ("id", "i8")])
+        data["id"] = np.arange(n)
+        ol = [0.05, 0.08, 0.03]
+        pos_o = pos.copy()
+        exp = ro.redistribute_by_position_overload_all_ranks([1, 1, 1], [1.0] * 3, 1, [data],
+                                                             [pos_o], ol)[0]
+        R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+        out = R.redistribute_by_position(data, pos, overload_lengths=ol, return_positions=rp)
+        if rp:
+            out, opos = out
+            ids = out["id"]
+            assert np.array_equal(opos.view(np.uint8), pos_o[ids % n].view(np.uint8))
+        assert out.tobytes() == exp.tobytes()

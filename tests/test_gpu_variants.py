@@ -43,9 +43,6 @@ VARIANTS = [
     {"pack_many": 0},
     {"xcd_pack": 4},
     {"xcd_pack": 64, "tile_rounds": 1},
-    {"ranked_rows": 1},
-    {"ranked_rows": 2, "ranked_walk": 1},
-    {"rank_rows": 2048, "ranked_rows": 2},
     {"tile_rounds": 1},
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},

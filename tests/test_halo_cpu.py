@@ -60,8 +60,11 @@ class CpuSelect:
         return torch.from_numpy(f.view(np.int16))
 
     def msel(self, flags, n, bits, tag):
+        return self.msel_masks(flags, n, [1 << int(b) for b in bits], tag)
+
+    def msel_masks(self, flags, n, masks, tag):
         fl = flags.numpy().view(np.uint16)[:n]
-        sets = [np.nonzero((fl >> b) & 1)[0] for b in bits]
+        sets = [np.nonzero((fl & m) == m)[0] for m in masks]
         return sets, torch.tensor([len(s) for s in sets], dtype=torch.int64)
 
     def msel_pack(self, handle, src_flat, row_bytes, dsts):
@@ -253,3 +256,31 @@ def test_threaded_halo_traffic(case):
             + lp.dtype.itemsize * lp.shape[1] + 2          # data + positions + face flags
         extra = int(recv[r].sum()) - m * rb                # the 8-byte count messages
         assert extra % 8 == 0 and 0 < extra <= 8 * 4 * dim, (r, extra)
+
+
+def test_halo_failed_selection_raises():
+    """A selection scan that failed on one rank (-1 counts) makes every rank
+    raise at the count exchange (the -1 travels to the neighbours), instead of
+    posting messages of mismatched sizes."""
+    from mpi_grid_redistribute_amd._lib import MgrError
+
+    class FailingSelect(CpuSelect):
+        def msel(self, flags, n, bits, tag):
+            sets, counts = super().msel(flags, n, bits, tag)
+            return sets, torch.full_like(counts, -1)
+
+    f = G.load("halo_p8_f64_rec32.npz")
+    size = int(f["size"])
+
+    def fn(comm, r):
+        data, pos, periodic = local_inputs(f, "halo_p8_f64_rec32.npz")
+        R = GeoRank(f["topology"], f["box"], size, r)
+        d, p = data[r], pos[r]
+        sel = FailingSelect() if r == 3 else CpuSelect()
+        with pytest.raises(MgrError, match="scan failed"):
+            exchange_overload(R, MpiHostComm(comm), _flat(d), d.dtype.itemsize, _flat(p),
+                              p.shape[1], _lib.MGR_F64, len(d), list(f["overload"]),
+                              periodic=periodic, sel=sel)
+        return True
+
+    assert all(run_ranks(size, fn))
