@@ -175,6 +175,23 @@ int mgr_pack_ids(const void* src, int64_t row_bytes, int64_t n, const void* dest
                  void* redirect_dst, const uint16_t* ids_src, uint16_t* ids_dst,
                  uint16_t* ids_redirect_dst, void* stream);
 
+/* mgr_pack_ids (ids_src NULL: mgr_pack) of the tiles [tile_begin, tile_end)
+ * only (0 <= begin <= end <= the tile count of n, tile_rows): the rows of
+ * those tiles land at their final places, so a caller can pack the tiles in
+ * chunks and start moving each chunk's completed segment prefixes (the
+ * pipelined exchange, exchange.py) while the next chunk is packed.       */
+int mgr_pack_tiles(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
+                   int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
+                   void* redirect_dst, const uint16_t* ids_src, uint16_t* ids_dst,
+                   uint16_t* ids_redirect_dst, int64_t tile_begin, int64_t tile_end,
+                   void* stream);
+/* After mgr_scan: out[i * nbins + b] (device int64) = the first row of bin b
+ * at tile tiles[i] in the packed layout (tiles[i] = the tile count: the bin's
+ * end), i.e. where a chunk of tiles starts inside every bin's segment.
+ * tiles: host array, ntiles <= 4096.                                       */
+int mgr_tile_offsets(const void* workspace, int64_t n, int nbins, int tile_rows,
+                     const int64_t* tiles, int ntiles, int64_t* out, void* stream);
+
 /* The destination-side fine sort in two light steps (config 5).
  * mgr_rank_ids : for n uint16 ids (< nbins), every row's rank among the rows
  *                of its id inside its tile (ranks, uint16 [n]), every tile's

@@ -47,6 +47,9 @@ SIGNATURES = {
     "mgr_scan": (_I, [_I64, _I, _I, _P, _P, _P]),
     "mgr_pack": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P]),
     "mgr_pack_ids": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "mgr_pack_tiles": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _I64, _I64,
+                            _P]),
+    "mgr_tile_offsets": (_I, [_P, _I64, _I, _I, _P, _I, _P, _P]),
     "mgr_partition_by_position": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I64, _P, _P, _P, _I,
                                        _P, _P]),
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),

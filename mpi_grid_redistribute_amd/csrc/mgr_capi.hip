@@ -505,6 +505,48 @@ int mgr_pack_ids(const void* src, int64_t row_bytes, int64_t n, const void* dest
     return MGR_OK;
 }
 
+int mgr_pack_tiles(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nbins,
+                   int drop_bin, int tile_rows, const void* workspace, void* dst, int redirect_bin,
+                   void* redirect_dst, const uint16_t* ids_src, uint16_t* ids_dst,
+                   uint16_t* ids_redirect_dst, int64_t tile_begin, int64_t tile_end,
+                   void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (row_bytes < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes);
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (n > 0 && (!src || !dest || !workspace)) return fail(MGR_EINVAL, "null argument");
+    if (n > 0 && redirect_bin >= 0 && (!redirect_dst || (ids_src && !ids_redirect_dst)))
+        return fail(MGR_EINVAL, "redirect without buffer");
+    if (redirect_bin >= nbins) return fail(MGR_EINVAL, "redirect_bin out of range");
+    mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
+    if (tile_begin < 0 || tile_end < tile_begin || tile_end > ws.T)
+        return fail(MGR_EINVAL, "tiles [%lld, %lld) of %lld", (long long)tile_begin,
+                    (long long)tile_end, (long long)ws.T);
+    if (tile_end == tile_begin) return MGR_OK;
+    ws.t0 = tile_begin;
+    ws.tn = tile_end - tile_begin;
+    HIP_OK(mgr::launch_pack(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
+                            redirect_bin, redirect_dst, (hipStream_t)stream, ids_src, ids_dst,
+                            ids_redirect_dst));
+    return MGR_OK;
+}
+
+int mgr_tile_offsets(const void* workspace, int64_t n, int nbins, int tile_rows,
+                     const int64_t* tiles, int ntiles, int64_t* out, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (nbins < 1 || nbins > MGR_MAX_BINS || ntiles < 0 || ntiles > 4096)
+        return fail(MGR_EINVAL, "nbins %d / ntiles %d", nbins, ntiles);
+    if (ntiles && (!workspace || !tiles || !out)) return fail(MGR_EINVAL, "null argument");
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
+    for (int i = 0; i < ntiles; ++i)
+        if (tiles[i] < 0 || tiles[i] > ws.T) return fail(MGR_EINVAL, "tile %lld of %lld",
+                                                         (long long)tiles[i], (long long)ws.T);
+    if (!ntiles) return MGR_OK;
+    HIP_OK(mgr::launch_tile_offsets(ws, nbins, tiles, ntiles, out, (hipStream_t)stream));
+    return MGR_OK;
+}
+
 int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n,
                               int64_t row_stride, int periodic, const void* src,
                               int64_t row_bytes, void* dst, void* dest, int64_t* bin_counts,

@@ -542,15 +542,29 @@ struct SetMasks {
     uint16_t m[kMaxSets];
 };
 
+// The chunk's flag bit-planes (plane b, bit j: the lane's row j has flag bit
+// b) for the bits below nbits (the bits any set uses): computed once per
+// chunk, every set's membership is then an AND of planes.
+struct FlagPlanes {
+    uint32_t p[16];
+};
+__device__ __forceinline__ void flag_planes(const uint32_t (&fw)[kSelWords], int nbits,
+                                            FlagPlanes& fp) {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) fp.p[b] = b < nbits ? set_mask(fw, b) : 0xFFFFu;
+}
 // bit j of the result: the lane's row j has every flag bit of mask
-__device__ __forceinline__ uint32_t set_mask_m(const uint32_t (&fw)[kSelWords], unsigned mask) {
+__device__ __forceinline__ uint32_t set_mask_m(const FlagPlanes& fp, unsigned mask, int nbits) {
     uint32_t r = 0xFFFFu;
-    while (mask) {
-        const int b = __builtin_ctz(mask);
-        mask &= mask - 1u;
-        r &= set_mask(fw, b);
-    }
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if (b < nbits) r &= ((mask >> b) & 1u) ? fp.p[b] : 0xFFFFu;
     return r;
+}
+__device__ __forceinline__ int mask_bits(const SetMasks& sm, int nsets) {
+    unsigned u = 0;
+    for (int k = 0; k < nsets; ++k) u |= sm.m[k];
+    return u ? 32 - __builtin_clz(u) : 0;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {

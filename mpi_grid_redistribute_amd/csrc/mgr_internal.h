@@ -77,6 +77,7 @@ struct Workspace {
                          // by the count producers (bin_count, bin_ids, select_count)
     const uint32_t* scan_err;  // &ScanCtl::err: packs return at once when set
     int64_t T;
+    int64_t t0 = 0, tn = 0;    // the tiles [t0, t0 + tn) one pack launch covers (all: 0, T)
 };
 int64_t num_tiles(int64_t n, int tile_rows);
 int64_t workspace_bytes(int64_t n, int nbins, int tile_rows);
@@ -126,6 +127,8 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
+hipError_t launch_tile_offsets(const Workspace& ws, int nbins, const int64_t* tiles, int ntiles,
+                               int64_t* out, hipStream_t s);
 int ranked_tile_rows(int64_t row_bytes, int nbins);
 hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);

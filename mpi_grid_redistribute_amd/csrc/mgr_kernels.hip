@@ -283,12 +283,15 @@ __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __re
     int c[kMaxSets];
 #pragma unroll
     for (int k = 0; k < kMaxSets; ++k) c[k] = 0;
+    const int nbits = mask_bits(masks, nsets);
     for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
         uint32_t fw[kSelWords];
         chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
+        FlagPlanes fp;
+        flag_planes(fw, nbits, fp);
 #pragma unroll
         for (int k = 0; k < kMaxSets; ++k)
-            if (k < nsets) c[k] += __popc(set_mask_m(fw, masks.m[k]));
+            if (k < nsets) c[k] += __popc(set_mask_m(fp, masks.m[k], nbits));
     }
 #pragma unroll
     for (int k = 0; k < kMaxSets; ++k) {
@@ -309,6 +312,35 @@ hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const 
                        nsets, sm, ws.counts, ws.T, tile_rows, ws.flags);
     prof_end(s, K_HALO);
     return hipGetLastError();
+}
+
+// Offsets of chosen tile boundaries (mgr_tile_offsets): out[i][b] = the first
+// row of bin b at tile tiles[i] in the packed layout (offsets[b][t]; at t = T
+// the bin's end, bin_starts[b + 1]).  The tiles ride in the kernarg segment.
+struct TileList {
+    int64_t t[64];
+};
+__global__ void tile_offsets_kernel(const int64_t* __restrict__ offsets,
+                                    const int64_t* __restrict__ bin_starts, int64_t T, int nbins,
+                                    TileList tl, int ntiles, int64_t* __restrict__ out) {
+    const int i = blockIdx.x, b = threadIdx.x + blockIdx.y * blockDim.x;
+    if (i >= ntiles || b >= nbins) return;
+    const int64_t t = tl.t[i];
+    out[(int64_t)i * nbins + b] = t >= T ? bin_starts[b + 1] : offsets[(int64_t)b * T + t];
+}
+
+hipError_t launch_tile_offsets(const Workspace& ws, int nbins, const int64_t* tiles, int ntiles,
+                               int64_t* out, hipStream_t s) {
+    for (int i0 = 0; i0 < ntiles; i0 += 64) {
+        TileList tl{};
+        const int k = ntiles - i0 < 64 ? ntiles - i0 : 64;
+        for (int i = 0; i < k; ++i) tl.t[i] = tiles[i0 + i];
+        hipLaunchKernelGGL(tile_offsets_kernel, dim3(k, (nbins + 255) / 256), dim3(256), 0, s,
+                           ws.offsets, ws.bin_starts, ws.T, nbins, tl, k, out + (int64_t)i0 * nbins);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // --------------------------------------------------------- synthetic data
@@ -373,6 +405,8 @@ int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
 Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
     Workspace ws;
     ws.T = num_tiles(n, tile_rows);
+    ws.t0 = 0;
+    ws.tn = ws.T;
     const int64_t M = (int64_t)nbins * (ws.T > 0 ? ws.T : 1);
     char* p = (char*)base;
     ws.counts = (int32_t*)p;     p += a256(M * 4);

@@ -19,13 +19,14 @@ __global__ __launch_bounds__(kBlock) void pack_kernel(
     const uint8_t* __restrict__ src, int64_t upr /* W-units per row */, int64_t n,
     const DestT* __restrict__ dest, int nb, int nbits, int drop_bin,
     const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts, int64_t T,
-    int tile_rows, int per_wave_lds, uint8_t* __restrict__ dst, int redirect_bin,
-    uint8_t* __restrict__ redirect_dst, const uint32_t* __restrict__ scan_err) {
+    int64_t t0, int64_t tn, int tile_rows, int per_wave_lds, uint8_t* __restrict__ dst,
+    int redirect_bin, uint8_t* __restrict__ redirect_dst, const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
-    if (tile >= T || scan_failed(scan_err)) return;
+    const int64_t tl = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+    if (tl >= tn || scan_failed(scan_err)) return;
+    const int64_t tile = t0 + tl;
     int64_t* goff = (int64_t*)(smem + w * per_wave_lds);
     int32_t* run = (int32_t*)(smem + w * per_wave_lds + align16(nb * 8));
     for (int b = lane; b < nb; b += 64) {
@@ -89,14 +90,14 @@ template <int W, int UPR, int RPW>
 __global__ __launch_bounds__(1024) void pack_coop_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd, int sel,
-    const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
+    const int64_t* __restrict__ bin_starts, int64_t T, int64_t t0, int64_t tn, int tile_rows,
+    uint8_t* __restrict__ dst, int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
+    int sel, const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     using U = typename Unit<W>::T;
     __shared__ int s_cnt[kCoopMaxRounds][64];
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = xcd ? xcd_tile_c(blockIdx.x, T, xcd) : (int64_t)blockIdx.x;
+    const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
     // wave w moves rounds w*RPW .. w*RPW+RPW-1 of the tile
     const int64_t row0 = tile * (int64_t)tile_rows + 64 * RPW * w;
     // issue every load of the wave's rounds first
@@ -182,13 +183,14 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
 template <int W, int UPR>
 __global__ __launch_bounds__(256) void compact_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
-    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err) {
+    const int64_t* __restrict__ offsets, int64_t T, int64_t t0, int64_t tn, int tile_rows,
+    uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     constexpr int D = 4;   // rounds per batch (8 measured the same: sparse rows cost whole lines)
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
-    if (tile >= T || scan_failed(scan_err)) return;
+    const int64_t tl = (int64_t)blockIdx.x * 4 + w;
+    if (tl >= tn || scan_failed(scan_err)) return;
+    const int64_t tile = t0 + tl;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     long long base = offsets[tile];          // bin 0 (kept) segment of the tile
@@ -334,9 +336,12 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         }
     }
     wave_sync();
+    const int nbits = mask_bits(masks, nsets);
     for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
         uint32_t fw[kSelWords];
         chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
+        FlagPlanes fp;
+        flag_planes(fw, nbits, fp);
         auto flush = [&](int fill) {
             wave_sync();
             for (int f = 0; f < nf; ++f) {
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         int fill = 0;
         for (int k = 0; k < nsets; ++k) {
             if (!((live >> k) & 1u)) continue;
-            uint32_t m = set_mask_m(fw, masks.m[k]);
+            uint32_t m = set_mask_m(fp, masks.m[k], nbits);
             int total;
             int pos = wave_excl(__popc(m), &total);
             if (!total) continue;
@@ -416,12 +421,13 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
 template <int W>
 __global__ __launch_bounds__(256) void compact_any_kernel(
     const uint8_t* __restrict__ src, int64_t upr, int64_t n, const uint8_t* __restrict__ dest,
-    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err) {
+    const int64_t* __restrict__ offsets, int64_t T, int64_t t0, int64_t tn, int tile_rows,
+    uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
-    if (tile >= T || scan_failed(scan_err)) return;
+    const int64_t tl = (int64_t)blockIdx.x * 4 + w;
+    if (tl >= tn || scan_failed(scan_err)) return;
+    const int64_t tile = t0 + tl;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
     long long base = offsets[tile];
@@ -442,13 +448,13 @@ __global__ __launch_bounds__(256) void compact_any_kernel(
 template <int W>
 static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                             int tile_rows, const Workspace& ws, void* dst, hipStream_t s) {
-    const dim3 grid((unsigned)((ws.T + 3) / 4));
+    const dim3 grid((unsigned)((ws.tn + 3) / 4));
     const int upr = (int)(row_bytes / W);
 #define MGR_CK(U_)                                                                             \
     case U_:                                                                                   \
         hipLaunchKernelGGL((compact_kernel<W, U_>), grid, dim3(256), 0, s, (const uint8_t*)src, \
-                           n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows, (uint8_t*)dst, \
-                           ws.scan_err);                                                          \
+                           n, (const uint8_t*)dest, ws.offsets, ws.T, ws.t0, ws.tn, tile_rows,  \
+                           (uint8_t*)dst, ws.scan_err);                                         \
         return hipGetLastError();
     if (64 * W <= 1024 || upr <= 4) {
         switch (upr) {
@@ -470,8 +476,8 @@ static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const
     }
 #undef MGR_CK
     hipLaunchKernelGGL(compact_any_kernel<W>, grid, dim3(256), 0, s, (const uint8_t*)src,
-                       row_bytes / W, n, (const uint8_t*)dest, ws.offsets, ws.T, tile_rows,
-                       (uint8_t*)dst, ws.scan_err);
+                       row_bytes / W, n, (const uint8_t*)dest, ws.offsets, ws.T, ws.t0, ws.tn,
+                       tile_rows, (uint8_t*)dst, ws.scan_err);
     return hipGetLastError();
 }
 
@@ -531,8 +537,8 @@ template <int RB, int RPW, bool SEL>
 __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
+    const int64_t* __restrict__ bin_starts, int64_t T, int64_t t0, int64_t tn, int tile_rows,
+    uint8_t* __restrict__ dst, int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
     const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
     static_assert(RB % 4 == 0 && RB % 16 != 0 && RB <= 64, "image pack row size");
@@ -549,7 +555,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     unsigned long long* gaddr = (unsigned long long*)(img + RBYTES);
     uint8_t* ibin = img + RBYTES + 64 * 8;
     uint32_t* imgw = (uint32_t*)img;
-    const int64_t tile = xcd ? xcd_tile_c(blockIdx.x, T, xcd) : (int64_t)blockIdx.x;
+    const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
     const int64_t row0 = tile * (int64_t)tile_rows + (int64_t)WR * w;
     const int nrows = (int)max((int64_t)0, min((int64_t)WR, n - row0));
     const int nbytes = nrows * RB;
@@ -690,8 +696,8 @@ template <int W, int UPR, typename DestT, int RPW>
 __global__ __launch_bounds__(1024) void pack_many_kernel(
     const uint8_t* __restrict__ src, int64_t n, const DestT* __restrict__ dest, int nb,
     int nbits, int drop_bin, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ bin_starts, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
+    const int64_t* __restrict__ bin_starts, int64_t T, int64_t t0, int64_t tn, int tile_rows,
+    uint8_t* __restrict__ dst, int redirect_bin, uint8_t* __restrict__ redirect_dst, int xcd,
     const uint32_t* __restrict__ scan_err) {
     using U = typename Unit<W>::T;
     constexpr int R = 16 * RPW;                                // rounds per super-round
@@ -699,7 +705,7 @@ __global__ __launch_bounds__(1024) void pack_many_kernel(
     long long* s_off = (long long*)smem;                       // [nb] running bin bases
     uint16_t* tab = (uint16_t*)(smem + align16(nb * 8));       // [R][nb]
     const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = xcd ? xcd_tile_c(blockIdx.x, T, xcd) : (int64_t)blockIdx.x;
+    const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
     if (scan_failed(scan_err)) return;
     for (int bb = threadIdx.x; bb < nb; bb += blockDim.x)
         s_off[bb] = seg_start(offsets, bin_starts, T, tile, bb, redirect_bin);
@@ -853,10 +859,11 @@ static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const vo
     const int wpb = waves_per_block(per_wave);
     const int lds = per_wave * wpb;
     ensure_lds(k, lds);
-    const int64_t grid = (ws.T + wpb - 1) / wpb;
+    const int64_t grid = (ws.tn + wpb - 1) / wpb;
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * wpb), (size_t)lds, s,
                        (const uint8_t*)src, row_bytes / W, n, (const DestT*)dest, nb,
-                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows,
+                       nbits_for(nb), drop_bin, ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn,
+                       tile_rows,
                        per_wave, (uint8_t*)dst, redirect_bin, (uint8_t*)redirect_dst, ws.scan_err);
     return hipGetLastError();
 }
@@ -870,9 +877,10 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
     const int rpw = tile_rows > 1024 ? 2 : 1;
     const int threads = tile_rows / rpw;
 #define MGR_PCK(RPW_)                                                                         \
-    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_>), dim3((unsigned)ws.T), dim3(threads), 0, \
+    hipLaunchKernelGGL((pack_coop_kernel<W, UPR, RPW_>), dim3((unsigned)ws.tn), dim3(threads), 0, \
                        s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),     \
-                       drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst,    \
+                       drop_bin, ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows,     \
+                       (uint8_t*)dst,                                                          \
                        redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel, ws.scan_err, \
                        side ? side->src : nullptr, side ? side->dst : nullptr,         \
                        side ? side->red : nullptr)
@@ -926,9 +934,10 @@ static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int 
     {                                                                                          \
         auto k = pack_many_kernel<W, UPR, DestT, RPW_>;                                        \
         ensure_lds(k, lds);                                                                    \
-        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,                \
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.tn), dim3(1024), (size_t)lds, s,               \
                            (const uint8_t*)src, n, (const DestT*)dest, nb, nbits_for(nb),      \
-                           drop_bin, ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, \
+                           drop_bin, ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows, \
+                           (uint8_t*)dst,                                                      \
                            redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err); \
     }
     if (round_rows == 4096) MGR_PMK(4)
@@ -980,9 +989,10 @@ static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int n
     auto k = sel ? (rpw == 2 ? pack_img_kernel<RB, 2, true> : pack_img_kernel<RB, 1, true>)
                  : (rpw == 2 ? pack_img_kernel<RB, 2, false> : pack_img_kernel<RB, 1, false>);
     ensure_lds(k, lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s,
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.tn), dim3(64 * nw), (size_t)lds, s,
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
-                       ws.offsets, ws.bin_starts, ws.T, tile_rows, (uint8_t*)dst, redirect_bin,
+                       ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows, (uint8_t*)dst,
+                       redirect_bin,
                        (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err,
                        side ? side->src : nullptr, side ? side->dst : nullptr,
                        side ? side->red : nullptr);
@@ -1075,8 +1085,20 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         }
         __syncthreads();
         const int nbytes = tr * RB;
+        // (the image pack's two-address unit store, store_img_unit, measured
+        // 12 % slower here, same box: profiles/round3/ab_notes.md)
         auto unit = [&](int x) __attribute__((always_inline)) {
-            store_img_unit<RB, false>((const uint8_t*)img, ibin, gaddr, x, nbytes);
+            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
+            const int bf = ibin[x / RB];
+            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+                gstore<u32x4_a4>(gaddr[bf] + x, q);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
+                }
+            }
         };
         if constexpr (UNR) {
             // unrolled: no store loop whose preheader would wait (vmcnt 0)

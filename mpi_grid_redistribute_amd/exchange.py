@@ -97,3 +97,93 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
                             lay.recv_offsets)
     transport.note_rows(row_bytes, sc, rc)
     return outs, lay
+
+
+def exchange_pipelined(transport, row_bytes, bin_counts, rank, device, chunk_offsets, pack_chunk,
+                       nchunks, extra_rows=None, scratch=None):
+    """exchange() with the pack and the row transfers overlapped: the tiles are
+    packed in ``nchunks`` consecutive chunks, and as soon as chunk c is packed
+    its rows travel -- every bin's rows of one chunk of tiles are a
+    contiguous piece of that bin's segment, so chunk c of peer p is one
+    message -- while chunk c + 1 is being packed (the messages run on a
+    stream of their own, ordered after chunk c's pack by an event).
+
+    ``chunk_offsets()`` -> host int64 [nchunks + 1][size]: the first row of
+    every bin at each chunk boundary in the packed (bin-major) layout, i.e.
+    the scan's offsets at the boundary tiles (mgr_tile_offsets).
+    ``pack_chunk(c, sends, outs, redirect_bin, out_offsets)`` packs chunk c of
+    every field (the self rows straight into the output, as exchange()'s
+    pack).  The per-chunk counts travel to the peers first (k int64 each way
+    per peer), so every receive is posted with its exact size.  Output bytes
+    and order are exactly exchange()'s (receives in source-rank order, S7)."""
+    sc, rc = transport.exchange_counts(bin_counts)
+    size = len(sc)
+    for p in range(size):
+        transport.note("send", p, 8)
+        transport.note("recv", p, 8)
+    check_counts(sc, rc)
+    # the self rows always go straight into the output (the pack's redirect),
+    # whatever the transport: only the other peers' pieces travel
+    lay = plan_layout(sc, rc, rank, True)
+    off = np.asarray(chunk_offsets(), dtype=np.int64).reshape(nchunks + 1, size)
+    cs = np.diff(off, axis=0)                                  # [chunk][peer] rows sent
+    if not np.array_equal(cs.sum(axis=0), sc):
+        raise MgrError(f"chunk offsets do not add up to the send counts: {cs.sum(axis=0)} vs {sc}")
+    # every peer's chunk counts for this rank (k int64 each way per peer)
+    send_c = torch.from_numpy(np.ascontiguousarray(cs.T)).to(device)      # [peer][chunk]
+    recv_c = torch.zeros_like(send_c)
+    ops = []
+    for j in range(1, size):   # ring order, as the row exchange
+        to, frm = (rank + j) % size, (rank - j) % size
+        ops.append(("send", to, send_c[to].view(torch.uint8)))
+        ops.append(("recv", frm, recv_c[frm].view(torch.uint8)))
+    transport.note_p2p(ops)
+    transport.p2p(ops)
+    cr = recv_c.cpu().numpy()                                  # [peer][chunk] rows received
+    cr[rank] = cs[:, rank]
+    if not np.array_equal(cr.sum(axis=1), rc):
+        raise MgrError(f"peers' chunk counts {cr.sum(axis=1)} do not add up to {rc}")
+    extra = int(extra_rows(lay.total_recv)) if extra_rows is not None else 0
+    outs, sends = [], []
+    for f, rb in enumerate(row_bytes):
+        outs.append(torch.empty(max((lay.total_recv + extra) * rb, 1), dtype=torch.uint8,
+                                device=device))
+        nbytes = max(lay.total_send * rb, 1)
+        sends.append(scratch(f"send{f}", nbytes) if scratch is not None
+                     else torch.empty(nbytes, dtype=torch.uint8, device=device))
+    redirect = rank
+    offs = [int(lay.recv_offsets[rank]) * rb for rb in row_bytes]
+    gpu = isinstance(device, torch.device) and device.type == "cuda" or str(device).startswith("cuda")
+    compute = torch.cuda.current_stream() if gpu else None
+    comm = torch.cuda.Stream(device=device) if gpu else None
+    sent_c = np.zeros(size, dtype=np.int64)     # rows of each peer's segment already sent
+    recv_at = np.zeros(size, dtype=np.int64)    # rows of each source already received
+    for c in range(nchunks):
+        pack_chunk(c, sends, outs, redirect, offs)
+        ops = []
+        for j in range(1, size):
+            to, frm = (rank + j) % size, (rank - j) % size
+            for f, rb in enumerate(row_bytes):
+                if cs[c, to]:
+                    a = int(lay.send_offsets[to] + sent_c[to]) * rb
+                    ops.append(("send", to, sends[f][a:a + int(cs[c, to]) * rb]))
+                if cr[frm, c]:
+                    a = int(lay.recv_offsets[frm] + recv_at[frm]) * rb
+                    ops.append(("recv", frm, outs[f][a:a + int(cr[frm, c]) * rb]))
+        for j in range(1, size):
+            sent_c[(rank + j) % size] += cs[c, (rank + j) % size]
+            recv_at[(rank - j) % size] += cr[(rank - j) % size, c]
+        if not ops:
+            continue
+        if comm is not None:
+            comm.wait_stream(compute)              # chunk c is packed
+            with torch.cuda.stream(comm):
+                transport.p2p(ops)
+        else:
+            transport.p2p(ops)
+    if comm is not None:
+        compute.wait_stream(comm)
+        for t in outs + sends:
+            t.record_stream(comm)
+    transport.note_rows(row_bytes, sc, rc)
+    return outs, lay

@@ -39,7 +39,7 @@ import torch
 from . import _lib
 from ._arrays import Positions, Rows, box_dtype_code, device, id_array
 from .comm import SelfComm, as_transport
-from .exchange import check_counts, exchange
+from .exchange import check_counts, exchange, exchange_pipelined
 from .halo import DeviceSelect, exchange_overload, halo_capacity, thresholds
 
 
@@ -281,6 +281,9 @@ class MPIGridRedistributor:
         self._fine_plans = {}
         self._dev = device()
         self._scratch = Scratch(self._dev)
+        # > 1: the pack and the row exchange overlap in this many chunks of
+        # tiles (exchange_pipelined); 1: pack everything, then one exchange
+        self.exchange_chunks = 1
 
     # ------------------------------------------------------ binning (L1)
     def get_cell_indexes_from_position(self, position, periodic=True):
@@ -607,6 +610,42 @@ class MPIGridRedistributor:
             for f in range(2, len(fields)):
                 pack(f, sends[f], redirect_bin, outs[f] if r else None, offs[f])
 
+        T = (n + tile_rows - 1) // tile_rows
+        k = min(int(self.exchange_chunks), T)
+        if k > 1 and P > 1:
+            # pipelined: pack the tiles in k chunks, each chunk's pieces travel
+            # while the next is packed (exchange_pipelined)
+            bounds = [T * c // k for c in range(k + 1)]
+
+            def chunk_offsets():
+                out = torch.empty((k + 1) * nb, dtype=torch.int64, device=self._dev)
+                arr = (ctypes.c_int64 * (k + 1))(*bounds)
+                _lib.call("mgr_tile_offsets", _lib.ptr(ws), n, nb, tile_rows, arr, k + 1,
+                          _lib.ptr(out), stream)
+                return out.view(k + 1, nb)[:, :P].cpu().numpy()
+
+            def pack_chunk(c, sends, outs, redirect_bin, offs):
+                t0, t1 = bounds[c], bounds[c + 1]
+                first = 0
+                if side_ids:   # field 1: the 2-byte side field of field 0, same pass
+                    _lib.call("mgr_pack_tiles", _lib.ptr(fields[0].flat), fields[0].row_bytes, n,
+                              _lib.ptr(dest), nb, P if drop else -1, tile_rows, _lib.ptr(ws),
+                              _lib.ptr(sends[0]), redirect_bin, red_ptr(outs[0], offs[0]),
+                              _lib.ptr(fields[1].flat), _lib.ptr(sends[1]),
+                              red_ptr(outs[1], offs[1]), t0, t1, stream)
+                    first = 2
+                for f in range(first, len(fields)):
+                    fld = fields[f]
+                    _lib.call("mgr_pack_tiles", _lib.ptr(fld.flat), fld.row_bytes, n,
+                              _lib.ptr(dest), nb, P if drop else -1, tile_rows, _lib.ptr(ws),
+                              _lib.ptr(sends[f]), redirect_bin, red_ptr(outs[f], offs[f]),
+                              None, None, None, t0, t1, stream)
+
+            outs, lay = exchange_pipelined(self.comm, [f.row_bytes for f in fields],
+                                           bin_counts[:P], self.rank, self._dev, chunk_offsets,
+                                           pack_chunk, k, extra_rows=extra_rows,
+                                           scratch=self._scratch.get)
+            return outs, lay.total_recv
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
                              self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
                              pack_all=pack_all if side_ids else None)

@@ -110,12 +110,13 @@ def rank_inputs(seed, sizes, lo=-0.5, hi=1.5, hot=None):
     return pos, data
 
 
-def case_random(mgr, comm, sizes, seed, as_torch, hot=None, return_positions=False):
+def case_random(mgr, comm, sizes, seed, as_torch, hot=None, return_positions=False, chunks=1):
     topo = TOPO[WORLD]
     pos, data = rank_inputs(seed, sizes, hot=hot)
     pos_o = [p.copy() for p in pos]
     exp = ro.redistribute_by_position_all_ranks(topo, BOX, WORLD, data, pos_o)[RANK]
     R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    R.exchange_chunks = chunks
     d, p = data[RANK], pos[RANK]
     if as_torch:
         d = torch.from_numpy(d.view(np.uint8).reshape(len(d), 32)).cuda()
@@ -161,7 +162,7 @@ def case_fine_fused(mgr, comm, fine, seed):
 REC36 = np.dtype([("pos", "f4", 3), ("vel", "f4", 3), ("mass", "f4"), ("id", "i8")])
 
 
-def case_fine_rec36(mgr, comm, fine, seed, as_torch):
+def case_fine_rec36(mgr, comm, fine, seed, as_torch, chunks=1):
     """BASELINE config 5's exact layout over RCCL: 36-byte records (f32 pos +
     vel + mass + i64 id), the position the f32 view into the record (the
     image pack moves the records, the fine cell travels as a u16 side field),
@@ -196,6 +197,7 @@ def case_fine_rec36(mgr, comm, fine, seed, as_torch):
     exp, exp_off = ro.fine_cell_sort(exp_rows, fid, int(np.prod(fine)))
     assert len(loc[RANK]) == len(exp_rows)
     R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    R.exchange_chunks = chunks
     d = data[RANK]
     if as_torch:
         raw = torch.from_numpy(d.view(np.uint8).reshape(len(d), 36).copy()).cuda()
@@ -261,7 +263,7 @@ def case_clustered(mgr, comm, seed, as_torch):
     assert t["send_bytes"] == sent, (t["send_bytes"], sent)
 
 
-def case_halo_random(mgr, comm, ol, return_positions, seed):
+def case_halo_random(mgr, comm, ol, return_positions, seed, chunks=1):
     """The halo over RCCL at larger sizes (flags from the bin kernel, the
     multi-selection packs, grouped p2p): against the oracle; with
     return_positions the positions travel as a third field."""
@@ -271,6 +273,7 @@ def case_halo_random(mgr, comm, ol, return_positions, seed):
     pos_o = [p.copy() for p in pos]
     exp = ro.redistribute_by_position_overload_all_ranks(topo, BOX, WORLD, data, pos_o, ol)[RANK]
     R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    R.exchange_chunks = chunks
     out = R.redistribute_by_position(data[RANK], pos[RANK], overload_lengths=ol,
                                      return_positions=return_positions)
     torch.cuda.synchronize()
@@ -357,6 +360,15 @@ def main():
             ("fine_rec36_888", lambda: case_fine_rec36(mgr, comm, [8, 8, 8], 31, False)),
             ("fine_rec36_888_torch", lambda: case_fine_rec36(mgr, comm, [8, 8, 8], 32, True)),
             ("fine_rec36_245", lambda: case_fine_rec36(mgr, comm, [2, 4, 5], 33, True)),
+            ("pipelined_empty_rank", lambda: case_random(mgr, comm, sizes, 51, True, chunks=3)),
+            ("pipelined_large", lambda: case_random(mgr, comm, [300_000] * WORLD, 52, True,
+                                                    chunks=4)),
+            ("pipelined_skewed", lambda: case_random(mgr, comm, [40_000] * WORLD, 53, False,
+                                                     hot=[0.5, 0.0, 0.0], chunks=2)),
+            ("pipelined_fine_rec36", lambda: case_fine_rec36(mgr, comm, [8, 8, 8], 54, True,
+                                                             chunks=3)),
+            ("pipelined_halo", lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], True, 55,
+                                                        chunks=3)),
             ("clustered_empty_rank", lambda: case_clustered(mgr, comm, 41, False)),
             ("clustered_torch", lambda: case_clustered(mgr, comm, 42, True)),
             ("halo_random", lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], False, 23)),

@@ -126,6 +126,71 @@ def test_threaded_mpi_host_comm_redirect():
         assert outs[r].tobytes() == expect[r].tobytes(), r
 
 
+def chunked_oracle_pack(data, dest, size, rb, nchunks):
+    """Stand-in for mgr_pack_tiles: the rows split into nchunks row ranges
+    (the tile chunks); chunk c's rows of every bin go to their final places
+    -- bin-major, stable, the redirect bin straight into the output.
+    Returns (chunk_offsets() -> [nchunks+1][size], pack_chunk, counts)."""
+    n = len(data)
+    raw = np.ascontiguousarray(data).view(np.uint8).reshape(n, rb)
+    bounds = [n * c // nchunks for c in range(nchunks + 1)]
+    counts = np.bincount(dest, minlength=size).astype(np.int64)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    off = np.array([[starts[b] + int(np.sum(dest[:bounds[c]] == b)) for b in range(size)]
+                    for c in range(nchunks + 1)], dtype=np.int64)
+
+    def pack_chunk(c, sends, outs, redirect_bin, offs):
+        for b in range(size):
+            rows = np.nonzero(dest[bounds[c]:bounds[c + 1]] == b)[0] + bounds[c]
+            if not len(rows):
+                continue
+            seg = torch.from_numpy(raw[rows].reshape(-1).copy())
+            o = off[c][b] - starts[b]          # rows of bin b in earlier chunks
+            if b == redirect_bin:
+                outs[0][offs[0] + o * rb: offs[0] + (o + len(rows)) * rb].copy_(seg)
+            else:
+                g = starts[b] - (counts[redirect_bin] if 0 <= redirect_bin < b else 0) + o
+                sends[0][g * rb:(g + len(rows)) * rb].copy_(seg)
+
+    return (lambda: off), pack_chunk, torch.from_numpy(counts)
+
+
+def _gloo_pipelined_worker(rank, size, port, empty_rank, nchunks):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        from mpi_grid_redistribute_amd.exchange import exchange_pipelined
+        topo = [size, 1, 1]
+        pos, data = make_rank_inputs(size, seed=31 + size, empty_rank=empty_rank)
+        rb = data[0].dtype.itemsize
+        expect = ro.redistribute_by_position_all_ranks(topo, BOX, size, data,
+                                                       [p.copy() for p in pos])[rank]
+        dest = ro.cell_number_from_position(ro.Geometry(topo, BOX, size, rank), pos[rank].copy())
+        offs_fn, pack_chunk, counts = chunked_oracle_pack(data[rank], dest, size, rb, nchunks)
+        comm = TorchDistComm()
+        comm.reset_traffic()
+        outs, lay = exchange_pipelined(comm, [rb], counts, rank, "cpu", offs_fn, pack_chunk,
+                                       nchunks)
+        got = outs[0][: lay.total_recv * rb].numpy()
+        assert got.tobytes() == np.ascontiguousarray(expect).view(np.uint8).tobytes()
+        sent = sum(int(counts[p]) * rb for p in range(size) if p != rank)
+        assert comm.traffic.send.sum() == sent + 8 * (size - 1) * (1 + nchunks)
+        comm.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,empty_rank,nchunks", [(2, None, 3), (3, 1, 2), (3, None, 5)])
+def test_gloo_pipelined_exchange(size, empty_rank, nchunks):
+    """The pipelined exchange (pack in chunks, each chunk's pieces sent while
+    the next is packed) gives exchange()'s bytes: gloo ranks, the oracle's
+    stable partition as the chunked pack, empty ranks, more chunks than rows
+    of some bins."""
+    mp.spawn(_gloo_pipelined_worker, args=(size, _free_port(), empty_rank, nchunks), nprocs=size,
+             join=True)
+
+
 # ------------------------------------------------ the RCCL schedule (host)
 class _SimWorld:
     """Shared state of the simulated RCCL group: per (src, dst) FIFO of the
