@@ -408,31 +408,42 @@ __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __res
     for (int b = threadIdx.x; b < nbins; b += kBlock) counts[(int64_t)b * T + tile] = hist[b];
 }
 
-// Stable ranks of u16 bin ids (the fine cells at the destination, config 5)
-// for mgr_pack_ranked: one 256-thread workgroup per tile of TR rows (4 waves
-// x RPW rounds, in order).  Per row: its rank among the tile's rows of its
-// bin (ballot match + wave-private running counts + a prefix over the
-// waves); per tile: every bin's start inside the tile (tile_starts[t][b],
-// tile-major, contiguous) and its count (counts[b * T + t], for mgr_scan).
-// The ranking work leaves the pack, which then only places rows.
-// RPW > 0 / NBITS > 0: the rounds per wave and the id bits at compile time
-// (the ranked tiles of mgr_ranked_tile_rows, 512 cells): unrolled rounds in
-// named registers and an unrolled ballot match; 0: read at run time.
-template <int NW, int RPW, int NBITS>
+// Stable tile slots of u16 bin ids (the fine cells at the destination, config
+// 5) for mgr_pack_ranked: one 256-thread workgroup per tile of TR rows (4
+// waves x RPW rounds, in order).  Per row: its slot in the tile's bin-sorted
+// order = the tile's start of its bin + the wave prefix of the bin + its rank
+// among the wave's earlier rows of the bin; per tile: every bin's start inside
+// the tile (tile_starts[t][b], tile-major, contiguous) and its count (counts[b
+// * T + t], for mgr_scan).  The ranking work leaves the pack, which then only
+// places rows.
+// ORM: a round's peers by LDS atomics -- every lane ORs its lane bit into its
+// bin's 64-bit word of the wave, reads the word back (the peers), the
+// leader clears it -- 3 LDS operations and a few VALU per round instead of
+// nbits ballots with their 64-bit selects (the ballot match kept VALU-bound at
+// ~180 instructions per round).  OR commutes, so the result does not depend on
+// the order the LDS unit serves the lanes in.
+// RPW > 0 / NBITS > 0: the rounds per wave and the id bits at compile time;
+// 0: read at run time.
+template <int NW, int RPW, int NBITS, bool ORM>
 __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     const uint16_t* __restrict__ ids, int64_t n, int nbins, int nbits,
-    int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ ranks,
-    uint16_t* __restrict__ tile_starts, uint8_t* __restrict__ dest8,
-    uint64_t* __restrict__ scan_flags, uint32_t* __restrict__ bad) {
+    int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ slots,
+    uint16_t* __restrict__ tile_starts, uint64_t* __restrict__ scan_flags,
+    uint32_t* __restrict__ bad) {
     constexpr int NT = NW * 64, RPW_MAX = RPW > 0 ? RPW : 4096 / 64 / NW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint16_t* wt = (uint16_t*)smem;   // [NW][nbins]
+    // [NW][nbins] peer words (ORM), then [NW][nbins] running counts
+    unsigned long long* mk = (unsigned long long*)smem;
+    uint16_t* wt = (uint16_t*)(smem + (ORM ? NW * nbins * 8 : 0));
     __shared__ int s_wsum[NW];
     clear_scan_flags(scan_flags);
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const int64_t tile = xcd_tile(blockIdx.x, T);
     const int rpw = RPW > 0 ? RPW : tile_rows / 64 / NW;
-    for (int i = tid; i < NW * nbins; i += NT) wt[i] = 0;
+    for (int i = tid; i < NW * nbins; i += NT) {
+        wt[i] = 0;
+        if (ORM) mk[i] = 0ull;
+    }
     unsigned b[RPW_MAX];
     bool oob = false;   // ids >= nbins: clamped, reported through *bad
 #pragma unroll
@@ -448,39 +459,48 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     }
     if (__any(oob) && lane == 0 && bad) atomicOr(bad, 1u);
     __syncthreads();
+    unsigned long long* mw = mk + w * nbins;
+    uint16_t* ww = wt + w * nbins;
     int rk[RPW_MAX];
 #pragma unroll
     for (int q = 0; q < RPW_MAX; ++q) {
         if (RPW == 0 && q >= rpw) break;
         const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
         const bool valid = row < n;
-        if (dest8 && valid) dest8[row] = (uint8_t)b[q];
-        const unsigned long long peers = match_bin_t<NBITS>(b[q], valid, nbits);
+        unsigned long long peers;
+        if constexpr (ORM) {
+            if (valid) __hip_atomic_fetch_or(&mw[b[q]], 1ull << lane, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+            wave_sync();
+            peers = valid ? mw[b[q]] : 0ull;
+        } else {
+            peers = match_bin_t<NBITS>(b[q], valid, nbits);
+        }
         const int r = rank_in(peers);
-        const int before = valid ? (int)wt[w * nbins + b[q]] : 0;
+        const int before = valid ? (int)ww[b[q]] : 0;
         wave_sync();
-        if (valid && r == 0) wt[w * nbins + b[q]] = (uint16_t)(before + __popcll(peers));
+        if (valid && r == 0) {
+            ww[b[q]] = (uint16_t)(before + __popcll(peers));
+            if (ORM) mw[b[q]] = 0ull;
+        }
         wave_sync();
         rk[q] = before + r;
     }
     __syncthreads();
-    // per bin (bin k*NT + tid): prefix over the waves (in place), the tile
-    // count; then the bins' starts in the tile (block scan over the bins)
+    // per bin (bin k*NT + tid): the tile count, the bins' starts in the tile
+    // (block scan over the bins), then every wave's base of the bin = start +
+    // the counts of the earlier waves (in place)
     int carry = 0;
     for (int k = 0; k * NT < nbins; ++k) {
         const int bb = k * NT + tid;
         int run = 0;
-        if (bb < nbins) {
-            int c[NW];
+        int c[NW];
 #pragma unroll
-            for (int ww = 0; ww < NW; ++ww) c[ww] = wt[ww * nbins + bb];
-#pragma unroll
-            for (int ww = 0; ww < NW; ++ww) {
-                wt[ww * nbins + bb] = (uint16_t)run;
-                run += c[ww];
-            }
-            counts[(int64_t)bb * T + tile] = run;
+        for (int ww2 = 0; ww2 < NW; ++ww2) {
+            c[ww2] = bb < nbins ? (int)wt[ww2 * nbins + bb] : 0;
+            run += c[ww2];
         }
+        if (bb < nbins) counts[(int64_t)bb * T + tile] = run;
         int incl = run;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -491,12 +511,20 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
         __syncthreads();
         int wpre = 0, wall = 0;
 #pragma unroll
-        for (int ww = 0; ww < NW; ++ww) {
-            const int x = s_wsum[ww];
-            wpre += ww < w ? x : 0;
+        for (int ww2 = 0; ww2 < NW; ++ww2) {
+            const int x = s_wsum[ww2];
+            wpre += ww2 < w ? x : 0;
             wall += x;
         }
-        if (bb < nbins) tile_starts[tile * nbins + bb] = (uint16_t)(carry + wpre + incl - run);
+        if (bb < nbins) {
+            int acc = carry + wpre + incl - run;
+            tile_starts[tile * nbins + bb] = (uint16_t)acc;
+#pragma unroll
+            for (int ww2 = 0; ww2 < NW; ++ww2) {
+                wt[ww2 * nbins + bb] = (uint16_t)acc;
+                acc += c[ww2];
+            }
+        }
         carry += wall;
         __syncthreads();
     }
@@ -504,25 +532,30 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     for (int q = 0; q < RPW_MAX; ++q) {
         if (RPW == 0 && q >= rpw) break;
         const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
-        if (row < n) ranks[row] = (uint16_t)(wt[w * nbins + b[q]] + rk[q]);
+        if (row < n) slots[row] = (uint16_t)(ww[b[q]] + rk[q]);
     }
 }
 
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
-                           const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
-                           uint8_t* dest8, uint32_t* bad, hipStream_t s) {
+                           const Workspace& ws, uint16_t* slots, uint16_t* tile_starts,
+                           uint32_t* bad, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     prof_begin(s, K_COUNT_IDS);
     // 4 waves (16 waves measured 0.57 vs 0.31 ms at 64M rows, 512 bins)
     const int nw = kWaves;
-    const int lds = align16(nw * nbins * 2);
+    // LDS peer words while they fit next to the counts (<= 2048 bins)
+    const bool orm = g_tune.rank_orm && nbins <= 2048;
+    const int lds = align16(nw * nbins * 2) + (orm ? nw * nbins * 8 : 0);
     const bool b9 = nbits_for(nbins) == 9;   // 257..512 cells (8x8x8)
-    auto k = tile_rows == 4096 ? (b9 ? rank_ids_kernel<kWaves, 16, 9> : rank_ids_kernel<kWaves, 16, 0>)
-           : tile_rows == 2048 ? (b9 ? rank_ids_kernel<kWaves, 8, 9> : rank_ids_kernel<kWaves, 8, 0>)
-                               : rank_ids_kernel<kWaves, 0, 0>;
+    auto k = orm ? (tile_rows == 4096 ? rank_ids_kernel<kWaves, 16, 0, true>
+                    : tile_rows == 2048 ? rank_ids_kernel<kWaves, 8, 0, true>
+                                        : rank_ids_kernel<kWaves, 0, 0, true>)
+           : tile_rows == 4096 ? (b9 ? rank_ids_kernel<kWaves, 16, 9, false> : rank_ids_kernel<kWaves, 16, 0, false>)
+           : tile_rows == 2048 ? (b9 ? rank_ids_kernel<kWaves, 8, 9, false> : rank_ids_kernel<kWaves, 8, 0, false>)
+                               : rank_ids_kernel<kWaves, 0, 0, false>;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s, ids, n, nbins,
-                       nbits_for(nbins), ws.counts, ws.T, tile_rows, ranks, tile_starts, dest8,
+                       nbits_for(nbins), ws.counts, ws.T, tile_rows, slots, tile_starts,
                        ws.flags, bad);
     prof_end(s, K_COUNT_IDS);
     return hipGetLastError();

@@ -394,7 +394,7 @@ int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint1
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (n > 0 && (!ids || !ranks || !tile_starts || !workspace)) return fail(MGR_EINVAL, "null argument");
     const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
-    HIP_OK(mgr::launch_rank_ids(ids, n, nbins, tile_rows, ws, ranks, tile_starts, nullptr, bad_ids,
+    HIP_OK(mgr::launch_rank_ids(ids, n, nbins, tile_rows, ws, ranks, tile_starts, bad_ids,
                                 (hipStream_t)stream));
     return MGR_OK;
 }
@@ -814,6 +814,8 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
     else if (!strcmp(key, "ranked_rows")) mgr::g_tune.ranked_rows = (int)value;
     else if (!strcmp(key, "ranked_walk")) mgr::g_tune.ranked_walk = (int)value;
+    else if (!strcmp(key, "ranked_v")) mgr::g_tune.ranked_v = (int)value;
+    else if (!strcmp(key, "rank_orm")) mgr::g_tune.rank_orm = (int)value;
     else if (!strcmp(key, "img_rpw")) {
         if (value != 1 && value != 2) return fail(MGR_EINVAL, "img_rpw %lld (1 or 2)", (long long)value);
         mgr::g_tune.img_rpw = (int)value;

@@ -14,7 +14,8 @@ constexpr int kMaxTileRows = 65536;      // many-bin pack tiles (super-rounds of
 constexpr int kCoopMaxRounds = 64;       // cooperative pack tiles <= 4096 rows
 constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
 constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups) at most
-constexpr int kMaxSets = 32;             // multi-selection sets per pass (halo pieces <= 26)
+constexpr int kMaxSets = 32;
+constexpr int kTrashBytes = 256 * 512;   // 512 B per workgroup of a persistent grid (<= 256)             // multi-selection sets per pass (halo pieces <= 26)
 
 // One-pass scan control words, right behind the kScanFlags chunk words and
 // zeroed with them by every count producer.
@@ -76,6 +77,10 @@ struct Workspace {
     uint64_t* flags;     // [kScanFlags] one-pass scan chunk words + ScanCtl; zeroed
                          // by the count producers (bin_count, bin_ids, select_count)
     const uint32_t* scan_err;  // &ScanCtl::err: packs return at once when set
+    uint8_t* trash;      // [kTrashBytes] never read: the target of branch-free stores
+                         // that have nothing to write (mgr_pack_ranked), 512 B per
+                         // workgroup (one shared line would serialise every CU on one
+                         // L2 channel)
     int64_t T;
     int64_t t0 = 0, tn = 0;    // the tiles [t0, t0 + tn) one pack launch covers (all: 0, T)
 };
@@ -106,8 +111,8 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
 hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                             const Workspace& ws, void* dest, uint32_t* bad, hipStream_t s);
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
-                           const Workspace& ws, uint16_t* ranks, uint16_t* tile_starts,
-                           uint8_t* dest8, uint32_t* bad, hipStream_t s);
+                           const Workspace& ws, uint16_t* slots, uint16_t* tile_starts,
+                           uint32_t* bad, hipStream_t s);
 hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
                               const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
                               int tile_rows, const Workspace& ws, void* dst, hipStream_t s);
@@ -156,6 +161,9 @@ struct Tune {
     int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
     int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
     int ranked_rows = 0;   // ranked pack store phase: 0 rolled loop, 2 unrolled
+    int ranked_v = 1;      // ranked pack: 1 row-wise loads + unit stores with dword straddles,
+                           // 2 coalesced unit loads + full-unit stores + per-bin partial units
+    int rank_orm = 1;      // rank_ids: peers by LDS OR words (1) or ballot match (0)
     int ranked_walk = 0;   // ranked pack tile walk: 0 one region per XCD, 1 all XCDs in one region
     int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096
     int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)

@@ -120,7 +120,9 @@ def _sort_by_ids(fields, ids, n, nb, dev, scratch=None, check_ids=True):
         T = (n + tile_rows - 1) // tile_rows
         get = scratch.get if scratch is not None else (
             lambda name, nbytes: torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev))
-        ranks = get("ranks_fine", 2 * max(n, 1))
+        # tile slots (+ 16 B: the ranked pack reads u16 quads, the last one
+        # a row past n when n is odd)
+        ranks = get("ranks_fine", 2 * max(n, 1) + 16)
         tstarts = get("tstarts_fine", 8 * max(T * nb, 1))   # u16 starts, or u32 x 2 halves
         _lib.call("mgr_rank_ids", _lib.ptr(ids), n, nb, tile_rows, _lib.ptr(ranks),
                   _lib.ptr(tstarts), _lib.ptr(bad), _lib.ptr(ws), s)
@@ -611,7 +613,10 @@ class MPIGridRedistributor:
                 pack(f, sends[f], redirect_bin, outs[f] if r else None, offs[f])
 
         T = (n + tile_rows - 1) // tile_rows
-        k = min(int(self.exchange_chunks), T)
+        # the chunk count is part of the exchange protocol: the same on every
+        # rank whatever its row count (a rank with fewer tiles than chunks --
+        # an empty one included -- packs empty chunks)
+        k = max(1, int(self.exchange_chunks))
         if k > 1 and P > 1:
             # pipelined: pack the tiles in k chunks, each chunk's pieces travel
             # while the next is packed (exchange_pipelined)

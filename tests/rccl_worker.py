@@ -19,6 +19,7 @@ from __future__ import annotations
 import json
 import os
 import sys
+import threading
 import time
 import traceback
 
@@ -41,6 +42,7 @@ from tests import golden_io as G  # noqa: E402
 
 TOPO = {1: [1, 1, 1], 2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}
 BOX = [1.0, 1.0, 1.0]
+CASE_TIMEOUT_S = float(os.environ.get("MGR_CASE_TIMEOUT", "60"))
 
 
 def log(msg):
@@ -200,7 +202,10 @@ def case_fine_rec36(mgr, comm, fine, seed, as_torch, chunks=1):
     R.exchange_chunks = chunks
     d = data[RANK]
     if as_torch:
-        raw = torch.from_numpy(d.view(np.uint8).reshape(len(d), 36).copy()).cuda()
+        # (an empty rank's (0, 36) array has a zero stride: build it fresh)
+        raw = torch.zeros((len(d), 36), dtype=torch.uint8, device="cuda")
+        if len(d):
+            raw.copy_(torch.from_numpy(d.view(np.uint8).reshape(len(d), 36).copy()))
         got, gpos, off = R.redistribute_by_position(raw, raw.view(torch.float32)[:, :3],
                                                     fine_cells=fine, return_positions=True)
         off = off.cpu().numpy()
@@ -378,11 +383,24 @@ def main():
     cases.append(("cell_number_dropped_ids", lambda: case_cell_number(mgr, comm)))
     for name, fn in cases:
         t0 = time.perf_counter()
+        # a rank that fails before a collective leaves its peers waiting in
+        # it: every case gets a watchdog that ends this rank (results so far
+        # written) instead of hanging the whole run
+        def _hung(n=name):
+            log(f"{n}: HUNG (> {CASE_TIMEOUT_S} s), exiting")
+            results[n] = f"FAIL: hung > {CASE_TIMEOUT_S} s"
+            with open(out_path, "w") as fh:
+                json.dump(results, fh)
+            os._exit(4)
+        dog = threading.Timer(CASE_TIMEOUT_S, _hung)
+        dog.daemon = True
+        dog.start()
         try:
             fn()
             results[name] = "ok"
         except Exception as e:   # record and go on: every rank runs every case
             results[name] = f"FAIL: {e!r}\n{traceback.format_exc()}"
+        dog.cancel()
         log(f"{name}: {results[name].splitlines()[0]} ({time.perf_counter() - t0:.2f} s)")
         # keep the ranks in step between cases (a failed case must not skew
         # the next collective's pairing)

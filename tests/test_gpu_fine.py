@@ -205,12 +205,17 @@ def test_ranked_sort_tile_sizes(rank_rows, row_bytes):
     assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
 
 
-@pytest.mark.parametrize("knobs", [{"ranked_rows": 2}, {"ranked_walk": 1},
-                                   {"ranked_rows": 2, "ranked_walk": 1}])
-@pytest.mark.parametrize("row_bytes", [12, 36])
+RANKED_DEFAULTS = {"ranked_rows": 0, "ranked_walk": 0, "ranked_v": 1, "rank_orm": 1}
+
+
+@pytest.mark.parametrize("knobs", [{"ranked_v": 2}, {"ranked_rows": 2},
+                                   {"ranked_walk": 1}, {"rank_orm": 0},
+                                   {"ranked_v": 2, "rank_orm": 0}])
+@pytest.mark.parametrize("row_bytes", [4, 12, 36])
 def test_ranked_pack_variants(knobs, row_bytes):
-    """Every ranked-pack variant (row-wise read-back, unrolled store phase,
-    the all-XCD tile walk) gives the same stable sort."""
+    """Every ranked-pack / rank_ids variant (row-wise loads with dword
+    straddles, unrolled store phase, the all-XCD tile walk; ballot-match
+    ranking) gives the same stable sort."""
     rng = np.random.default_rng(row_bytes + 7 * len(knobs))
     n = 200_003
     ids = rng.integers(0, 512, n).astype(np.uint16)
@@ -226,7 +231,7 @@ def test_ranked_pack_variants(knobs, row_bytes):
                                     fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
     finally:
         for k in knobs:
-            _lib.tune(k, 0)
+            _lib.tune(k, RANKED_DEFAULTS[k])
     assert np.array_equal(got.cpu().numpy(), exp)
     assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
 
@@ -258,3 +263,20 @@ def test_fine_ids_out_of_range(row_bytes):
                                 [4, 4, 4], fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
     assert np.array_equal(got.cpu().numpy(), data[np.argsort(ids, kind="stable")])
     assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=64))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 63, 4095, 4097, 8193])
+@pytest.mark.parametrize("row_bytes", [4, 36])
+def test_ranked_sort_small_and_ragged(n, row_bytes):
+    """The ranked sort at tiny and tile-edge sizes (the unit-streamed pack
+    reads the slots of row pairs: no read before row 0 or past row n - 1)."""
+    rng = np.random.default_rng(n * 7 + row_bytes)
+    ids = rng.integers(0, 512, n).astype(np.uint16)
+    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
+    exp = data[np.argsort(ids, kind="stable")]
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    pos = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+    got, off = R.fine_cell_sort(torch.from_numpy(data).cuda(), pos, [8, 8, 8],
+                                fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
+    assert np.array_equal(got.cpu().numpy(), exp)
+    assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
