@@ -814,7 +814,6 @@ int mgr_tune(const char* key, int64_t value) {
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
     else if (!strcmp(key, "ranked_rows")) mgr::g_tune.ranked_rows = (int)value;
     else if (!strcmp(key, "ranked_walk")) mgr::g_tune.ranked_walk = (int)value;
-    else if (!strcmp(key, "ranked_v")) mgr::g_tune.ranked_v = (int)value;
     else if (!strcmp(key, "rank_orm")) mgr::g_tune.rank_orm = (int)value;
     else if (!strcmp(key, "img_rpw")) {
         if (value != 1 && value != 2) return fail(MGR_EINVAL, "img_rpw %lld (1 or 2)", (long long)value);

@@ -77,10 +77,6 @@ struct Workspace {
     uint64_t* flags;     // [kScanFlags] one-pass scan chunk words + ScanCtl; zeroed
                          // by the count producers (bin_count, bin_ids, select_count)
     const uint32_t* scan_err;  // &ScanCtl::err: packs return at once when set
-    uint8_t* trash;      // [kTrashBytes] never read: the target of branch-free stores
-                         // that have nothing to write (mgr_pack_ranked), 512 B per
-                         // workgroup (one shared line would serialise every CU on one
-                         // L2 channel)
     int64_t T;
     int64_t t0 = 0, tn = 0;    // the tiles [t0, t0 + tn) one pack launch covers (all: 0, T)
 };
@@ -161,8 +157,6 @@ struct Tune {
     int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
     int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
     int ranked_rows = 0;   // ranked pack store phase: 0 rolled loop, 2 unrolled
-    int ranked_v = 1;      // ranked pack: 1 row-wise loads + unit stores with dword straddles,
-                           // 2 coalesced unit loads + full-unit stores + per-bin partial units
     int rank_orm = 1;      // rank_ids: peers by LDS OR words (1) or ballot match (0)
     int ranked_walk = 0;   // ranked pack tile walk: 0 one region per XCD, 1 all XCDs in one region
     int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096

@@ -399,7 +399,7 @@ int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
     const int64_t T = num_tiles(n, tile_rows);
     const int64_t M = (int64_t)nbins * (T > 0 ? T : 1);
     return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) +
-           a256((kScanFlags + kScanCtlWords) * 8) + a256(kTrashBytes);
+           a256((kScanFlags + kScanCtlWords) * 8);
 }
 
 Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
@@ -412,9 +412,8 @@ Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
     ws.counts = (int32_t*)p;     p += a256(M * 4);
     ws.offsets = (int64_t*)p;    p += a256(M * 8);
     ws.bin_starts = (int64_t*)p; p += a256((nbins + 1) * 8);
-    ws.flags = (uint64_t*)p;     p += a256((kScanFlags + kScanCtlWords) * 8);
+    ws.flags = (uint64_t*)p;
     ws.scan_err = &((const ScanCtl*)(ws.flags + kScanFlags))->err;
-    ws.trash = (uint8_t*)p;
     return ws;
 }
 

@@ -1131,176 +1131,11 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
-// Ranked pack, unit-streamed (ranked_v 2).  Same placement as
-// pack_ranked_kernel (row -> tile slot from mgr_rank_ids, a bin-sorted LDS
-// image of the tile), but every global access is a whole 16-byte unit:
-//  * loads: the tile's bytes in coalesced 16-byte units (thread t, unit t +
-//    1024 k: every load instruction reads 1 KiB contiguous), with the slot and
-//    bin of the (at most R) rows a unit touches; each dword goes to its row's
-//    slot in the image, and the unit holding a row's first dword records the
-//    slot's bin;
-//  * stores: a unit of the image that lies inside one bin's run is one 16-byte
-//    store to the run's place; the few units that straddle runs are left to
-//    the bins themselves -- thread b writes the head and tail dwords of bin b's
-//    run (at most 3 + 3) -- so no store instruction diverges into dwords.
-//    Stores with nothing to write go to the workspace's trash line instead of
-//    branching (a fixed store count lets the next tile's loads, issued before
-//    them, be waited for without waiting for the stores).
-// Persistent: one 1024-thread workgroup per CU walks its XCD's tiles (the
-// lines the runs of neighbouring tiles share meet in one L2); the next tile's
-// loads are in flight while this tile's image is stored.  Two barriers per
-// tile.
-template <int RB, int TR>
-__global__ __launch_bounds__(1024) void pack_ranked2_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
-    const uint16_t* __restrict__ slots, const uint16_t* __restrict__ tile_starts, int nb,
-    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err, uint8_t* __restrict__ trash) {
-    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
-    constexpr int NT = 1024, TB = TR * RB;
-    constexpr int NU = (TB / 16 + NT - 1) / NT;   // 16-byte units per thread
-    static_assert(RB >= 8, "a 16-byte unit touches at most two rows");
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* img = smem;
-    uint32_t* imgw = (uint32_t*)smem;
-    uint16_t* ibin = (uint16_t*)(smem + align16(TB));                  // [TR] bin of each slot
-    unsigned long long* gaddr = (unsigned long long*)(smem + align16(TB) + TR * 2);   // [nb]
-    uint16_t* lstart = (uint16_t*)(smem + align16(TB) + TR * 2 + nb * 8);           // [nb + 1]
-    if (scan_failed(scan_err)) return;
-    const int tid = threadIdx.x, lane = lane_id();
-    const int64_t per = (T + 7) >> 3;
-    const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3), xx = (int)(blockIdx.x & 7);
-    const int64_t first = (int64_t)xx * per + kx, last = min(T, (int64_t)xx * per + per);
-    const int mb = min(tid, nb - 1);
-    // this workgroup's own trash lines (grid <= 256 workgroups)
-    const unsigned long long tr_a =
-        (unsigned long long)(trash + 512 * (blockIdx.x & 255) + 16 * (lane & 31));
-    // a unit that starts inside the array stays inside its page
-    const int64_t xmax = ((n * RB - 1) & ~(int64_t)15);
-    const int64_t qmax = ((n + 1) & ~(int64_t)1) - 4;
-    struct Set {
-        u32x4_t v[NU];
-        u32x2_t sl[NU];   // slots of 4 rows from the even row at or before the unit's first
-        u32x2_t bi[NU];   // their bins
-        long long seg;
-        unsigned ls;
-    };
-    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
-        t = min(t, last - 1);
-        int tv = tid;
-        asm volatile("" : "+v"(tv));   // unit indices per tile, not hoisted (registers)
-        S.seg = offsets[(int64_t)mb * T + t];
-        S.ls = tile_starts[t * nb + mb];
-        const int64_t b0 = t * (int64_t)TB;
-#pragma unroll
-        for (int k = 0; k < NU; ++k) {
-            const int x = 16 * (tv + NT * k);
-            S.v[k] = *(const u32x4_a4*)(src + min(b0 + min(x, TB - 16), xmax));
-            // 4 rows from an even row (dword-aligned u16 quads; n >= 4); the
-            // last quad ends at row n - 1, or at row n when n is odd (2 bytes
-            // past the arrays, inside their allocation granule)
-            const int64_t q0 = min((t * TR + min(x, TB - 16) / RB) & ~(int64_t)1, qmax);
-            S.sl[k] = *(const u32x2_t __attribute__((aligned(4)))*)(slots + q0);
-            S.bi[k] = *(const u32x2_t __attribute__((aligned(4)))*)(ids + q0);
-        }
-    };
-    // the partial- and full-unit stores of the tile: a fixed count per
-    // thread (NU + 6, no branches around them), so the next tile's loads --
-    // issued before them -- can be waited for with a static vmcnt that leaves
-    // the stores in flight
-    auto stores = [&](int tbytes, int tv) __attribute__((always_inline)) {
-        // the bins' head and tail dwords (units straddling two runs, the
-        // tile's last partial unit): at most 3 + 3 per bin
-        {
-            const int b = min(tid, nb - 1);
-            const int s0 = (int)lstart[b] * RB, e = (int)lstart[b + 1] * RB;
-            const int he = (s0 & 15) ? min(e, (s0 + 15) & ~15) : s0;
-            const int ts = (e & 15) ? max(he, e & ~15) : e;
-            const unsigned long long ga = gaddr[b];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const int o = (i < 3 ? s0 : ts) + 4 * (i % 3);
-                const bool ok = tid < nb && o < (i < 3 ? he : e);
-                gstore<uint32_t>(ok ? ga + o : tr_a, imgw[(ok ? o : 0) >> 2]);
-            }
-        }
-        // the units inside one run: one 16-byte store each
-#pragma unroll
-        for (int k = 0; k < NU; ++k) {
-            const int x = min(16 * (tv + NT * k), TB - 16);
-            const u32x4_t q = *(const u32x4_t*)(img + x);
-            const int bf = ibin[x / RB], bl = ibin[(x + 15) / RB];
-            const unsigned long long ga = gaddr[bf];
-            const bool ok = 16 * (tv + NT * k) + 16 <= tbytes && bf == bl;
-            gstore<u32x4_a4>(ok ? ga + x : tr_a, q);
-        }
-    };
-    Set A;
-    int64_t t = first;
-    if (t >= last) return;
-    load(A, t);
-    {   // the same count of (trash) stores behind the first loads as behind every later tile's
-#pragma unroll
-        for (int i = 0; i < 6; ++i) gstore<uint32_t>(tr_a, 0u);
-#pragma unroll
-        for (int k = 0; k < NU; ++k) gstore<u32x4_a4>(tr_a, u32x4_a4{0u, 0u, 0u, 0u});
-    }
-    for (;;) {
-        const int tr = (int)min((int64_t)TR, n - t * TR);
-        const int tbytes = tr * RB;
-        const int64_t rbase = t * TR;
-        int tv = tid;
-        asm volatile("" : "+v"(tv));   // per-unit index math per tile, not hoisted
-        if (tid < nb) {
-            lstart[tid] = (uint16_t)A.ls;
-            gaddr[tid] = (unsigned long long)(dst + (A.seg - (long long)A.ls) * (long long)RB);
-        }
-        if (tid == 0) lstart[nb] = (uint16_t)tr;
-        // scatter: dword d of unit k -> its row's slot
-#pragma unroll
-        for (int k = 0; k < NU; ++k) {
-            const int x = 16 * (tv + NT * k);
-            const int xr = min(x, TB - 16);
-            const int r0 = xr / RB;
-            const int64_t q0 = min((rbase + r0) & ~(int64_t)1, qmax);
-            const int sh = (int)(rbase - q0);   // row r of the tile is entry r + sh of the quad
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const int o = x + 4 * d;
-                const int r = o / RB;
-                const int j = r + sh;   // 0 .. 3 for the rows of this unit
-                const uint32_t sw = A.sl[k][(j >> 1) & 1], bw = A.bi[k][(j >> 1) & 1];
-                const int slot = (int)((sw >> (16 * (j & 1))) & 0xFFFFu);
-                const int bin = min((int)((bw >> (16 * (j & 1))) & 0xFFFFu), nb - 1);
-                if (o < tbytes) {
-                    const int off = o - r * RB;
-                    imgw[(slot * RB + off) >> 2] = A.v[k][d];
-                    if (off == 0) ibin[slot] = (uint16_t)bin;
-                }
-            }
-        }
-        const int64_t tn = t + gx;
-        load(A, tn);   // (clamped: the last tile again after the walk's end, not used)
-        __syncthreads();
-        tv = tid;
-        asm volatile("" : "+v"(tv));
-        stores(tbytes, tv);
-        __syncthreads();   // the image, ibin, lstart and gaddr are reused by the next tile
-        t = tn;
-        if (t >= last) break;
-    }
-}
-
 // LDS of the ranked pack: the tile image, its row bins, per-bin output
 // addresses and tile starts.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
     return align16(tile_rows * (int)row_bytes) + align16(tile_rows * 2) + nbins * 8 + nbins * 2;
 }
-// ranked_v 2: image, slot bins, per-bin output addresses, tile starts + end
-static int ranked2_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
-    return align16(tile_rows * (int)row_bytes) + tile_rows * 2 + nbins * 8 + (nbins + 1) * 2;
-}
-
 // Ranked tiles: 4096 rows when their image fits the LDS (36-byte rows: 157 KiB),
 // else 2048.  Longer tiles halve the [bins][tiles] histogram the scan walks and
 // the per-tile fixed work (A/B: profiles/round2/ab_notes.md).
@@ -1326,26 +1161,14 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
 #define MGR_PRT(RB_, TR_)                                                                     \
-    if (g_tune.ranked_v == 2 && (TR_ * RB_) % 16 == 0 && n >= 4 && RB_ >= 8 &&              \
-        !((uintptr_t)ids & 3) && !((uintptr_t)ranks & 3) && grid <= 256) {                   \
-        auto k = pack_ranked2_kernel<(RB_ >= 8 ? RB_ : 8), TR_>; /* RB_ < 8: never launched */\
-        const int lds2 = ranked2_lds_bytes(TR_, RB_, nbins);                                  \
-        if (lds2 > 160 * 1024) return hipErrorNotSupported;                                   \
-        ensure_lds(k, lds2);                                                                  \
-        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds2, s,              \
+    {                                                                                         \
+        auto k = g_tune.ranked_rows == 2 ? pack_ranked_kernel<RB_, TR_, true>                 \
+                                         : pack_ranked_kernel<RB_, TR_, false>;               \
+        ensure_lds(k, lds);                                                                   \
+        hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,               \
                            (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,            \
-                           ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err, ws.trash);           \
-        e = hipGetLastError();                                                                \
-    } else {                                                                                  \
-        {                                                                                     \
-            auto k = g_tune.ranked_rows == 2 ? pack_ranked_kernel<RB_, TR_, true>             \
-                                             : pack_ranked_kernel<RB_, TR_, false>;           \
-            ensure_lds(k, lds);                                                               \
-            hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,           \
-                               (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,        \
-                               ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,                  \
-                               g_tune.ranked_walk);                                           \
-        }                                                                                     \
+                           ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,                      \
+                           g_tune.ranked_walk);                                               \
         e = hipGetLastError();                                                                \
     }
 #define MGR_PR(RB_)                                                                           \
