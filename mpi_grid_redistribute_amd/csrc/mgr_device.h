@@ -561,6 +561,35 @@ __device__ __forceinline__ uint32_t set_mask_m(const FlagPlanes& fp, unsigned ma
         if (b < nbits) r &= ((mask >> b) & 1u) ? fp.p[b] : 0xFFFFu;
     return r;
 }
+// flag_planes / set_mask_m with the flag bits at compile time (NB > 0, NB >=
+// every bit a mask uses): the planes unrolled, a set's membership NB ANDs
+// with a uniform per-bit fill instead of a run-time loop over 16 bits (the
+// loop kept the halo's selection kernels VALU-bound); NB = 0: run time.
+template <int NB>
+__device__ __forceinline__ void flag_planes_t(const uint32_t (&fw)[kSelWords], int nbits,
+                                              FlagPlanes& fp) {
+    if constexpr (NB > 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) fp.p[b] = set_mask(fw, b);
+    } else {
+        flag_planes(fw, nbits, fp);
+    }
+}
+template <int NB>
+__device__ __forceinline__ uint32_t set_mask_t(const FlagPlanes& fp, unsigned mask, int nbits) {
+    if constexpr (NB > 0) {
+        uint32_t r = 0xFFFFu;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) r &= fp.p[b] | (((mask >> b) & 1u) ? 0u : 0xFFFFu);
+        return r;
+    } else {
+        return set_mask_m(fp, mask, nbits);
+    }
+}
+// The compile-time flag-bit count a launcher instantiates for nbits.
+static inline int flag_bits_class(int nbits) {
+    return nbits <= 2 ? 2 : nbits <= 4 ? 4 : nbits <= 6 ? 6 : nbits <= 8 ? 8 : 0;
+}
 __device__ __forceinline__ int mask_bits(const SetMasks& sm, int nsets) {
     unsigned u = 0;
     for (int k = 0; k < nsets; ++k) u |= sm.m[k];

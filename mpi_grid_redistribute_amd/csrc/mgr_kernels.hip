@@ -269,6 +269,7 @@ __global__ __launch_bounds__(kBlock) void select_count_kernel(const uint16_t* __
 // tile_rows rows read in kSelChunk-row chunks (chunk_flags); counts[s * T +
 // tile] for mgr_scan with nbins = nsets, whose offsets then lay the sets out
 // one after the other, each in row order.
+template <int NB>
 __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __restrict__ flags,
                                                             int64_t n, int nsets, SetMasks masks,
                                                             int32_t* __restrict__ counts,
@@ -280,24 +281,59 @@ __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __re
     if (tile >= T) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
-    int c[kMaxSets];
+    if constexpr (NB > 0) {
+        // NB flag bits at compile time: a histogram of the rows' flag codes
+        // (the low NB bits; code 0 is in no set), then superset sums over the
+        // NB bits -- a set's count is the sum of every code holding its mask
+        // (one LDS add per flagged row instead of a membership test per set)
+        constexpr int NC = 1 << NB;
+        __shared__ int hist_s[kWaves][NC];
+        int* hist = hist_s[w];
+        for (int i = lane; i < NC; i += 64) hist[i] = 0;
+        wave_sync();
+        for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
+            uint32_t fw[kSelWords];
+            chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
 #pragma unroll
-    for (int k = 0; k < kMaxSets; ++k) c[k] = 0;
-    const int nbits = mask_bits(masks, nsets);
-    for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
-        uint32_t fw[kSelWords];
-        chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
-        FlagPlanes fp;
-        flag_planes(fw, nbits, fp);
+            for (int i = 0; i < kSelWords; ++i) {
+                const unsigned f0 = fw[i] & (NC - 1), f1 = (fw[i] >> 16) & (NC - 1);
+                if (f0) atomicAdd(&hist[f0], 1);
+                if (f1) atomicAdd(&hist[f1], 1);
+            }
+        }
+        wave_sync();
 #pragma unroll
-        for (int k = 0; k < kMaxSets; ++k)
-            if (k < nsets) c[k] += __popc(set_mask_m(fp, masks.m[k], nbits));
-    }
+        for (int b = 0; b < NB; ++b) {
+            for (int c = lane; c < NC; c += 64)
+                if (!((c >> b) & 1)) hist[c] += hist[c | (1 << b)];
+            wave_sync();
+        }
+        if (lane == 0) {
+            for (int k = 0; k < nsets; ++k) {
+                const unsigned m = masks.m[k];
+                counts[(int64_t)k * T + tile] = m ? hist[m] : rows;
+            }
+        }
+    } else {
+        int c[kMaxSets];
 #pragma unroll
-    for (int k = 0; k < kMaxSets; ++k) {
-        if (k >= nsets) break;
-        const int t = wave_sum(c[k]);
-        if (lane == 0) counts[(int64_t)k * T + tile] = t;
+        for (int k = 0; k < kMaxSets; ++k) c[k] = 0;
+        const int nbits = mask_bits(masks, nsets);
+        for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
+            uint32_t fw[kSelWords];
+            chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
+            FlagPlanes fp;
+            flag_planes(fw, nbits, fp);
+#pragma unroll
+            for (int k = 0; k < kMaxSets; ++k)
+                if (k < nsets) c[k] += __popc(set_mask_m(fp, masks.m[k], nbits));
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxSets; ++k) {
+            if (k >= nsets) break;
+            const int t = wave_sum(c[k]);
+            if (lane == 0) counts[(int64_t)k * T + tile] = t;
+        }
     }
 }
 
@@ -305,11 +341,19 @@ hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const 
                              int tile_rows, const Workspace& ws, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     SetMasks sm{};
-    for (int k = 0; k < nsets; ++k) sm.m[k] = (uint16_t)masks[k];
+    unsigned u = 0;
+    for (int k = 0; k < nsets; ++k) {
+        sm.m[k] = (uint16_t)masks[k];
+        u |= (unsigned)sm.m[k];
+    }
+    const int nb = flag_bits_class(u ? 32 - __builtin_clz(u) : 0);
     const int64_t grid = (ws.T + kWaves - 1) / kWaves;
+    auto k = nb == 2 ? msel_count_kernel<2> : nb == 4 ? msel_count_kernel<4>
+           : nb == 6 ? msel_count_kernel<6> : nb == 8 ? msel_count_kernel<8>
+                     : msel_count_kernel<0>;
     prof_begin(s, K_HALO);
-    hipLaunchKernelGGL(msel_count_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, flags, n,
-                       nsets, sm, ws.counts, ws.T, tile_rows, ws.flags);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kBlock), 0, s, flags, n, nsets, sm,
+                       ws.counts, ws.T, tile_rows, ws.flags);
     prof_end(s, K_HALO);
     return hipGetLastError();
 }

@@ -306,6 +306,7 @@ __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_
     }
 }
 
+template <int NB>
 __global__ __launch_bounds__(256) void msel_pack_kernel(
     SelFields fs, int nf, int64_t n, const uint16_t* __restrict__ flags, int nsets, SetMasks masks,
     const int64_t* __restrict__ offsets, const int64_t* __restrict__ set_starts, int64_t T,
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         uint32_t fw[kSelWords];
         chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
         FlagPlanes fp;
-        flag_planes(fw, nbits, fp);
+        flag_planes_t<NB>(fw, nbits, fp);
         auto flush = [&](int fill) {
             wave_sync();
             for (int f = 0; f < nf; ++f) {
@@ -365,7 +366,8 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         int fill = 0;
         for (int k = 0; k < nsets; ++k) {
             if (!((live >> k) & 1u)) continue;
-            uint32_t m = set_mask_m(fp, masks.m[k], nbits);
+            uint32_t m = set_mask_t<NB>(fp, masks.m[k], nbits);
+            if (!__ballot(m != 0u)) continue;   // an empty set costs no prefix
             int total;
             int pos = wave_excl(__popc(m), &total);
             if (!total) continue;
@@ -409,9 +411,15 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
         }
         fs.wlog[f] = (a & 15) == 0 ? 4 : (a & 7) == 0 ? 3 : (a & 3) == 0 ? 2 : (a & 1) == 0 ? 1 : 0;
     }
+    unsigned u = 0;
+    for (int k = 0; k < nsets; ++k) u |= (unsigned)sb.m[k];
+    const int nb = flag_bits_class(u ? 32 - __builtin_clz(u) : 0);
+    auto kern = nb == 2 ? msel_pack_kernel<2> : nb == 4 ? msel_pack_kernel<4>
+              : nb == 6 ? msel_pack_kernel<6> : nb == 8 ? msel_pack_kernel<8>
+                        : msel_pack_kernel<0>;
     const dim3 grid((unsigned)((ws.T + 3) / 4));
     prof_begin(s, K_HALO_PACK);
-    hipLaunchKernelGGL(msel_pack_kernel, grid, dim3(256), 0, s, fs, nfields, n, flags, nsets, sb,
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, fs, nfields, n, flags, nsets, sb,
                        ws.offsets, ws.bin_starts, ws.T, tile_rows, ws.scan_err);
     prof_end(s, K_HALO_PACK);
     return hipGetLastError();
