@@ -328,3 +328,37 @@ def test_one_rank_halo_vs_oracle():
             ids = out["id"]
             assert np.array_equal(opos.view(np.uint8), pos_o[ids % n].view(np.uint8))
         assert out.tobytes() == exp.tobytes()
+
+
+@pytest.mark.parametrize("case", ["f64", "f32_positions", "corner_overflow", "torch"])
+def test_halo_one_rank_vs_oracle(case):
+    """One rank (1x1x1 grid): the rows stay in order and the halo is the
+    rank's own periodic images (one selection pass over the received flags,
+    one multi-set pack) against the oracle, with the wrapped positions
+    returned; 'corner_overflow' puts every row into all 7 corner-region
+    pieces, beyond the reserved capacity."""
+    rng = np.random.default_rng(len(case))
+    n, box, ol = 200_003, [1.0, 1.0, 1.0], [0.06, 0.1, 0.04]
+    pos = rng.uniform(-0.2, 1.2, (n, 3))
+    if case == "corner_overflow":
+        pos = rng.uniform(0.0, 0.03, (n, 3))
+    if case == "f32_positions":
+        pos = pos.astype(np.float32)
+    data = np.arange(n, dtype=np.int64) * 3 + 1
+    pos_o = pos.copy()
+    exp = ro.redistribute_by_position_overload_all_ranks([1, 1, 1], box, 1, [data],
+                                                         [pos_o], ol)[0]
+    R = MPIGridRedistributor(None, [1, 1, 1], box)
+    if case == "torch":
+        d, p = torch.from_numpy(data).cuda(), torch.from_numpy(pos).cuda()
+    else:
+        d, p = data, pos
+    out, opos = R.redistribute_by_position(d, p, overload_lengths=ol, return_positions=True)
+    torch.cuda.synchronize()
+    if case == "torch":
+        out, opos, p = out.cpu().numpy(), opos.cpu().numpy(), p.cpu().numpy()
+    assert np.array_equal(out, exp)
+    # positions travel with the rows: every output row's position is its source row's
+    want = pos_o[(out - 1) // 3]
+    assert np.array_equal(np.asarray(opos).view(np.uint8), want.view(np.uint8))
+    assert np.array_equal(np.asarray(p).view(np.uint8), pos_o.view(np.uint8))   # wrapped in place
