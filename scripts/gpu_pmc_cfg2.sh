@@ -1,6 +1,6 @@
 #!/bin/bash
-# rocprofv3 SQ/TA PMC passes over the config-5 bench line (one counter group
-# per pass, no tracing domains): what bounds each config-5 kernel.
+# rocprofv3 SQ/TA PMC passes over the default (config-2) bench line (one
+# counter group per pass, no tracing domains): what bounds the pack.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/pmc2
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,23 @@
+#!/bin/bash
+# A round's evidence: rocprofv3 kernel-trace stats of every bench line, and
+# FETCH_SIZE / WRITE_SIZE PMC passes (one counter per run) of each line, into
+# gpurun_out/$PROF (default r3prof; tools/round_profiles.py assembles them).
+PROF=${PROF:-r3prof}
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/$PROF
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+run() {  # name, rocprof args..., -- bench args
+  local name=$1; shift
+  timeout -k 10 240 "$@" > $R/gpurun_out/$PROF/$name.log 2>&1
+  local rc=$?; echo "$name rc=$rc" >> $R/gpurun_out/$PROF/summary.txt
+  return $rc
+}
+for cfg in "cfg2::" "cfg5::--config 5" "cfg3x::--exchange --config 3" "halo::--exchange --config 3 --overload 0.05"; do
+  name=${cfg%%::*}; args=${cfg#*::}
+  run ${name}_trace rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$PROF/${name}_trace -o run \
+    -- python3 $R/bench.py --no-cpu-baseline $args --steps 20 --warmup 5 || exit 1
+  for c in FETCH_SIZE WRITE_SIZE; do
+    run ${name}_${c} rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/$PROF/${name}_${c} -o pmc \
+      -- python3 $R/bench.py --no-cpu-baseline --prof none $args --steps 3 --warmup 1 || exit 1
+  done
+done

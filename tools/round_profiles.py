@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Assemble a round's profile evidence from gpurun_out/<dir> (made by
-scripts/gpu_round2_profiles.sh): per bench line, the rocprofv3 kernel-trace
+scripts/gpu_round_profiles.sh): per bench line, the rocprofv3 kernel-trace
 stats (copied), the bench JSON line, and FETCH_SIZE/WRITE_SIZE PMC bytes per
 launch of each kernel (gfx950 correction, MI355X_MICROARCH.md §HBM:
 FETCH_SIZE x 2, both in KB) merged into profiles/traffic.json under the
 line's workload; plus a markdown summary.
-usage: python tools/round_profiles.py gpurun_out/r2prof profiles/round2"""
+usage: python tools/round_profiles.py gpurun_out/r3prof profiles/round3"""
 import csv
 import json
 import os
