@@ -812,7 +812,6 @@ int mgr_tune(const char* key, int64_t value) {
     if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
     else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
     else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
-    else if (!strcmp(key, "ranked_rows")) mgr::g_tune.ranked_rows = (int)value;
     else if (!strcmp(key, "ranked_walk")) mgr::g_tune.ranked_walk = (int)value;
     else if (!strcmp(key, "rank_orm")) mgr::g_tune.rank_orm = (int)value;
     else if (!strcmp(key, "img_rpw")) {

@@ -156,7 +156,6 @@ struct Tune {
                                  // (-1: give up at once -- tests of the error path)
     int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
     int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
-    int ranked_rows = 0;   // ranked pack store phase: 0 rolled loop, 2 unrolled
     int rank_orm = 1;      // rank_ids: peers by LDS OR words (1) or ballot match (0)
     int ranked_walk = 0;   // ranked pack tile walk: 0 one region per XCD, 1 all XCDs in one region
     int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096

@@ -1030,7 +1030,7 @@ static int device_cus() {
 // LDS) walks its XCD's tiles, the workgroups of an XCD on adjacent tiles at a
 // time (the lines their runs share meet in one L2).  No ballots, no per-tile
 // count table, three barriers per tile.
-template <int RB, int TR, bool UNR>
+template <int RB, int TR>
 __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
     const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
@@ -1094,8 +1094,8 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         __syncthreads();
         const int nbytes = tr * RB;
         // (the image pack's two-address unit store, store_img_unit, measured
-        // 12 % slower here, same box: profiles/round3/ab_notes.md)
-        auto unit = [&](int x) __attribute__((always_inline)) {
+        // 12 % slower here; an unrolled store loop, no gain)
+        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
             const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
             const int bf = ibin[x / RB];
             if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
@@ -1107,19 +1107,6 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
                     if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
                 }
             }
-        };
-        if constexpr (UNR) {
-            // unrolled: no store loop whose preheader would wait (vmcnt 0)
-            // for the next tile's loads already in flight
-            constexpr int NU = (TR * RB / 16 + 1023) / 1024;
-#pragma unroll
-            for (int k = 0; k < NU; ++k) {
-                int x = 16 * (tid + 1024 * k);
-                asm volatile("" : "+v"(x));   // computed per tile, not hoisted (registers)
-                if (x < nbytes) unit(x);
-            }
-        } else {
-            for (int x = 16 * tid; x < nbytes; x += 16 * 1024) unit(x);
         }
         __syncthreads();   // the image, ibin, lstart and gaddr are reused by the next tile
     };
@@ -1170,8 +1157,7 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     hipError_t e = hipErrorNotSupported;
 #define MGR_PRT(RB_, TR_)                                                                     \
     {                                                                                         \
-        auto k = g_tune.ranked_rows == 2 ? pack_ranked_kernel<RB_, TR_, true>                 \
-                                         : pack_ranked_kernel<RB_, TR_, false>;               \
+        auto k = pack_ranked_kernel<RB_, TR_>;                                                \
         ensure_lds(k, lds);                                                                   \
         hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,               \
                            (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,            \

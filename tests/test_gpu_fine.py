@@ -205,15 +205,15 @@ def test_ranked_sort_tile_sizes(rank_rows, row_bytes):
     assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
 
 
-RANKED_DEFAULTS = {"ranked_rows": 0, "ranked_walk": 0, "rank_orm": 1}
+RANKED_DEFAULTS = {"ranked_walk": 0, "rank_orm": 1}
 
 
-@pytest.mark.parametrize("knobs", [{"ranked_rows": 2}, {"ranked_walk": 1},
-                                   {"ranked_rows": 2, "ranked_walk": 1}, {"rank_orm": 0}])
+@pytest.mark.parametrize("knobs", [{"ranked_walk": 1}, {"rank_orm": 0},
+                                   {"ranked_walk": 1, "rank_orm": 0}])
 @pytest.mark.parametrize("row_bytes", [4, 12, 36])
 def test_ranked_pack_variants(knobs, row_bytes):
-    """Every ranked-pack / rank_ids variant (unrolled store phase, the
-    all-XCD tile walk; ballot-match ranking) gives the same stable sort."""
+    """Every ranked-pack / rank_ids variant (the all-XCD tile walk;
+    ballot-match ranking) gives the same stable sort."""
     rng = np.random.default_rng(row_bytes + 7 * len(knobs))
     n = 200_003
     ids = rng.integers(0, 512, n).astype(np.uint16)

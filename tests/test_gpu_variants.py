@@ -22,7 +22,7 @@ DEFAULTS = {"xcd_pack": 16, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 0, "
             "many_rows": 0, "bin_staged": 1, "tile_rounds": 0,
             "pack_many": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
             "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0,
-            "img_rpw": 2, "ranked_rows": 0, "ranked_walk": 0,
+            "img_rpw": 2, "ranked_walk": 0,
             "rank_orm": 1}
 VARIANTS = [
     {"img_rpw": 1},

@@ -67,7 +67,7 @@ def main():
 
 
 DEFAULTS = {"scan_max_chunks": 1024, "scan_chunk": 2048, "img_rpw": 2, "bin_geo": 1, "rank_rows": 0, "bin_waves": 0, "pack_img": 1, "tile_rounds": 0, "xcd_pack": 16,
-            "bin_staged": 1, "bin_skip_clean": 1, "ranked_rows": 0, "ranked_walk": 0,
+            "bin_staged": 1, "bin_skip_clean": 1, "ranked_walk": 0,
             "rank_orm": 1}
 
 if __name__ == "__main__":

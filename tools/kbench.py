@@ -61,7 +61,7 @@ def run(variant):
                  "xcd_pack": 16, "xcd_bin": 0, "bin_skip_clean": 1,
                  "bin_waves": 0, "pack_many": 1, "scan_chunk": 2048,
                  "pack_img": 1, "many_super": 1, "scan_max_chunks": 1024, "pack_sel": 1,
-                 "pack_compact": 1, "many_rows": 0, "bin_geo": 1, "img_rpw": 2, "ranked_rows": 0, "ranked_walk": 0}.items():
+                 "pack_compact": 1, "many_rows": 0, "bin_geo": 1, "img_rpw": 2, "ranked_walk": 0}.items():
         _lib.tune(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
