@@ -211,6 +211,9 @@ def main():
                          "the step then includes the halo exchange (redist.py:161-166)")
     ap.add_argument("--exchange", action="store_true",
                     help="run the N>1 path (config 3, RCCL exchange) even at one GPU")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="N > 1: pack the tiles in this many chunks, each chunk's rows sent "
+                         "while the next is packed (exchange_pipelined); 0 = 4 for N > 1, else 1")
     args = ap.parse_args()
 
     import mpi_grid_redistribute_amd as mgr
@@ -243,6 +246,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = args.config or (3 if multi else 2)
+    chunks = args.chunks or (4 if world > 1 else 1)
     if multi and cfg == 2:
         cfg = 3
     topo = topology_for(world) if multi else [2, 2, 2]
@@ -286,6 +290,7 @@ def main():
         n = args.n or (N_CFG5_PER_GPU if cfg == 5 else N_CFG3_PER_GPU)
         comm = mgr.RcclComm.from_torch_distributed()
         R = mgr.MPIGridRedistributor(comm, topo, [1.0, 1.0, 1.0])
+        R.exchange_chunks = chunks
         if cfg == 5:
             workload = f"cfg5_rec36_per_gpu_{_m(n)}_full_exchange_plus_fine_sort_888"
             rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
@@ -418,7 +423,8 @@ def main():
             "config": {"workload": workload, "particles_per_gpu": n,
                        "grid": topo, "payload_bytes": rb, "position": pos_desc,
                        "parallelism": f"{world} rank(s), one GPU per grid cell" if multi
-                       else "1 GPU, 8 virtual subdomains"},
+                       else "1 GPU, 8 virtual subdomains",
+                       "exchange_chunks": chunks if multi else None},
             "roofline": roofline,
             "kernels": kernels,
             "xgmi": xgmi,
