@@ -390,7 +390,7 @@ def main():
     # host-counted bytes of the halo's selections
     fine_tr = int(_lib.load().mgr_ranked_tile_rows(36, 512)) if cfg == 5 else 2048
     for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr).items():
-        if k in kernels:
+        if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
             kernels[k]["alg_bytes_per_launch"] = b * n
     for k, e in kernels.items():
         if "alg_bytes_per_launch" in e:
