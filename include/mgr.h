@@ -278,6 +278,15 @@ int mgr_msel_pack(const void* src, int64_t row_bytes, int64_t n, const uint16_t*
 int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
                          const uint16_t* flags, int nsets, const int* masks, int tile_rows,
                          const void* workspace, void* const* dsts, void* stream);
+/* mgr_msel_pack_fields with the sets placed on the device: every set of
+ * field f back to back from dsts[f] (nfields pointers), set k at the scan's
+ * start of set k -- the caller needs no set sizes before the launch (the
+ * one-rank halo launches it before its one host sync).  Rows at or beyond
+ * cap_rows (>= 0) are not written; the caller compares the scanned total
+ * with cap_rows afterwards.                                               */
+int mgr_msel_pack_placed(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                         const uint16_t* flags, int nsets, const int* masks, int tile_rows,
+                         const void* workspace, void* const* dsts, int64_t cap_rows, void* stream);
 
 /* ------------------------------------------------------------ exchange --
  * Replaces comm.alltoall(send_buff) + np.concatenate (redist.py:199):

@@ -59,6 +59,7 @@ SIGNATURES = {
     "mgr_msel_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
     "mgr_msel_pack": (_I, [_P, _I64, _I64, _P, _I, _P, _I, _P, _P, _P]),
     "mgr_msel_pack_fields": (_I, [_I, _P, _P, _I64, _P, _I, _P, _I, _P, _P, _P]),
+    "mgr_msel_pack_placed": (_I, [_I, _P, _P, _I64, _P, _I, _P, _I, _P, _P, _I64, _P]),
     "mgr_group_p2p": (_I, [_P, _I, _P, _P, _P, _P, _P]),
     "mgr_comm_unique_id": (_I, [_P]),
     "mgr_comm_create": (_I, [_P, _I, _I, ctypes.POINTER(_P)]),

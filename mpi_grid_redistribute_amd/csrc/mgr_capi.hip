@@ -372,6 +372,26 @@ int mgr_msel_pack_fields(int nfields, const void* const* srcs, const int64_t* ro
     return MGR_OK;
 }
 
+int mgr_msel_pack_placed(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                         const uint16_t* flags, int nsets, const int* masks, int tile_rows,
+                         const void* workspace, void* const* dsts, int64_t cap_rows, void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc || (rc = check_sets(nsets, masks))) return rc;
+    if (nfields < 1 || nfields > 3 || !srcs || !row_bytes)
+        return fail(MGR_EINVAL, "nfields %d (1..3)", nfields);
+    if (cap_rows < 0) return fail(MGR_EINVAL, "cap_rows %lld", (long long)cap_rows);
+    for (int f = 0; f < nfields; ++f)
+        if (row_bytes[f] < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes[f]);
+    if (n > 0 && (!flags || !workspace || !dsts)) return fail(MGR_EINVAL, "null argument");
+    for (int f = 0; n > 0 && f < nfields; ++f)
+        if (!srcs[f] || (cap_rows > 0 && !dsts[f])) return fail(MGR_EINVAL, "null argument");
+    if (n <= 0 || cap_rows == 0) return MGR_OK;
+    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nsets, tile_rows);
+    HIP_OK(mgr::launch_msel_pack(nfields, srcs, row_bytes, n, flags, nsets, masks, tile_rows, ws,
+                                 dsts, (hipStream_t)stream, cap_rows));
+    return MGR_OK;
+}
+
 int mgr_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, void* dest,
                   uint32_t* bad_ids, void* workspace, void* stream) {
     int rc = check_tile(tile_rows);

@@ -103,7 +103,8 @@ hipError_t launch_msel_count(const uint16_t* flags, int64_t n, int nsets, const 
                              int tile_rows, const Workspace& ws, hipStream_t s);
 hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
                             int64_t n, const uint16_t* flags, int nsets, const int* masks,
-                            int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s);
+                            int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s,
+                            int64_t cap_rows = -1);
 hipError_t launch_count_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,
                             const Workspace& ws, void* dest, uint32_t* bad, hipStream_t s);
 hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows,

@@ -271,7 +271,7 @@ template <int W>
 __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_t row_bytes,
                                          uint8_t* const* dst, const long long* at,
                                          const int* start, const uint16_t* list, int fill,
-                                         int lane) {
+                                         int lane, long long cap) {
     using U = typename Unit<W>::T;
     const int64_t upr = row_bytes / W;
     const U* __restrict__ sp = (const U*)src;
@@ -288,7 +288,8 @@ __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_
                 const bool ok = lr < per && i < fill;
                 const unsigned e = list[ok ? i : 0];
                 const int k = (int)(e >> 10);
-                o[q] = ok ? (U*)dst[k] + (at[k] + (i - start[k])) * upr + u : nullptr;
+                const long long row = at[k] + (i - start[k]);
+                o[q] = ok && row < cap ? (U*)dst[k] + row * upr + u : nullptr;
                 v[q] = sp[(int64_t)(e & 1023u) * upr + u];
             }
 #pragma unroll
@@ -299,8 +300,10 @@ __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_
         for (int i = 0; i < fill; ++i) {
             const unsigned e = list[i];
             const int k = (int)(e >> 10);
+            const long long row = at[k] + (i - start[k]);
+            if (row >= cap) continue;
             const U* rs = sp + (int64_t)(e & 1023u) * upr;
-            U* rd = (U*)dst[k] + (at[k] + (i - start[k])) * upr;
+            U* rd = (U*)dst[k] + row * upr;
             for (int64_t q = lane; q < upr; q += 64) rd[q] = rs[q];
         }
     }
@@ -310,7 +313,7 @@ template <int NB>
 __global__ __launch_bounds__(256) void msel_pack_kernel(
     SelFields fs, int nf, int64_t n, const uint16_t* __restrict__ flags, int nsets, SetMasks masks,
     const int64_t* __restrict__ offsets, const int64_t* __restrict__ set_starts, int64_t T,
-    int tile_rows, const uint32_t* __restrict__ scan_err) {
+    int tile_rows, long long cap, const uint32_t* __restrict__ scan_err) {
     __shared__ uint16_t list_s[4][kSelCap];
     __shared__ uint8_t* dst_s[4][kSelFields][kMaxSets];
     __shared__ long long at_s[4][kMaxSets];    // next output row of every set
@@ -332,7 +335,8 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         if (lane == k) {
 #pragma unroll
             for (int f = 0; f < kSelFields; ++f) dst_s[w][f][k] = fs.dst[f][k];
-            at[k] = offsets[(int64_t)k * T + tile] - set_starts[k];
+            // set_starts == nullptr: the sets back to back from dst (placed on the device)
+            at[k] = offsets[(int64_t)k * T + tile] - (set_starts ? set_starts[k] : 0);
             cnt[k] = 0;
         }
     }
@@ -349,11 +353,11 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
                 const uint8_t* sp = fs.src[f] + (row0 + c0) * fs.row_bytes[f];
                 uint8_t* const* d = dst_s[w][f];
                 switch (fs.wlog[f]) {
-                    case 4: sel_copy<16>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
-                    case 3: sel_copy<8>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
-                    case 2: sel_copy<4>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
-                    case 1: sel_copy<2>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
-                    default: sel_copy<1>(sp, fs.row_bytes[f], d, at, start, list, fill, lane); break;
+                    case 4: sel_copy<16>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
+                    case 3: sel_copy<8>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
+                    case 2: sel_copy<4>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
+                    case 1: sel_copy<2>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
+                    default: sel_copy<1>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
                 }
             }
             wave_sync();
@@ -393,7 +397,8 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
 
 hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
                             int64_t n, const uint16_t* flags, int nsets, const int* masks,
-                            int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s) {
+                            int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s,
+                            int64_t cap_rows) {
     if (n <= 0) return hipSuccess;
     if (nfields < 1 || nfields > kSelFields || nsets < 1 || nsets > kMaxSets)
         return hipErrorInvalidValue;
@@ -405,8 +410,10 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
         fs.row_bytes[f] = row_bytes[f];
         uintptr_t a = (uintptr_t)srcs[f] | (uintptr_t)row_bytes[f];
         for (int k = 0; k < nsets; ++k) {
-            // a set is written in every field or in none (field 0 decides)
-            fs.dst[f][k] = dsts[0 * nsets + k] ? (uint8_t*)dsts[f * nsets + k] : nullptr;
+            // a set is written in every field or in none (field 0 decides);
+            // placed mode (cap_rows >= 0): every set of field f from dsts[f]
+            fs.dst[f][k] = cap_rows >= 0 ? (uint8_t*)dsts[f]
+                           : dsts[0 * nsets + k] ? (uint8_t*)dsts[f * nsets + k] : nullptr;
             a |= (uintptr_t)fs.dst[f][k];
         }
         fs.wlog[f] = (a & 15) == 0 ? 4 : (a & 7) == 0 ? 3 : (a & 3) == 0 ? 2 : (a & 1) == 0 ? 1 : 0;
@@ -420,7 +427,8 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
     const dim3 grid((unsigned)((ws.T + 3) / 4));
     prof_begin(s, K_HALO_PACK);
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, fs, nfields, n, flags, nsets, sb,
-                       ws.offsets, ws.bin_starts, ws.T, tile_rows, ws.scan_err);
+                       ws.offsets, cap_rows >= 0 ? nullptr : ws.bin_starts, ws.T, tile_rows,
+                       cap_rows >= 0 ? (long long)cap_rows : (long long)INT64_MAX, ws.scan_err);
     prof_end(s, K_HALO_PACK);
     return hipGetLastError();
 }

@@ -59,7 +59,7 @@ def plan_layout(send_counts, recv_counts, rank, redirect_self):
 
 
 def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=None,
-             scratch=None, pack_all=None):
+             scratch=None, pack_all=None, known_rows=None):
     """Run steps 1-4.  ``bin_counts``: int64 tensor [size] of rows per
     destination (on ``device``).  ``pack(field, send, redirect_bin, out,
     out_offset)`` packs field ``field`` (the redirect bin's rows into ``out``
@@ -69,12 +69,18 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
     else fresh allocations.  ``pack_all(sends, outs, redirect_bin,
     out_offsets)``, when given, packs every field in one call instead (fields
     moved by one kernel, e.g. rows with their fine cells).  Returns (outs, layout); outs are new flat uint8
-    tensors of (total_recv + extra) * row_bytes[f] bytes (>= 1 byte)."""
-    sc, rc = transport.exchange_counts(bin_counts)
-    for p in range(len(sc)):   # the count row: one int64 each way per peer
-        transport.note("send", p, 8)
-        transport.note("recv", p, 8)
-    check_counts(sc, rc)
+    tensors of (total_recv + extra) * row_bytes[f] bytes (>= 1 byte).
+    ``known_rows``: on one rank whose rows all stay, their number -- the
+    counts are not read back (no host sync) and the CALLER checks
+    ``bin_counts`` with its next host read (check_counts)."""
+    if known_rows is not None and transport.size == 1 and bin_counts.numel() == 1:
+        sc = rc = np.array([int(known_rows)], dtype=np.int64)
+    else:
+        sc, rc = transport.exchange_counts(bin_counts)
+        for p in range(len(sc)):   # the count row: one int64 each way per peer
+            transport.note("send", p, 8)
+            transport.note("recv", p, 8)
+        check_counts(sc, rc)
     lay = plan_layout(sc, rc, rank, transport.skips_self)
     extra = int(extra_rows(lay.total_recv)) if extra_rows is not None else 0
     outs, sends = [], []

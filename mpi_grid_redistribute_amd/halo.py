@@ -95,7 +95,7 @@ def self_halo_pieces(dim):
     return buf
 
 
-def _self_halo(transport, sel, srcs, rbs, flags, n, dim, carry_pos, arena, dev):
+def _self_halo(transport, sel, srcs, rbs, flags, n, dim, carry_pos, arena, dev, pending=()):
     """exchange_overload when every neighbour is this rank: all pieces are
     known from the local rows' flags, so one selection pass counts them all
     and one multi-set pack writes every row straight to each of its pieces
@@ -103,10 +103,26 @@ def _self_halo(transport, sel, srcs, rbs, flags, n, dim, carry_pos, arena, dev):
     and nothing is staged or received."""
     pieces = self_halo_pieces(dim)
     h, cnt = sel.msel_masks(flags, n, pieces, "_self")
-    counts = sel.to_host([cnt])[0]
-    _agree_counts(transport, counts, [])                    # the one host sync
-    total = int(counts.sum())
     F = len(rbs)
+    placed = arena is not None and arena[3] > 0
+    if placed:   # into the arena before the sizes are known: no gap at the sync
+        ast = [arena[0]] + ([arena[1]] if carry_pos else [])
+        sel.msel_pack_placed(h, srcs, rbs, [ast[f][arena[2] * rbs[f]:] for f in range(F)],
+                             arena[3])
+    got = sel.to_host([cnt] + list(pending))              # the one host sync
+    counts = got[0]
+    for c in got[1:]:   # the redistribution's deferred count check
+        check_counts(c, [])
+    _agree_counts(transport, counts, [])
+    total = int(counts.sum())
+    if placed and total <= arena[3]:
+        _lib.alg_add("halo_pack", 2 * n + 2 * total * sum(rbs))
+        if not total:
+            empty = torch.empty(0, dtype=torch.uint8, device=dev)
+            return empty, (empty if carry_pos else None), 0, True
+        b = arena[2]
+        out = [ast[f][b * rbs[f]:(b + total) * rbs[f]] for f in range(F)]
+        return out[0], (out[1] if carry_pos else None), total, True
     if arena is not None and total <= arena[3]:
         st, base, in_arena = [arena[0]] + ([arena[1]] if carry_pos else []), arena[2], True
     else:
@@ -231,6 +247,18 @@ class DeviceSelect:
         _lib.call("mgr_msel_pack_fields", nf, sp, rb, n, _lib.ptr(flags), k, cb, tile_rows,
                   _lib.ptr(ws), dp, _lib.stream_handle())
 
+    def msel_pack_placed(self, handle, srcs, row_bytes, dsts, cap_rows):
+        """msel_pack_fields with the sets back to back from dsts[f] at the
+        scan's set starts, rows beyond cap_rows not written: launched before
+        the set sizes are known on the host."""
+        n, flags, cb, k, ws, tile_rows = handle
+        nf = len(srcs)
+        sp = (ctypes.c_void_p * nf)(*[_lib.ptr(t) for t in srcs])
+        rb = (ctypes.c_int64 * nf)(*row_bytes)
+        dp = (ctypes.c_void_p * nf)(*[_lib.ptr(t) for t in dsts])
+        _lib.call("mgr_msel_pack_placed", nf, sp, rb, n, _lib.ptr(flags), k, cb, tile_rows,
+                  _lib.ptr(ws), dp, int(cap_rows), _lib.stream_handle())
+
     def to_host(self, tensors):
         """One device->host read of several small int64 tensors (one sync)."""
         flat = torch.cat([t.reshape(-1) for t in tensors]) if len(tensors) > 1 else tensors[0]
@@ -243,7 +271,8 @@ class DeviceSelect:
 
 
 def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n,
-                      overload_lengths, periodic=True, sel=None, arena=None, flags=None):
+                      overload_lengths, periodic=True, sel=None, arena=None, flags=None,
+                      pending=()):
     """Overload rows of rank R (redist.py:202-309).  ``data_flat``: flat uint8
     tensor of this rank's n payload rows of ``rbd`` bytes; ``pos_flat``: their
     positions (n, ncols) float32/float64 rows (ncols >= dim), or None when the
@@ -255,7 +284,9 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
     row, spare rows), e.g. the free tail of the redistribution's output, is
     used while the rows fit; beyond it the rows move once to a store of their
     own with headroom.  Returns (overload data flat, overload positions flat
-    or None, rows, whether they stayed in the arena)."""
+    or None, rows, whether they stayed in the arena).  ``pending``: device
+    count tensors of the caller whose check (check_counts) rides on this
+    exchange's first host read."""
     dim = R.dim
     assert len(overload_lengths) == dim, \
         "Overload lengths must be the same length as the dimensions"  # redist.py:245
@@ -275,7 +306,9 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
     selfd = [a == me and b == me for a, b, _, _ in nb]
     if dim <= 3 and all(selfd) and all(ka and kb for _, _, ka, kb in nb):
         return _self_halo(transport, sel, srcs[:F - 1], rbs[:F - 1], flags, n, dim, carry_pos,
-                          arena, dev)
+                          arena, dev, pending)
+    for c in pending:   # (the general path reads them here)
+        check_counts(c.cpu().numpy(), [])
 
     # 1. the local rows' counts of every dimension's two selections, one pass
     S = 2 * dim

@@ -415,8 +415,9 @@ class MPIGridRedistributor:
 
         hint = [rows.row_bytes, 2] + ([self._pos_row_bytes(position, pos)] if rp else [])
         extra = lambda m_: halo_capacity(self, m_, overload_lengths)  # noqa: E731
+        pending = []   # one rank: the scan's counts checked at the halo's host read
         outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=hint,
-                            extra_rows=extra, side_ids=True)
+                            extra_rows=extra, side_ids=True, deferred=pending)
         rbd = rows.row_bytes
         rbp = fields[2].row_bytes if rp else 0
         cap = outs[0].numel() // max(rbd, 1) - m
@@ -426,7 +427,7 @@ class MPIGridRedistributor:
             self, self.comm, outs[0][: m * rbd], rbd, outs[2][: m * rbp] if rp else None,
             int(position.shape[1]), pos.code, m, list(overload_lengths), periodic=True,
             sel=DeviceSelect(self._dev, self._scratch),
-            arena=(outs[0], outs[2] if rp else None, m, cap), flags=flags)
+            arena=(outs[0], outs[2] if rp else None, m, cap), flags=flags, pending=pending)
         if in_place:   # redist.py:166: concatenate(data, overload)
             res_d = outs[0][: (m + mo) * rbd]
             res_p = outs[2][: (m + mo) * rbp] if rp else None
@@ -579,10 +580,13 @@ class MPIGridRedistributor:
         outs, m = self._run([rows], binner, rows.n, drop=True)
         return rows.wrap(outs[0], m)
 
-    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None, side_ids=None):
+    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None, side_ids=None,
+             deferred=None):
         """bin -> scan -> count exchange -> pack -> row exchange.  ``side_ids``:
         field 1 is the rows' 2-byte side field (fine cells), packed by the
-        same kernel as field 0 (mgr_pack_ids)."""
+        same kernel as field 0 (mgr_pack_ids).  ``deferred`` (a list): on one
+        rank without drops the counts are not read back; the scan's count
+        tensor is appended to it for the caller's next host read to check."""
         P = self.size
         nb = P + 1 if drop else P
         hint = row_bytes_hint or [f.row_bytes for f in fields]
@@ -651,9 +655,13 @@ class MPIGridRedistributor:
                                            pack_chunk, k, extra_rows=extra_rows,
                                            scratch=self._scratch.get)
             return outs, lay.total_recv
+        known = None
+        if deferred is not None and P == 1 and not drop:
+            known = n
+            deferred.append(bin_counts)
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
                              self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
-                             pack_all=pack_all if side_ids else None)
+                             pack_all=pack_all if side_ids else None, known_rows=known)
         return outs, lay.total_recv
 
     @property

@@ -79,6 +79,15 @@ class CpuSelect:
             self.msel_pack(handle, src, rb, [t if t0 is not None else None
                                              for t, t0 in zip(d, dsts[0])])
 
+    def msel_pack_placed(self, handle, srcs, row_bytes, dsts, cap_rows):
+        """Sets back to back from dsts[f]; rows at or beyond cap_rows dropped."""
+        for src, rb, d in zip(srcs, row_bytes, dsts):
+            s = src.numpy()
+            rows = s[: (len(s) // rb) * rb].reshape(-1, rb)
+            idx = np.concatenate(list(handle))[:cap_rows] if len(handle) else np.zeros(0, int)
+            if len(idx):
+                d[: len(idx) * rb].copy_(torch.from_numpy(rows[idx].reshape(-1).copy()))
+
     def to_host(self, tensors):
         return [t.numpy().copy() for t in tensors]
 
