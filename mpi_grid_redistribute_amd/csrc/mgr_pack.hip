@@ -259,6 +259,7 @@ __global__ __launch_bounds__(256) void compact_kernel(
 // gather.  Rows wider than 64 units are copied one after the other, lanes
 // across the row.
 constexpr int kSelCap = 2048;   // LDS entries per wave (>= kSelChunk)
+constexpr int kSelDepth = 4;    // copy instructions in flight per field (8: 1.17 vs 1.10 ms)
 constexpr int kSelFields = 3;
 struct SelFields {
     const uint8_t* src[kSelFields];
@@ -279,11 +280,11 @@ __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_
         const int per = 64 / (int)upr;   // rows per copy instruction
         const int lr = lane / (int)upr;
         const int u = lane - lr * (int)upr;
-        for (int i0 = 0; i0 < fill; i0 += 4 * per) {
-            U v[4];
-            U* o[4];
+        for (int i0 = 0; i0 < fill; i0 += kSelDepth * per) {
+            U v[kSelDepth];
+            U* o[kSelDepth];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < kSelDepth; ++q) {
                 const int i = i0 + q * per + lr;
                 const bool ok = lr < per && i < fill;
                 const unsigned e = list[ok ? i : 0];
@@ -293,7 +294,7 @@ __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_
                 v[q] = sp[(int64_t)(e & 1023u) * upr + u];
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < kSelDepth; ++q)
                 if (o[q]) *o[q] = v[q];
         }
     } else {

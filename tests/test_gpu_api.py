@@ -155,6 +155,27 @@ def test_halo_scan_failure_raises():
     assert len(out) > 0
 
 
+@pytest.mark.parametrize("ol", [0.1, 0.45])
+def test_one_rank_halo_deferred_count_check_raises(ol):
+    """One rank with overload_lengths: the redistribution's counts are not
+    read back (all rows stay) -- a failed scan must still raise, at the
+    halo's host read."""
+    rng = np.random.default_rng(9)
+    n = 200_000
+    pos = rng.random((n, 3))
+    data = np.arange(n)
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    ol = [ol] * 3
+    _lib.tune("scan_spins", -1)
+    try:
+        with pytest.raises(_lib.MgrError, match="scan failed"):
+            R.redistribute_by_position(data, pos.copy(), overload_lengths=ol)
+    finally:
+        _lib.tune("scan_spins", 1 << 24)
+    out = R.redistribute_by_position(data, pos.copy(), overload_lengths=ol)
+    assert len(out) > n
+
+
 def test_no_device_allocation_after_warmup():
     """Skewed inputs of changing size on repeated calls: after warm-up the
     redistributor reuses its scratch (workspace, destination bytes, send
