@@ -343,9 +343,14 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
     }
     wave_sync();
     const int nbits = mask_bits(masks, nsets);
+    uint32_t fn[kSelWords];   // the next chunk's flags, loaded a chunk ahead
+    chunk_flags(flags, row0, min(kSelChunk, rows), lane, fn);
     for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
         uint32_t fw[kSelWords];
-        chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
+#pragma unroll
+        for (int i = 0; i < kSelWords; ++i) fw[i] = fn[i];
+        if (c0 + kSelChunk < rows)
+            chunk_flags(flags, row0 + c0 + kSelChunk, min(kSelChunk, rows - c0 - kSelChunk), lane, fn);
         FlagPlanes fp;
         flag_planes_t<NB>(fw, nbits, fp);
         auto flush = [&](int fill) {

@@ -400,7 +400,11 @@ class MPIGridRedistributor:
         spare capacity (no concatenation copies)."""
         flags_src = self._scratch.get("halo_flags_src", max(rows.n, 1) * 2)
         rp = bool(return_positions)
-        fields = [rows, _IdField(flags_src)] + ([None] if rp else [])
+        # one rank: the rows keep their order (one bin, nothing dropped), so the
+        # selections read the binning's flags in place -- no flag field packed
+        one = self.size == 1
+        fields = [rows] + ([] if one else [_IdField(flags_src)]) + ([None] if rp else [])
+        ip = len(fields) - 1                                 # the positions' field
         cl = np.ascontiguousarray(self.cell_length, dtype=np.float64)
         ol = np.ascontiguousarray(np.asarray(overload_lengths, dtype=np.float64))
 
@@ -411,32 +415,35 @@ class MPIGridRedistributor:
                       tile_rows, _lib.ptr(ws), _lib.stream_handle())
             pos.finish()
             if rp:   # redist.py:164: the wrapped positions travel with the rows
-                fields[2] = Rows(position, self._dev)
+                fields[ip] = Rows(position, self._dev)
 
-        hint = [rows.row_bytes, 2] + ([self._pos_row_bytes(position, pos)] if rp else [])
+        hint = ([rows.row_bytes] + ([] if one else [2])
+                + ([self._pos_row_bytes(position, pos)] if rp else []))
         extra = lambda m_: halo_capacity(self, m_, overload_lengths)  # noqa: E731
         pending = []   # one rank: the scan's counts checked at the halo's host read
         outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=hint,
-                            extra_rows=extra, side_ids=True, deferred=pending)
+                            extra_rows=extra, side_ids=not one, deferred=pending)
         rbd = rows.row_bytes
-        rbp = fields[2].row_bytes if rp else 0
+        rbp = fields[ip].row_bytes if rp else 0
         cap = outs[0].numel() // max(rbd, 1) - m
-        flags = outs[1][: 2 * m].view(torch.int16) if m else torch.empty(
+        fsrc = flags_src if one else outs[1]
+        flags = fsrc[: 2 * m].view(torch.int16) if m else torch.empty(
             0, dtype=torch.int16, device=self._dev)
+        op = outs[ip] if rp else None
         ov_d, ov_p, mo, in_place = exchange_overload(
-            self, self.comm, outs[0][: m * rbd], rbd, outs[2][: m * rbp] if rp else None,
+            self, self.comm, outs[0][: m * rbd], rbd, op[: m * rbp] if rp else None,
             int(position.shape[1]), pos.code, m, list(overload_lengths), periodic=True,
             sel=DeviceSelect(self._dev, self._scratch),
-            arena=(outs[0], outs[2] if rp else None, m, cap), flags=flags, pending=pending)
+            arena=(outs[0], op, m, cap), flags=flags, pending=pending)
         if in_place:   # redist.py:166: concatenate(data, overload)
             res_d = outs[0][: (m + mo) * rbd]
-            res_p = outs[2][: (m + mo) * rbp] if rp else None
+            res_p = op[: (m + mo) * rbp] if rp else None
         else:
             res_d = torch.cat([outs[0][: m * rbd], ov_d])
-            res_p = torch.cat([outs[2][: m * rbp], ov_p]) if rp else None
+            res_p = torch.cat([op[: m * rbp], ov_p]) if rp else None
         res = rows.wrap(res_d, m + mo)
         if rp:
-            return res, fields[2].wrap(res_p, m + mo)
+            return res, fields[ip].wrap(res_p, m + mo)
         return res
 
     def _fine_plan(self, fine_cells):
