@@ -213,11 +213,13 @@ def main():
                     help="run the N>1 path (config 3, RCCL exchange) even at one GPU")
     ap.add_argument("--chunks", type=int, default=0,
                     help="N > 1: pack the tiles in this many chunks, each chunk's rows sent "
-                         "while the next is packed (exchange_pipelined); 0 = 4 for N > 1, else 1")
+                         "while the next is packed (exchange_pipelined); 0 = the product default "
+                         "(redistributor.exchange_chunks_for)")
     args = ap.parse_args()
 
     import mpi_grid_redistribute_amd as mgr
     from mpi_grid_redistribute_amd import _lib
+    from mpi_grid_redistribute_amd.exchange import count_skew
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -246,7 +248,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = args.config or (3 if multi else 2)
-    chunks = args.chunks or (4 if world > 1 else 1)
+    chunks = args.chunks or None      # None: the product's own choice
     if multi and cfg == 2:
         cfg = 3
     topo = topology_for(world) if multi else [2, 2, 2]
@@ -291,6 +293,7 @@ def main():
         comm = mgr.RcclComm.from_torch_distributed()
         R = mgr.MPIGridRedistributor(comm, topo, [1.0, 1.0, 1.0])
         R.exchange_chunks = chunks
+        chunks = chunks or mgr.redistributor.exchange_chunks_for(world, rb + (2 if cfg == 5 else 0))
         if cfg == 5:
             workload = f"cfg5_rec36_per_gpu_{_m(n)}_full_exchange_plus_fine_sort_888"
             rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
@@ -317,11 +320,12 @@ def main():
     # kernel skips slabs whose bits did not change, which after the first
     # step is every slab of these re-used inputs; that would time a
     # repeat-call steady state, so every timed f64 step writes back as on
-    # fresh input.  f32 positions (config 5) wrap in f64 and round back to
-    # the same f32 bits (S9: x + L is exact), so fresh f32 input is clean and
-    # keeps the skip.
+    # fresh input (a per-plan option of this bench's own partitioner or
+    # redistributor, not process state).  f32 positions (config 5) wrap in f64
+    # and round back to the same f32 bits (S9: x + L is exact), so fresh f32
+    # input is clean and keeps the skip.
     if cfg != 5:
-        _lib.tune("bin_skip_clean", 0)
+        (R if multi else part).set_write_back("all")
 
     def barrier():
         if dist is not None:
@@ -381,6 +385,19 @@ def main():
             if cnt:
                 kernels[k] = {"avg_ms": ms / cnt, "launches": cnt, "in_timed_region": False}
     _lib.profile_select(None)
+    # the count matrix's max/mean (load imbalance of the
+    # redistribution: rows each destination receives, max over mean) -- the
+    # N=1 line's 1 x 8 row of virtual destinations, or the N>1 ranks' count rows
+    # gathered after the timed region
+    skew = None
+    if not multi and cfg in (2, 4):
+        skew = count_skew(part.buffers(n, 32)[4].cpu().numpy().reshape(1, -1))
+    elif multi:
+        sc = torch.as_tensor(R.last_counts[0], dtype=torch.int64, device="cuda")
+        rows = [torch.empty_like(sc) for _ in range(world)] if world > 1 else [sc]
+        if world > 1:
+            dist.all_gather(rows, sc)
+        skew = count_skew(torch.stack(rows).cpu().numpy())
     xgmi = None
     if multi and "exchange" in kernels:
         xgmi = xgmi_report(R.last_traffic, kernels["exchange"], dist, world)
@@ -428,6 +445,7 @@ def main():
             "roofline": roofline,
             "kernels": kernels,
             "xgmi": xgmi,
+            "count_skew": skew,
             "cpu_baseline": cpu,
             "cpu_baseline_cfg1": cpu_1,
             "cpu_baseline_c": cpu_c,

@@ -77,6 +77,14 @@ int mgr_plan_create(int dim, const int64_t* grid_topology, const double* box_len
 int mgr_plan_create_fine(int dim, const int64_t* grid_topology, const int64_t* fine,
                          const double* box_length, int box_dtype, mgr_plan** out);
 int mgr_plan_destroy(mgr_plan* plan);
+/* Position write-back of the periodic wrap (redist.py:68, :328-329 mutate
+ * `position` in place).  MGR_WRITE_BACK_CHANGED (default): a 64-row slab is
+ * stored only if one of its coordinates changed under the wrap -- the bytes
+ * in memory are the reference's either way.  MGR_WRITE_BACK_ALL: every slab
+ * is stored, the cost fresh input pays (87.5 % of uniform in-box f64 rows
+ * change under x + L - L); bench.py times this.  Per plan, not process-wide. */
+enum { MGR_WRITE_BACK_CHANGED = 0, MGR_WRITE_BACK_ALL = 1 };
+int mgr_plan_set_write_back(mgr_plan* plan, int mode);
 
 /* Rows per tile used by the histogram / pack kernels for rows of at most
  * max_row_bytes bytes and nbins destinations (a multiple of 64 rows).      */
@@ -142,7 +150,7 @@ int mgr_cell_number_from_indexes(const mgr_plan* plan, const int64_t* idx, int64
  * segment start of every (bin, tile), bin starts, and per-bin totals
  * (bin_counts, int64[nbins], device) = the element counts of the
  * reference's send_buff[i] (redist.py:195-198).  Consumes what a count
- * producer (mgr_bin_count / mgr_bin_ids / mgr_select_count) left in the
+ * producer (mgr_bin_count / mgr_bin_ids / mgr_msel_count ...) left in the
  * workspace, including the zeroed one-pass scan words: one producer
  * launch precedes every scan on the same stream.
  * Failure: the scan never hangs the GPU.  If a look-back gives up (a chunk's
@@ -237,14 +245,9 @@ int mgr_bin_starts(int64_t n, int nbins, int tile_rows, const void* workspace,
  * mgr_halo_flags  : one pass over n position rows; flags[r] (uint16) bit 2d =
  *                   coordinate d > hi[d], bit 2d+1 = coordinate d < lo[d].
  *                   hi/lo: host arrays of dim doubles.
- * mgr_select_count: selection (flags & mask) != 0 as a 2-bin partition for
- *                   mgr_scan / mgr_pack (bin 0 = selected, in order; bin 1 =
- *                   not selected, pass drop_bin = 1 to mgr_pack).  Workspace
- *                   sized by mgr_workspace_bytes(n, 2, tile_rows).           */
+ *                   (exchange_overload_by_position on caller rows).       */
 int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
                    const double* hi, const double* lo, uint16_t* flags, void* stream);
-int mgr_select_count(const uint16_t* flags, int64_t n, int mask, void* dest, int tile_rows,
-                     void* workspace, void* stream);
 /* The halo face flags computed by the binning kernel itself, against the
  * limits of the cell each row lands in: mgr_bin_count + flags[r] (uint16, the
  * layout of mgr_halo_flags) for cell_length[d] (numpy's box/topology,
@@ -303,6 +306,14 @@ int mgr_comm_size(const mgr_comm* comm);
 int mgr_exchange_counts(mgr_comm* comm, const int64_t* send_counts, int64_t* recv_counts,
                         void* stream);
 
+/* All-to-all of `width` int64 per peer in one RCCL group: row p of send
+ * ([size][width], device) goes to peer p, row s of recv comes from peer s.
+ * The pipelined exchange sends [total, chunk counts...] per peer, so the totals
+ * and the per-chunk counts take one host sync (replaces redist.py:199's count
+ * alltoall; the chunks have no reference counterpart). */
+int mgr_exchange_count_rows(mgr_comm* comm, const int64_t* send, int64_t* recv, int width,
+                            void* stream);
+
 /* Grouped ncclSend/ncclRecv of nfields packed, bin-major fields.  Counts and
  * offsets are in ROWS and live on the host.  Rows from source s land at
  * recv[f] + recv_offsets[s]*row_bytes[f]: source order (S7).  skip_self:
@@ -348,33 +359,8 @@ int mgr_comm_allreduce_max_f64(mgr_comm* comm, const double* in, double* out, in
 int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const double* box,
                       double* pos, void* rec32, void* stream);
 
-/* -------------------------------------------------------------- tuning --
- * Kernel-variant knobs for A/B measurement: "bin_staged", "bin_skip_clean",
- * "bin_waves", "bin_geo", "xcd_bin", "pack_coop", "xcd_pack", "tile_rounds",
- * "scan_chunk", "scan_max_chunks", "pack_img", "img_rpw", "pack_sel", "pack_compact",
- * "pack_many", "pack_fine", "many_super", "many_rows", "rank_rows", "scan_spins" (polls
- * per look-back word before the scan gives up; -1 gives up at once, for
- * tests of the failure path) and "prof_mask" (bit k: time profiler kernel id
- * k, in the order of the names listed under profiling below; default all)
- * (mgr_internal.h Tune); the defaults are the shipped configuration.
- * Process-wide: call between launches, not concurrently with them.        */
-int mgr_tune(const char* key, int64_t value);
-
-/* ----------------------------------------------------------- profiling --
- * Per-kernel HIP-event timing of every launch made while enabled, on the
- * launch's own stream.  mgr_profile_read synchronises those events and
- * returns the accumulated device time (ms) and launch count of the named
- * kernel ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx",
- * "synth", "halo" (mgr_halo_flags, mgr_msel_count), "bin_fine"
- * (mgr_bin_count_fine), "count_ids" (mgr_count_ids, mgr_rank_ids),
- * "pack_fine" (the 65..1024-bin sorted-image and ranked packs),
- * "pack_narrow" (rows < 4 bytes), "halo_pack" (mgr_msel_pack*)) or of the
- * RCCL grouped row exchange ("exchange").                                  */
-int mgr_profile_enable(int on);
-int mgr_profile_reset(void);
-int mgr_profile_read(const char* kernel, double* total_ms, int64_t* launches);
-/* Profiler id of a kernel name (its bit in the "prof_mask" knob), < 0 if unknown. */
-int mgr_profile_kernel_id(const char* kernel);
+/* Measurement and test hooks (mgr_test_hook, mgr_profile_*) are not part of
+ * the drop-in boundary: include/mgr_instrument.h.                          */
 
 #ifdef __cplusplus
 }

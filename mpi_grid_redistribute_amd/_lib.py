@@ -1,4 +1,5 @@
-"""ctypes binding of libmgr.so (C ABI: include/mgr.h).
+"""ctypes binding of libmgr.so (C ABI: include/mgr.h; measurement and test
+hooks: include/mgr_instrument.h).
 
 The HIP library is the only compute path: if it is missing or cannot be
 loaded, every entry point raises -- there is no CPU or eager fallback.
@@ -32,6 +33,7 @@ SIGNATURES = {
     "mgr_plan_create": (_I, [_I, _P, _P, _I, _I, ctypes.POINTER(_P)]),
     "mgr_plan_create_fine": (_I, [_I, _P, _P, _P, _I, ctypes.POINTER(_P)]),
     "mgr_plan_destroy": (_I, [_P]),
+    "mgr_plan_set_write_back": (_I, [_P, _I]),
     "mgr_tile_rows": (_I, [_I64, _I]),
     "mgr_ranked_tile_rows": (_I, [_I64, _I]),
     "mgr_workspace_bytes": (_I64, [_I64, _I, _I]),
@@ -54,7 +56,6 @@ SIGNATURES = {
                                        _P, _P]),
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
     "mgr_halo_flags": (_I, [_P, _I, _I64, _I64, _I, _P, _P, _P, _P]),
-    "mgr_select_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
     "mgr_bin_count_halo": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P, _P, _I, _P, _P]),
     "mgr_msel_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
     "mgr_msel_pack": (_I, [_P, _I64, _I64, _P, _I, _P, _I, _P, _P, _P]),
@@ -67,16 +68,22 @@ SIGNATURES = {
     "mgr_comm_rank": (_I, [_P]),
     "mgr_comm_size": (_I, [_P]),
     "mgr_exchange_counts": (_I, [_P, _P, _P, _P]),
+    "mgr_exchange_count_rows": (_I, [_P, _P, _P, _I, _P]),
     "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "mgr_exchange_schedule": (_I, [_I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I]),
     "mgr_comm_allreduce_max_f64": (_I, [_P, _P, _P, _I64, _P]),
     "mgr_synth_uniform": (_I, [ctypes.c_uint64, _I64, _I64, _I, _P, _P, _P, _P]),
-    "mgr_tune": (_I, [ctypes.c_char_p, _I64]),
+}
+# include/mgr_instrument.h: measurement and test hooks (not the boundary).
+INSTRUMENT_SIGNATURES = {
+    "mgr_test_hook": (_I, [ctypes.c_char_p, _I64]),
     "mgr_profile_enable": (_I, [_I]),
     "mgr_profile_reset": (_I, []),
+    "mgr_profile_select": (_I, [_I64]),
     "mgr_profile_read": (_I, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _PI64]),
     "mgr_profile_kernel_id": (_I, [ctypes.c_char_p]),
 }
+MGR_WRITE_BACK_CHANGED, MGR_WRITE_BACK_ALL = 0, 1
 
 
 class MgrError(RuntimeError):
@@ -121,7 +128,7 @@ def load():
                 f"libmgr.so not found at {LIB_PATH}: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
         lib = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in {**SIGNATURES, **INSTRUMENT_SIGNATURES}.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -158,9 +165,15 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
 
 
-def tune(key, value):
-    """Kernel-variant knob (A/B measurement only; defaults are shipped)."""
-    call("mgr_tune", key.encode(), int(value))
+def test_hook(key, value):
+    """mgr_test_hook: make a fallback path run for the parity tests
+    (include/mgr_instrument.h; results are unchanged, defaults are shipped)."""
+    call("mgr_test_hook", key.encode(), int(value))
+
+
+HOOK_DEFAULTS = {"tile_rounds": 0, "scan_chunk": 2048, "scan_max_chunks": 1024,
+                 "scan_spins": 1 << 24, "pack_img_all": 0, "rank_rows": 0, "bin_unstaged": 0,
+                 "bin_generic": 0, "pack_generic": 0}
 
 
 # --------------------------------------------------------------- profiler
@@ -196,7 +209,7 @@ def profile_select(kernels=None):
     """Time only these kernels (None: all).  Every timed launch adds two HIP
     event records to its stream, so a benchmark times just what it reports."""
     if kernels is None:
-        tune("prof_mask", -1)
+        call("mgr_profile_select", -1)
         return
     mask = 0
     for k in kernels:
@@ -204,7 +217,7 @@ def profile_select(kernels=None):
         if kid < 0:
             check(kid, "mgr_profile_kernel_id")
         mask |= 1 << kid
-    tune("prof_mask", mask)
+    call("mgr_profile_select", mask)
 
 
 def profile_reset():

@@ -123,6 +123,13 @@ class Transport:
         Returns (send_counts_host, recv_counts_host) as int64 numpy arrays."""
         raise NotImplementedError
 
+    def exchange_count_rows(self, send):
+        """send: int64 tensor [size][w] (device or host), row p for peer p.
+        Returns (send_host, recv_host) int64 numpy [size][w], recv row s from
+        peer s -- one message per peer and one host sync (the pipelined
+        exchange's totals + per-chunk counts)."""
+        raise NotImplementedError
+
     def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
                       recv_offsets):
         """sends/outs: per-field uint8 tensors; counts/offsets in rows (host)."""
@@ -167,6 +174,10 @@ class SelfComm(Transport):
 
     def exchange_counts(self, send_counts):
         s = send_counts.detach().to("cpu").numpy().astype(np.int64)
+        return s, s.copy()
+
+    def exchange_count_rows(self, send):
+        s = send.detach().to("cpu").numpy().astype(np.int64)
         return s, s.copy()
 
     def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
@@ -231,6 +242,20 @@ class RcclComm(Transport):
         host = self._pinned.numpy().copy()
         return host[:P], host[P:]
 
+    def exchange_count_rows(self, send):
+        send = send.contiguous()
+        P, w = self.size, int(send.shape[1])
+        recv = torch.empty_like(send)
+        _lib.call("mgr_exchange_count_rows", self._h, _lib.ptr(send), _lib.ptr(recv), w,
+                  _lib.stream_handle())
+        if self._pinned.numel() < 2 * P * w:
+            self._pinned = torch.empty(2 * P * w, dtype=torch.int64, pin_memory=True)
+        self._pinned[: P * w].copy_(send.reshape(-1), non_blocking=True)
+        self._pinned[P * w: 2 * P * w].copy_(recv.reshape(-1), non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        host = self._pinned[: 2 * P * w].numpy().copy()
+        return host[: P * w].reshape(P, w), host[P * w:].reshape(P, w)
+
     def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
                       recv_offsets):
         nf = len(sends)
@@ -285,6 +310,11 @@ class MpiHostComm(Transport):
         s = send_counts.detach().to("cpu").numpy().astype(np.int64)
         r = self.comm.alltoall([int(x) for x in s])
         return s, np.asarray(r, dtype=np.int64)
+
+    def exchange_count_rows(self, send):
+        s = send.detach().to("cpu").numpy().astype(np.int64)
+        r = self.comm.alltoall([[int(x) for x in row] for row in s])
+        return s, np.asarray(r, dtype=np.int64).reshape(s.shape)
 
     def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,
                       recv_offsets):
@@ -347,6 +377,13 @@ class TorchDistComm(Transport):
         recv = torch.empty_like(send_counts)
         self.dist.all_to_all_single(recv, send_counts.contiguous(), group=self.group)
         return (send_counts.detach().cpu().numpy().astype(np.int64),
+                recv.detach().cpu().numpy().astype(np.int64))
+
+    def exchange_count_rows(self, send):
+        send = send.contiguous()
+        recv = torch.empty_like(send)
+        self.dist.all_to_all_single(recv.view(-1), send.view(-1), group=self.group)
+        return (send.detach().cpu().numpy().astype(np.int64),
                 recv.detach().cpu().numpy().astype(np.int64))
 
     def exchange_rows(self, sends, outs, row_bytes, send_counts, send_offsets, recv_counts,

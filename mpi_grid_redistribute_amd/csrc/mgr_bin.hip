@@ -281,7 +281,7 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
                 : hg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideHalo>
                      : bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideNone>;
     if constexpr (DIM == 3 && kP && NU > 0) {
-        const int geo = g_tune.bin_geo ? geo_kind(g, sizeof(PosT) == 4) : kGeoAny;
+        const int geo = hooks().bin_generic ? kGeoAny : geo_kind(g, sizeof(PosT) == 4);
         if (geo == kGeoF32)
             k = fg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideFine, kGeoF32>
                    : hg ? bin_count_kernel<PosT, kP, DestT, NU, DIM, true, 1, kSideHalo, kGeoF32>
@@ -297,17 +297,18 @@ static hipError_t bin_count_t(const Geom& g, void* pos, int64_t n, int64_t strid
     if (hg) h = *hg;
     const int rb = (int)(stride * (int64_t)sizeof(PosT));
     const int per_wave = NU > 0 ? align16(64 * rb) : 0;     // staging slab
-    // <= bin_waves waves, whole rounds each.  Auto (0): 1 wave for f32
-    // positions (in-box rows wrap to themselves: a read-mostly pass, which
-    // streams best with more rounds per wave), 2 for f64 (the write-back)
-    const int want = g_tune.bin_waves > 0 ? g_tune.bin_waves : (sizeof(PosT) == 4 ? 1 : 2);
+    // waves per workgroup, whole rounds each: 1 for f32 positions (in-box rows
+    // wrap to themselves: a read-mostly pass, which streams best with more
+    // rounds per wave), 2 for f64 (the write-back) -- A/B: 1/2/4/8/16 waves,
+    // DESIGN.md §3.1 and §3.3
+    const int want = sizeof(PosT) == 4 ? 1 : 2;
     int nwaves = tile_rows / 64;
     while (nwaves > want || (tile_rows / 64) % nwaves) --nwaves;
     const int lds = align16(g.nbins * 4) + per_wave * nwaves;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nwaves), (size_t)lds, s, (PosT*)pos, n,
                        stride, g, (DestT*)dest, ws.counts, ws.T, tile_rows, per_wave,
-                       g_tune.bin_skip_clean, g_tune.xcd_bin || g.nbins > 64, ws.flags, f, h,
+                       !g.write_back_all, g.nbins > 64, ws.flags, f, h,
                        side_out);
     return hipGetLastError();
 }
@@ -329,7 +330,7 @@ static hipError_t bin_count_w(const Geom& g, void* pos, int64_t n, int64_t strid
                               int tile_rows, const Workspace& ws, hipStream_t s,
                               const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
     const int64_t rb = stride * (int64_t)sizeof(PosT);
-    if (g_tune.bin_staged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0) {
+    if (!hooks().bin_unstaged && rb <= kStageMaxRowBytes && ((uintptr_t)pos & 15) == 0) {
         switch ((int)((rb + 15) / 16)) {   // 16-byte units per lane per 64-row slab
             case 1: return bin_count_dim<PosT, kP, DestT, 1>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
             case 2: return bin_count_dim<PosT, kP, DestT, 2>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
@@ -416,72 +417,61 @@ __global__ __launch_bounds__(kBlock) void count_ids_kernel(const uint16_t* __res
 // the tile (tile_starts[t][b], tile-major, contiguous) and its count (counts[b
 // * T + t], for mgr_scan).  The ranking work leaves the pack, which then only
 // places rows.
-// ORM: a round's peers by LDS atomics -- every lane ORs its lane bit into its
-// bin's 64-bit word of the wave, reads the word back (the peers), the
-// leader clears it -- 3 LDS operations and a few VALU per round instead of
-// nbits ballots with their 64-bit selects (the ballot match kept VALU-bound at
-// ~180 instructions per round).  OR commutes, so the result does not depend on
-// the order the LDS unit serves the lanes in.
-// RPW > 0 / NBITS > 0: the rounds per wave and the id bits at compile time;
-// 0: read at run time.
-template <int NW, int RPW, int NBITS, bool ORM>
+// A round's peers by LDS atomics: every lane ORs its lane bit into its bin's
+// 64-bit word of the wave, reads the word back (the peers), the leader clears
+// it -- 3 LDS operations and a few VALU per round instead of nbits ballots
+// with their 64-bit selects (the ballot match measured VALU-bound at ~180
+// instructions per round: 0.223 vs 0.146-0.155 ms per 64M ids).  OR commutes,
+// so the result does not depend on the order the LDS unit serves the lanes in.
+// RPW: the rounds per wave (the ranked tiles are 2048 or 4096 rows).
+template <int NW, int RPW>
 __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
-    const uint16_t* __restrict__ ids, int64_t n, int nbins, int nbits,
-    int32_t* __restrict__ counts, int64_t T, int tile_rows, uint16_t* __restrict__ slots,
+    const uint16_t* __restrict__ ids, int64_t n, int nbins,
+    int32_t* __restrict__ counts, int64_t T, uint16_t* __restrict__ slots,
     uint16_t* __restrict__ tile_starts, uint64_t* __restrict__ scan_flags,
     uint32_t* __restrict__ bad) {
-    constexpr int NT = NW * 64, RPW_MAX = RPW > 0 ? RPW : 4096 / 64 / NW;
+    constexpr int NT = NW * 64, TR = NW * 64 * RPW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    // [NW][nbins] peer words (ORM), then [NW][nbins] running counts
+    // [NW][nbins] peer words, then [NW][nbins] running counts
     unsigned long long* mk = (unsigned long long*)smem;
-    uint16_t* wt = (uint16_t*)(smem + (ORM ? NW * nbins * 8 : 0));
+    uint16_t* wt = (uint16_t*)(smem + NW * nbins * 8);
     __shared__ int s_wsum[NW];
     clear_scan_flags(scan_flags);
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const int64_t tile = xcd_tile(blockIdx.x, T);
-    const int rpw = RPW > 0 ? RPW : tile_rows / 64 / NW;
     for (int i = tid; i < NW * nbins; i += NT) {
         wt[i] = 0;
-        if (ORM) mk[i] = 0ull;
+        mk[i] = 0ull;
     }
-    unsigned b[RPW_MAX];
+    unsigned b[RPW];
     bool oob = false;   // ids >= nbins: clamped, reported through *bad
 #pragma unroll
-    for (int q = 0; q < RPW_MAX; ++q) {
-        if (RPW == 0 && q >= rpw) break;
-        const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
+    for (int q = 0; q < RPW; ++q) {
+        const int64_t row = tile * TR + (int64_t)(w * RPW + q) * 64 + lane;
         b[q] = row < n ? (unsigned)ids[row] : 0u;
     }
 #pragma unroll
-    for (int q = 0; q < RPW_MAX; ++q) {
-        if (RPW == 0 && q >= rpw) break;
+    for (int q = 0; q < RPW; ++q)
         if (b[q] >= (unsigned)nbins) { b[q] = nbins - 1; oob = true; }
-    }
     if (__any(oob) && lane == 0 && bad) atomicOr(bad, 1u);
     __syncthreads();
     unsigned long long* mw = mk + w * nbins;
     uint16_t* ww = wt + w * nbins;
-    int rk[RPW_MAX];
+    int rk[RPW];
 #pragma unroll
-    for (int q = 0; q < RPW_MAX; ++q) {
-        if (RPW == 0 && q >= rpw) break;
-        const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
+    for (int q = 0; q < RPW; ++q) {
+        const int64_t row = tile * TR + (int64_t)(w * RPW + q) * 64 + lane;
         const bool valid = row < n;
-        unsigned long long peers;
-        if constexpr (ORM) {
-            if (valid) __hip_atomic_fetch_or(&mw[b[q]], 1ull << lane, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-            wave_sync();
-            peers = valid ? mw[b[q]] : 0ull;
-        } else {
-            peers = match_bin_t<NBITS>(b[q], valid, nbits);
-        }
+        if (valid) __hip_atomic_fetch_or(&mw[b[q]], 1ull << lane, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WAVEFRONT);
+        wave_sync();
+        const unsigned long long peers = valid ? mw[b[q]] : 0ull;
         const int r = rank_in(peers);
         const int before = valid ? (int)ww[b[q]] : 0;
         wave_sync();
         if (valid && r == 0) {
             ww[b[q]] = (uint16_t)(before + __popcll(peers));
-            if (ORM) mw[b[q]] = 0ull;
+            mw[b[q]] = 0ull;
         }
         wave_sync();
         rk[q] = before + r;
@@ -529,9 +519,8 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
         __syncthreads();
     }
 #pragma unroll
-    for (int q = 0; q < RPW_MAX; ++q) {
-        if (RPW == 0 && q >= rpw) break;
-        const int64_t row = tile * tile_rows + (int64_t)(w * rpw + q) * 64 + lane;
+    for (int q = 0; q < RPW; ++q) {
+        const int64_t row = tile * TR + (int64_t)(w * RPW + q) * 64 + lane;
         if (row < n) slots[row] = (uint16_t)(ww[b[q]] + rk[q]);
     }
 }
@@ -540,23 +529,16 @@ hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_r
                            const Workspace& ws, uint16_t* slots, uint16_t* tile_starts,
                            uint32_t* bad, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    prof_begin(s, K_COUNT_IDS);
+    // the ranked tiles (ranked_tile_rows: <= 1024 bins, 2048 or 4096 rows);
     // 4 waves (16 waves measured 0.57 vs 0.31 ms at 64M rows, 512 bins)
-    const int nw = kWaves;
-    // LDS peer words while they fit next to the counts (<= 2048 bins)
-    const bool orm = g_tune.rank_orm && nbins <= 2048;
-    const int lds = align16(nw * nbins * 2) + (orm ? nw * nbins * 8 : 0);
-    const bool b9 = nbits_for(nbins) == 9;   // 257..512 cells (8x8x8)
-    auto k = orm ? (tile_rows == 4096 ? rank_ids_kernel<kWaves, 16, 0, true>
-                    : tile_rows == 2048 ? rank_ids_kernel<kWaves, 8, 0, true>
-                                        : rank_ids_kernel<kWaves, 0, 0, true>)
-           : tile_rows == 4096 ? (b9 ? rank_ids_kernel<kWaves, 16, 9, false> : rank_ids_kernel<kWaves, 16, 0, false>)
-           : tile_rows == 2048 ? (b9 ? rank_ids_kernel<kWaves, 8, 9, false> : rank_ids_kernel<kWaves, 8, 0, false>)
-                               : rank_ids_kernel<kWaves, 0, 0, false>;
+    if (nbins < 1 || nbins > 2048 || (tile_rows != 2048 && tile_rows != 4096))
+        return hipErrorNotSupported;
+    const int lds = align16(kWaves * nbins * 2) + kWaves * nbins * 8;
+    auto k = tile_rows == 4096 ? rank_ids_kernel<kWaves, 16> : rank_ids_kernel<kWaves, 8>;
+    prof_begin(s, K_COUNT_IDS);
     ensure_lds(k, lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * nw), (size_t)lds, s, ids, n, nbins,
-                       nbits_for(nbins), ws.counts, ws.T, tile_rows, slots, tile_starts,
-                       ws.flags, bad);
+    hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(64 * kWaves), (size_t)lds, s, ids, n, nbins,
+                       ws.counts, ws.T, slots, tile_starts, ws.flags, bad);
     prof_end(s, K_COUNT_IDS);
     return hipGetLastError();
 }

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -100,7 +101,8 @@ const char* kernel_name(int k) {
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 
-static bool prof_selected(int k) { return g_prof_on && ((g_tune.prof_mask >> k) & 1); }
+std::atomic<int64_t> g_prof_mask{-1};   // mgr_profile_select: bit k times kernel id k
+static bool prof_selected(int k) { return g_prof_on && ((g_prof_mask.load(std::memory_order_relaxed) >> k) & 1); }
 
 void prof_begin(hipStream_t s, int k) {
     if (!prof_selected(k)) return;
@@ -221,6 +223,14 @@ int mgr_plan_create_fine(int dim, const int64_t* topo, const int64_t* fine, cons
 
 int mgr_plan_destroy(mgr_plan* plan) {
     delete plan;
+    return MGR_OK;
+}
+
+int mgr_plan_set_write_back(mgr_plan* plan, int mode) {
+    if (!plan) return fail(MGR_EINVAL, "null plan");
+    if (mode != MGR_WRITE_BACK_CHANGED && mode != MGR_WRITE_BACK_ALL)
+        return fail(MGR_EINVAL, "write-back mode %d", mode);
+    plan->g.write_back_all = mode == MGR_WRITE_BACK_ALL;
     return MGR_OK;
 }
 
@@ -595,18 +605,6 @@ int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride
     return MGR_OK;
 }
 
-int mgr_select_count(const uint16_t* flags, int64_t n, int mask, void* dest, int tile_rows,
-                     void* workspace, void* stream) {
-    int rc = check_tile(tile_rows);
-    if (rc) return rc;
-    if (n < 0) return fail(MGR_EINVAL, "n < 0");
-    if (n > 0 && (!flags || !dest || !workspace)) return fail(MGR_EINVAL, "null argument");
-    const mgr::Workspace ws = mgr::carve(workspace, n, 2, tile_rows);
-    HIP_OK(mgr::launch_select_count(flags, n, (unsigned)mask, (uint8_t*)dest, tile_rows, ws,
-                                    (hipStream_t)stream));
-    return MGR_OK;
-}
-
 // ------------------------------------------------------------ exchange
 int mgr_comm_unique_id(void* out_id) {
     if (!out_id) return fail(MGR_EINVAL, "null id");
@@ -671,13 +669,19 @@ struct Group {
 
 int mgr_exchange_counts(mgr_comm* comm, const int64_t* send_counts, int64_t* recv_counts,
                         void* stream) {
-    if (!comm || !send_counts || !recv_counts) return fail(MGR_EINVAL, "null argument");
+    return mgr_exchange_count_rows(comm, send_counts, recv_counts, 1, stream);
+}
+
+int mgr_exchange_count_rows(mgr_comm* comm, const int64_t* send, int64_t* recv, int width,
+                            void* stream) {
+    if (!comm || !send || !recv) return fail(MGR_EINVAL, "null argument");
+    if (width < 1) return fail(MGR_EINVAL, "width %d", width);
     hipStream_t s = (hipStream_t)stream;
     NCCL_OK(ncclGroupStart());
     Group g;
     for (int p = 0; p < comm->size; ++p) {
-        GROUP_CALL(g, ncclSend(send_counts + p, 1, ncclInt64, p, comm->nccl, s));
-        GROUP_CALL(g, ncclRecv(recv_counts + p, 1, ncclInt64, p, comm->nccl, s));
+        GROUP_CALL(g, ncclSend(send + (int64_t)p * width, (size_t)width, ncclInt64, p, comm->nccl, s));
+        GROUP_CALL(g, ncclRecv(recv + (int64_t)p * width, (size_t)width, ncclInt64, p, comm->nccl, s));
     }
     return g.end();
 }
@@ -826,60 +830,12 @@ int mgr_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim, const dou
     return MGR_OK;
 }
 
-// -------------------------------------------------------------- tuning
-int mgr_tune(const char* key, int64_t value) {
+// ---------------------------------------------------------- test hooks
+int mgr_test_hook(const char* key, int64_t value) {
     if (!key) return fail(MGR_EINVAL, "null key");
-    if (!strcmp(key, "bin_staged")) mgr::g_tune.bin_staged = (int)value;
-    else if (!strcmp(key, "pack_coop")) mgr::g_tune.pack_coop = (int)value;
-    else if (!strcmp(key, "bin_geo")) mgr::g_tune.bin_geo = (int)value;
-    else if (!strcmp(key, "ranked_walk")) mgr::g_tune.ranked_walk = (int)value;
-    else if (!strcmp(key, "rank_orm")) mgr::g_tune.rank_orm = (int)value;
-    else if (!strcmp(key, "img_rpw")) {
-        if (value != 1 && value != 2) return fail(MGR_EINVAL, "img_rpw %lld (1 or 2)", (long long)value);
-        mgr::g_tune.img_rpw = (int)value;
-    }
-    else if (!strcmp(key, "rank_rows")) {
-        if (value != 0 && value != 2048 && value != 4096)
-            return fail(MGR_EINVAL, "rank_rows %lld (0, 2048 or 4096)", (long long)value);
-        mgr::g_tune.rank_rows = (int)value;
-    }
-    else if (!strcmp(key, "many_rows")) {
-        if (value != 0 && value != 1024 && value != 2048 && value != 4096)
-            return fail(MGR_EINVAL, "many_rows %lld (0, 1024, 2048 or 4096)", (long long)value);
-        mgr::g_tune.many_rows = (int)value;
-    }
-    else if (!strcmp(key, "bin_skip_clean")) mgr::g_tune.bin_skip_clean = (int)value;
-    else if (!strcmp(key, "xcd_bin")) mgr::g_tune.xcd_bin = (int)value;
-    else if (!strcmp(key, "xcd_pack")) mgr::g_tune.xcd_pack = (int)value;
-    else if (!strcmp(key, "pack_many")) mgr::g_tune.pack_many = (int)value;
-    else if (!strcmp(key, "pack_img")) mgr::g_tune.pack_img = (int)value;
-    else if (!strcmp(key, "pack_sel")) mgr::g_tune.pack_sel = (int)value;
-    else if (!strcmp(key, "pack_compact")) mgr::g_tune.pack_compact = (int)value;
-    else if (!strcmp(key, "scan_max_chunks")) {
-        if (value < 1 || value > mgr::kScanFlags) return fail(MGR_EINVAL, "scan_max_chunks %lld", (long long)value);
-        mgr::g_tune.scan_max_chunks = (int)value;
-    }
-    else if (!strcmp(key, "many_super")) {
-        if (value < 1 || value > 16) return fail(MGR_EINVAL, "many_super %lld", (long long)value);
-        mgr::g_tune.many_super = (int)value;
-    }
-    else if (!strcmp(key, "scan_chunk")) {
-        if (value < 256 || value > (1 << 20)) return fail(MGR_EINVAL, "scan_chunk %lld", (long long)value);
-        mgr::g_tune.scan_chunk = (int)value;
-    }
-    else if (!strcmp(key, "prof_mask")) mgr::g_tune.prof_mask = value;
-    else if (!strcmp(key, "scan_spins")) {
-        if (value < -1 || value > (1 << 30)) return fail(MGR_EINVAL, "scan_spins %lld", (long long)value);
-        mgr::g_tune.scan_spins = (int)value;
-    } else if (!strcmp(key, "bin_waves")) {
-        if (value < 0 || value > 16) return fail(MGR_EINVAL, "bin_waves %lld", (long long)value);
-        mgr::g_tune.bin_waves = (int)value;
-    }
-    else if (!strcmp(key, "tile_rounds")) {
-        if (value < 0 || value > 16)
-            return fail(MGR_EINVAL, "tile_rounds %lld", (long long)value);
-        mgr::g_tune.tile_rounds = (int)value;
-    } else return fail(MGR_EINVAL, "unknown tuning key '%s'", key);
+    if (mgr::set_hook(key, value))
+        return fail(MGR_EINVAL, "unknown test hook '%s' or value %lld out of range", key,
+                    (long long)value);
     return MGR_OK;
 }
 
@@ -898,6 +854,11 @@ int mgr_profile_reset(void) {
         mgr::g_ms[k] = 0.0;
         mgr::g_cnt[k] = 0;
     }
+    return MGR_OK;
+}
+
+int mgr_profile_select(int64_t mask) {
+    mgr::g_prof_mask.store(mask, std::memory_order_relaxed);
     return MGR_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "mgr.h"
+#include "mgr_instrument.h"
 
 namespace mgr {
 
@@ -14,8 +15,7 @@ constexpr int kMaxTileRows = 65536;      // many-bin pack tiles (super-rounds of
 constexpr int kCoopMaxRounds = 64;       // cooperative pack tiles <= 4096 rows
 constexpr int kLdsBudget = 78 * 1024;    // per pack workgroup: 2 workgroups per CU (160 KiB)
 constexpr int kScanFlags = 4096;         // one-pass scan: chunks (= workgroups) at most
-constexpr int kMaxSets = 32;
-constexpr int kTrashBytes = 256 * 512;   // 512 B per workgroup of a persistent grid (<= 256)             // multi-selection sets per pass (halo pieces <= 26)
+constexpr int kMaxSets = 32;           // multi-selection sets per pass (halo pieces <= 26)
 
 // One-pass scan control words, right behind the kScanFlags chunk words and
 // zeroed with them by every count producer.
@@ -48,6 +48,7 @@ struct Geom {
     int fine;                            // fine-cell plan (mgr_plan_create_fine)
     int64_t fmod[MGR_MAX_DIM];           // fine cells per rank cell and dimension
     int fast32;                          // every n[d] < 2^30: in-box rows bin in 32-bit ints
+    int write_back_all;                  // mgr_plan_set_write_back: every slab written back
 };
 
 // The fine cells a row falls in, inside its destination's cell (SURVEY f4,
@@ -75,7 +76,7 @@ struct Workspace {
     int64_t* offsets;    // [nbins][T] exclusive scan of counts
     int64_t* bin_starts; // [nbins + 1]
     uint64_t* flags;     // [kScanFlags] one-pass scan chunk words + ScanCtl; zeroed
-                         // by the count producers (bin_count, bin_ids, select_count)
+                         // by the count producers (bin_count, bin_ids, rank_ids, msel_count)
     const uint32_t* scan_err;  // &ScanCtl::err: packs return at once when set
     int64_t T;
     int64_t t0 = 0, tn = 0;    // the tiles [t0, t0 + tn) one pack launch covers (all: 0, T)
@@ -134,35 +135,29 @@ hipError_t launch_tile_offsets(const Workspace& ws, int nbins, const int64_t* ti
 int ranked_tile_rows(int64_t row_bytes, int nbins);
 hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
-hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,
-                               int tile_rows, const Workspace& ws, hipStream_t s);
 
-// Tuning knobs (mgr_tune); defaults are the shipped configuration.
-struct Tune {
-    int bin_staged = 1;    // stage 64-row position slabs through LDS
-    int tile_rounds = 0;   // 0: automatic; else rows per wave tile / 64
-    int pack_coop = 1;     // one workgroup per tile, one wave per round (<= 64 bins)
-    int bin_skip_clean = 1;  // write a position slab back only if a row changed
-    int xcd_bin = 0;       // XCD-contiguous tile order in the bin kernel
-    int xcd_pack = 16;     // ... in the pack kernels: tiles dealt in chunks of 16 per XCD (1: one run per XCD)
-    int pack_many = 1;     // cooperative pack with an LDS count table for 65..1024 bins
-    int bin_waves = 0;     // waves per bin workgroup (1..16; a tile's rounds split over them; 0: auto)
-    int many_super = 1;    // pack_many: 4096-row super-rounds per tile (A/B: 2-16 slower)
-    int pack_compact = 1;  // selections (2 bins, bin 1 dropped): wave-per-tile compaction
-    int pack_sel = 1;      // selection packs (2 bins, one dropped) load only kept rows
-    int pack_img = 1;      // 16-byte-unit image pack for 4-byte-multiple rows (1: 24..60 B, 2: 12..60 B)
-    int scan_chunk = 2048; // one-pass scan: counts per chunk (8 per thread, one block scan)
+// Test hooks (include/mgr_instrument.h, mgr_test_hook): switches that make a
+// product-reachable fallback or shape run on inputs that would not take it,
+// so the parity tests reach every path.  None changes results.  Launches read
+// an immutable snapshot (hooks()); mgr_test_hook publishes a new one as a
+// whole, so a launch sees either the old or the new set, never a mix.  The
+// shipped configuration is the default-constructed snapshot.
+struct Hooks {
+    int tile_rounds = 0;     // != 0: pack/bin tiles of 64 * tile_rounds rows
+    int scan_chunk = 2048;   // one-pass scan: counts per chunk (8 per thread)
     int scan_max_chunks = 1024;  // one-pass scan: at most this many chunks (look-back depth)
-    int scan_spins = 1 << 24;    // one-pass scan: polls per look-back word before giving up
-                                 // (-1: give up at once -- tests of the error path)
-    int img_rpw = 2;       // image pack: 64-row rounds per wave (1 or 2)
-    int bin_geo = 1;       // bin kernel: compile-time geometry when the plan's is simple (geo_kind)
-    int rank_orm = 1;      // rank_ids: peers by LDS OR words (1) or ballot match (0)
-    int ranked_walk = 0;   // ranked pack tile walk: 0 one region per XCD, 1 all XCDs in one region
-    int rank_rows = 0;     // ranked fine sort tiles: 0 automatic (4096 when the LDS image fits), 2048, 4096
-    int many_rows = 0;     // pack_many: rows per super-round (1024/2048/4096; 0: automatic)
-    int64_t prof_mask = -1;  // profiler: bit k times kernel id k (mgr_profile_*)
+    int scan_spins = 1 << 24;    // polls per look-back word before giving up (-1: at once)
+    int pack_img_all = 0;    // image pack for every 4-byte-multiple row of 12..60 B (else 24..60)
+    int rank_rows = 0;       // ranked fine sort tiles: 0 automatic, 2048, 4096
+    int bin_unstaged = 0;    // bin kernel without LDS slab staging (the wide / unaligned fallback)
+    int bin_generic = 0;     // bin kernel with run-time geometry also for simple plans
+    int pack_generic = 0;    // wave-per-tile pack_kernel also for <= 64 bins (the > 64-B row path)
 };
-extern Tune g_tune;
+const Hooks& hooks();
+int set_hook(const char* key, int64_t value);   // mgr_test_hook
+
+// Shipped constants that were A/B knobs (DESIGN.md §3.3 records the A/Bs).
+constexpr int kXcdPackChunk = 16;   // packs: tiles dealt to the XCDs in chunks of 16
+constexpr int kImgRoundsPerWave = 2;  // image pack: 64-row rounds per wave
 
 }  // namespace mgr

@@ -17,14 +17,47 @@
 
 //
 // Translation units: mgr_bin.hip (binning), mgr_pack.hip (pack), this file
-// (tuning state, workspace, scan, halo selection, synthetic input); shared
+// (test hooks, workspace, scan, halo selection, synthetic input); shared
 // device helpers in mgr_device.h.
 
 #include "mgr_device.h"
 
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
 namespace mgr {
 
-Tune g_tune;
+// The test-hook snapshots: every published set is kept until exit (a launch
+// may still hold a reference to an older one; there are a handful per test
+// run), the current one behind an atomic pointer.
+static const Hooks kShipped{};
+static std::atomic<const Hooks*> g_hooks{&kShipped};
+static std::mutex g_hooks_mu;
+
+const Hooks& hooks() { return *g_hooks.load(std::memory_order_acquire); }
+
+int set_hook(const char* key, int64_t v) {
+    std::lock_guard<std::mutex> lk(g_hooks_mu);
+    static std::vector<std::unique_ptr<Hooks>> kept;
+    auto h = std::make_unique<Hooks>(hooks());
+    auto in = [&](int64_t lo, int64_t hi) { return v >= lo && v <= hi; };
+    if (!strcmp(key, "tile_rounds") && in(0, 64)) h->tile_rounds = (int)v;
+    else if (!strcmp(key, "scan_chunk") && in(256, 1 << 20)) h->scan_chunk = (int)v;
+    else if (!strcmp(key, "scan_max_chunks") && in(1, kScanFlags)) h->scan_max_chunks = (int)v;
+    else if (!strcmp(key, "scan_spins") && in(-1, 1 << 30)) h->scan_spins = (int)v;
+    else if (!strcmp(key, "pack_img_all") && in(0, 1)) h->pack_img_all = (int)v;
+    else if (!strcmp(key, "rank_rows") && (v == 0 || v == 2048 || v == 4096)) h->rank_rows = (int)v;
+    else if (!strcmp(key, "bin_unstaged") && in(0, 1)) h->bin_unstaged = (int)v;
+    else if (!strcmp(key, "bin_generic") && in(0, 1)) h->bin_generic = (int)v;
+    else if (!strcmp(key, "pack_generic") && in(0, 1)) h->pack_generic = (int)v;
+    else return -1;
+    g_hooks.store(h.get(), std::memory_order_release);
+    kept.push_back(std::move(h));
+    return 0;
+}
 
 // ------------------------------------------------------------------ scan
 // One-pass scan (decoupled look-back).  Chunks never straddle a bin: chunk
@@ -218,48 +251,6 @@ __global__ __launch_bounds__(kBlock) void halo_flags_kernel(const PosT* __restri
             f |= (x < t.lo[d] ? 1u : 0u) << (2 * d + 1);
         }
         flags[r] = (uint16_t)f;
-    }
-}
-
-// Selection as a 2-bin partition for mgr_scan / mgr_pack: bin 0 = selected
-// ((flags & mask) != 0), bin 1 = not (the drop bin).  Wave-private tiles of
-// tile_rows rows; counts[b * T + tile].
-__global__ __launch_bounds__(kBlock) void select_count_kernel(const uint16_t* __restrict__ flags,
-                                                              int64_t n, unsigned mask,
-                                                              uint8_t* __restrict__ dest,
-                                                              int32_t* __restrict__ counts,
-                                                              int64_t T, int tile_rows,
-                                                              uint64_t* __restrict__ scan_flags) {
-    clear_scan_flags(scan_flags);
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * kWaves + w;
-    if (tile >= T) return;
-    const int64_t row0 = tile * (int64_t)tile_rows;
-    const int rows = (int)min((int64_t)tile_rows, n - row0);
-    int sel = 0, all = 0;
-    // batches of 8 rounds: the 8 flag loads of a batch are in flight together
-    // (one at a time left the wave latency-bound at ~3 TB/s)
-    constexpr int B = 8;
-    for (int r0 = 0; r0 < rows; r0 += 64 * B) {
-        unsigned f[B];
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-            const int r = r0 + 64 * q + lane;
-            f[q] = r < rows ? (unsigned)flags[row0 + r] : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-            const int r = r0 + 64 * q + lane;
-            const bool valid = r < rows;
-            const bool on = valid && (f[q] & mask) != 0;
-            if (valid) dest[row0 + r] = on ? 0 : 1;
-            sel += __popcll(__ballot(on));
-            all += __popcll(__ballot(valid));
-        }
-    }
-    if (lane == 0) {
-        counts[tile] = sel;
-        counts[T + tile] = all - sel;
     }
 }
 
@@ -470,9 +461,9 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
         if (e == hipSuccess && bin_counts) e = hipMemsetAsync(bin_counts, 0, (size_t)nbins * 8, s);
         return e;
     }
-    const int64_t target = g_tune.scan_chunk;         // counts per chunk (workgroup)
+    const int64_t target = hooks().scan_chunk;         // counts per chunk (workgroup)
     int64_t cpb = (ws.T + target - 1) / target;
-    int64_t cap = min((int64_t)g_tune.scan_max_chunks, (int64_t)kScanFlags) / nbins;
+    int64_t cap = min((int64_t)hooks().scan_max_chunks, (int64_t)kScanFlags) / nbins;
     if (cap < 1) cap = 1;                             // nbins <= MGR_MAX_BINS = kScanFlags
     if (cpb > cap) cpb = cap;
     const int64_t chunk = (ws.T + cpb - 1) / cpb;
@@ -481,7 +472,7 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     auto k = chunk <= 8 * kBlock ? scan_onepass_kernel<8> : scan_onepass_kernel<16>;
     hipLaunchKernelGGL(k, dim3((unsigned)(nbins * cpb)), dim3(kBlock), 0, s, ws.counts, ws.T,
                        chunk, (int)cpb, nbins, ws.flags, ws.offsets, ws.bin_starts, bin_counts,
-                       g_tune.scan_spins);
+                       hooks().scan_spins);
     prof_end(s, K_SCAN);
     return hipGetLastError();
 }
@@ -505,16 +496,6 @@ hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t st
     return hipGetLastError();
 }
 
-hipError_t launch_select_count(const uint16_t* flags, int64_t n, unsigned mask, uint8_t* dest,
-                               int tile_rows, const Workspace& ws, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int64_t grid = (ws.T + kWaves - 1) / kWaves;
-    prof_begin(s, K_HALO);
-    hipLaunchKernelGGL(select_count_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, flags, n,
-                       mask, dest, ws.counts, ws.T, tile_rows, ws.flags);
-    prof_end(s, K_HALO);
-    return hipGetLastError();
-}
 
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s) {

@@ -174,75 +174,6 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
 }
 
-// Compaction for selections (2 bins, bin 1 dropped: the halo's rows to send,
-// redist.py:271-275): one wave per tile walks its rounds, ballots the kept
-// rows, and each kept row is copied by its own lane to the tile's bin-0
-// segment.  Per row only the destination byte is read unless it is kept, so a
-// sparse selection costs ~1 byte per row plus the kept rows -- the
-// cooperative pack reads every row and pays its per-tile barrier.
-template <int W, int UPR>
-__global__ __launch_bounds__(256) void compact_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest,
-    const int64_t* __restrict__ offsets, int64_t T, int64_t t0, int64_t tn, int tile_rows,
-    uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
-    using U = typename Unit<W>::T;
-    constexpr int D = 4;   // rounds per batch (8 measured the same: sparse rows cost whole lines)
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tl = (int64_t)blockIdx.x * 4 + w;
-    if (tl >= tn || scan_failed(scan_err)) return;
-    const int64_t tile = t0 + tl;
-    const int64_t row0 = tile * (int64_t)tile_rows;
-    const int rows = (int)min((int64_t)tile_rows, n - row0);
-    long long base = offsets[tile];          // bin 0 (kept) segment of the tile
-    const U* __restrict__ s_u = (const U*)src + row0 * UPR;
-    U* __restrict__ d_u = (U*)dst;
-    unsigned nb_[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
-        const int r = 64 * q + lane;
-        nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
-    }
-    for (int r0 = 0; r0 < rows; r0 += 64 * D) {
-        unsigned long long m[D];
-#pragma unroll
-        for (int q = 0; q < D; ++q) m[q] = __ballot(nb_[q] == 0u);
-        // next batch's destination bytes in flight
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-            const int r = r0 + 64 * (D + q) + lane;
-            nb_[q] = r < rows ? (unsigned)dest[row0 + r] : 1u;
-        }
-        // unit-transposed loads of the kept rows only (lane l: units 64k + l);
-        // a dropped row's lanes all read the tile's first unit (one cached
-        // line, no HBM traffic) so every load is unconditional and the
-        // values stay in registers (a predicated load into an array is
-        // demoted to scratch)
-        U v[D][UPR];
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-#pragma unroll
-            for (int k = 0; k < UPR; ++k) {
-                const int u = 64 * k + lane, r = u / UPR;
-                const int64_t idx = ((m[q] >> r) & 1ull) ? (int64_t)(r0 + 64 * q) * UPR + u : 0;
-                v[q][k] = s_u[idx];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-#pragma unroll
-            for (int k = 0; k < UPR; ++k) {
-                const int u = 64 * k + lane, r = u / UPR, part = u - r * UPR;
-                if ((m[q] >> r) & 1ull) {
-                    const long long slot = base + __popcll(m[q] & ((1ull << r) - 1ull));
-                    d_u[slot * UPR + part] = v[q][k];
-                }
-            }
-            base += __popcll(m[q]);
-        }
-    }
-}
-
-
 // Multi-selection pack (the halo's sends, msel counts + mgr_scan with nbins
 // = nsets), up to kSelFields fields of the same rows in one launch.  Set k's
 // rows of field f go, in row order, to dsts[f][k] (null: set k is not
@@ -436,70 +367,6 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
                        ws.offsets, cap_rows >= 0 ? nullptr : ws.bin_starts, ws.T, tile_rows,
                        cap_rows >= 0 ? (long long)cap_rows : (long long)INT64_MAX, ws.scan_err);
     prof_end(s, K_HALO_PACK);
-    return hipGetLastError();
-}
-
-// Rows of any width: one lane copies one kept row.
-template <int W>
-__global__ __launch_bounds__(256) void compact_any_kernel(
-    const uint8_t* __restrict__ src, int64_t upr, int64_t n, const uint8_t* __restrict__ dest,
-    const int64_t* __restrict__ offsets, int64_t T, int64_t t0, int64_t tn, int tile_rows,
-    uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
-    using U = typename Unit<W>::T;
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tl = (int64_t)blockIdx.x * 4 + w;
-    if (tl >= tn || scan_failed(scan_err)) return;
-    const int64_t tile = t0 + tl;
-    const int64_t row0 = tile * (int64_t)tile_rows;
-    const int rows = (int)min((int64_t)tile_rows, n - row0);
-    long long base = offsets[tile];
-    const U* __restrict__ s_u = (const U*)src;
-    U* __restrict__ d_u = (U*)dst;
-    for (int r0 = 0; r0 < rows; r0 += 64) {
-        const bool keep = r0 + lane < rows && dest[row0 + r0 + lane] == 0;
-        const unsigned long long m = __ballot(keep);
-        if (keep) {
-            const U* sp = s_u + (row0 + r0 + lane) * upr;
-            U* dp = d_u + (base + rank_in(m)) * upr;
-            for (int64_t k = 0; k < upr; ++k) dp[k] = sp[k];
-        }
-        base += __popcll(m);
-    }
-}
-
-template <int W>
-static hipError_t compact_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
-                            int tile_rows, const Workspace& ws, void* dst, hipStream_t s) {
-    const dim3 grid((unsigned)((ws.tn + 3) / 4));
-    const int upr = (int)(row_bytes / W);
-#define MGR_CK(U_)                                                                             \
-    case U_:                                                                                   \
-        hipLaunchKernelGGL((compact_kernel<W, U_>), grid, dim3(256), 0, s, (const uint8_t*)src, \
-                           n, (const uint8_t*)dest, ws.offsets, ws.T, ws.t0, ws.tn, tile_rows,  \
-                           (uint8_t*)dst, ws.scan_err);                                         \
-        return hipGetLastError();
-    if (64 * W <= 1024 || upr <= 4) {
-        switch (upr) {
-            MGR_CK(1) MGR_CK(2) MGR_CK(3) MGR_CK(4)
-            default: break;
-        }
-    }
-    if (W <= 8) {
-        switch (upr) {
-            MGR_CK(5) MGR_CK(6) MGR_CK(7) MGR_CK(8)
-            default: break;
-        }
-    }
-    if (W == 4) {
-        switch (upr) {
-            MGR_CK(9) MGR_CK(10) MGR_CK(11) MGR_CK(12) MGR_CK(13) MGR_CK(14) MGR_CK(15) MGR_CK(16)
-            default: break;
-        }
-    }
-#undef MGR_CK
-    hipLaunchKernelGGL(compact_any_kernel<W>, grid, dim3(256), 0, s, (const uint8_t*)src,
-                       row_bytes / W, n, (const uint8_t*)dest, ws.offsets, ws.T, ws.t0, ws.tn,
-                       tile_rows, (uint8_t*)dst, ws.scan_err);
     return hipGetLastError();
 }
 
@@ -837,23 +704,19 @@ struct SideField {
     bool used = false;
 };
 
-// pack_many_kernel: super-rounds of 64 * R rows (the uint16 [R][nbins] LDS
-// table stays <= 128 KiB at 4096 rows and 1024 bins), many_super super-rounds
-// per tile (A/B: longer per-bin runs, slower).
+// pack_many_kernel: one super-round of 64 * R rows per tile (the uint16
+// [R][nbins] LDS table stays <= 128 KiB at 4096 rows and 1024 bins; A/B: 2-16
+// super-rounds per tile, i.e. longer per-bin runs, measured slower).
 // Up to 512 bins 2048-row super-rounds (8x8x8 cells, 64M 36-byte rows: pack
 // 1.43-1.49 vs 1.55-1.70 ms at 4096 rows and 1.70 at 1024; the bin kernel and
 // the scan pay ~+0.05 ms each for the twice larger histogram; whole sort 2.17-2.24
 // vs 2.19-2.34 ms; 120 cells 1.85 vs 2.03 ms); above 512 bins 4096 rows (1024
 // cells: 2.53 vs 2.84 ms -- there the [bins][tiles] histogram dominates).
 // profiles/round1/fine_many_ab.log, fine_shapes_ab.log.
-static int many_round_rows(int nbins) {
-    if (g_tune.many_rows > 0) return g_tune.many_rows;
-    return nbins <= 512 ? 2048 : 4096;
-}
-static int many_tile_rows(int nbins) { return many_round_rows(nbins) * g_tune.many_super; }
+static int many_round_rows(int nbins) { return nbins <= 512 ? 2048 : 4096; }
 
 int pack_tile_rows(int64_t row_bytes, int nbins) {
-    if (g_tune.tile_rounds > 0) return 64 * g_tune.tile_rounds;
+    if (hooks().tile_rounds > 0) return 64 * hooks().tile_rounds;
     // <= 16 bins: 512-row tiles (bin: 4 waves x 2 rounds; pack: 8 waves x
     // 1 round; A/B against 1024 at 8 bins: bin -3 %, pack within noise);
     // <= 64 bins: 1024 rows (64 bins: pack 0.92 vs 1.07 ms at 512: longer
@@ -864,9 +727,9 @@ int pack_tile_rows(int64_t row_bytes, int nbins) {
     // workgroup; A/B at 36 B: bin 0.382 vs 0.418, scan 0.014 vs 0.023, pack
     // 0.850 vs 0.856 ms per 64M)
     const bool img = row_bytes % 4 == 0 && row_bytes % 16 != 0 && row_bytes >= 24 && row_bytes <= 60;
-    if (nbins <= 16) return img && g_tune.img_rpw == 2 ? 1024 : 512;
+    if (nbins <= 16) return img ? 1024 : 512;
     if (nbins <= 64) return 1024;
-    if (g_tune.pack_many && nbins <= 1024 && row_bytes <= 64) return many_tile_rows(nbins);
+    if (nbins <= 1024 && row_bytes <= 64) return many_round_rows(nbins);
     int r = 16;
     while (r < 4096 / 64 && (int64_t)nbins * 4 > (int64_t)r * 8) r *= 2;
     return 64 * r;
@@ -894,7 +757,7 @@ template <int W, int UPR>
 static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                               void* redirect_dst, hipStream_t s, SideField* side) {
-    if (!g_tune.pack_coop || tile_rows > 2048) return hipErrorNotSupported;
+    if (hooks().pack_generic || tile_rows > 2048) return hipErrorNotSupported;
     // one wave per RPW 64-row rounds of the tile (<= 16 waves)
     const int rpw = tile_rows > 1024 ? 2 : 1;
     const int threads = tile_rows / rpw;
@@ -903,12 +766,12 @@ static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int 
                        s, (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb),     \
                        drop_bin, ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows,     \
                        (uint8_t*)dst,                                                          \
-                       redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, sel, ws.scan_err, \
+                       redirect_bin, (uint8_t*)redirect_dst, kXcdPackChunk, sel, ws.scan_err, \
                        side ? side->src : nullptr, side ? side->dst : nullptr,         \
                        side ? side->red : nullptr)
     // selection packs (2 bins, one dropped: the halo's rows to send) skip
     // the loads of dropped rows; elsewhere loads go out before the bins are known
-    const int sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
+    const int sel = nb <= 2 && drop_bin >= 0;
     if (side) side->used = side->src != nullptr;
     if (rpw == 2) MGR_PCK(2); else MGR_PCK(1);
 #undef MGR_PCK
@@ -960,11 +823,10 @@ static hipError_t pack_many_u(const void* src, int64_t n, const void* dest, int 
                            (const uint8_t*)src, n, (const DestT*)dest, nb, nbits_for(nb),      \
                            drop_bin, ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows, \
                            (uint8_t*)dst,                                                      \
-                           redirect_bin, (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err); \
+                           redirect_bin, (uint8_t*)redirect_dst, kXcdPackChunk, ws.scan_err); \
     }
     if (round_rows == 4096) MGR_PMK(4)
     else if (round_rows == 2048) MGR_PMK(2)
-    else if (round_rows == 1024) MGR_PMK(1)
     else return hipErrorNotSupported;
 #undef MGR_PMK
     return hipGetLastError();
@@ -999,23 +861,22 @@ template <int RB>
 static hipError_t pack_img_t(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                              int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
                              void* redirect_dst, hipStream_t s, SideField* side) {
-    // img_rpw 64-row rounds per wave when they divide the tile: 2 (A/B, 36-B
-    // records: 0.90-0.92 vs 1.02-1.05 ms per 64M, 4: 1.17 -- a wave's fixed
-    // per-round chain of load, count exchange, LDS permutation and store then
-    // moves twice the rows)
-    int rpw = g_tune.img_rpw;
-    while (rpw > 1 && tile_rows % (64 * rpw)) rpw >>= 1;
+    // two 64-row rounds per wave (A/B, 36-B records: 0.90-0.92 vs 1.02-1.05
+    // ms per 64M with one, 4: 1.17 -- a wave's fixed per-round chain of load,
+    // count exchange, LDS permutation and store then moves twice the rows);
+    // tiles that are not a multiple of two rounds go to the coop pack
+    constexpr int rpw = kImgRoundsPerWave;
+    if (tile_rows % (64 * rpw)) return hipErrorNotSupported;
     const int nw = tile_rows / (64 * rpw);
     const int lds = nw * 64 * 4 + nw * (64 * rpw * RB + 64 * 8 + 64 * rpw);
-    const bool sel = g_tune.pack_sel && nb <= 2 && drop_bin >= 0;
-    auto k = sel ? (rpw == 2 ? pack_img_kernel<RB, 2, true> : pack_img_kernel<RB, 1, true>)
-                 : (rpw == 2 ? pack_img_kernel<RB, 2, false> : pack_img_kernel<RB, 1, false>);
+    const bool sel = nb <= 2 && drop_bin >= 0;
+    auto k = sel ? pack_img_kernel<RB, rpw, true> : pack_img_kernel<RB, rpw, false>;
     ensure_lds(k, lds);
     hipLaunchKernelGGL(k, dim3((unsigned)ws.tn), dim3(64 * nw), (size_t)lds, s,
                        (const uint8_t*)src, n, (const uint8_t*)dest, nb, nbits_for(nb), drop_bin,
                        ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows, (uint8_t*)dst,
                        redirect_bin,
-                       (uint8_t*)redirect_dst, g_tune.xcd_pack, ws.scan_err,
+                       (uint8_t*)redirect_dst, kXcdPackChunk, ws.scan_err,
                        side ? side->src : nullptr, side ? side->dst : nullptr,
                        side ? side->red : nullptr);
     if (side) side->used = side->src != nullptr;
@@ -1049,7 +910,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
     const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
     const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err, int walk) {
+    const uint32_t* __restrict__ scan_err) {
     static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
     constexpr int NW = kFineWaves, RPW = TR / 64 / NW;
     constexpr int NDW = RB / 4;
@@ -1057,18 +918,18 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     uint32_t* img = (uint32_t*)smem;
     uint8_t* p = smem + align16(TR * RB);
     uint16_t* ibin = (uint16_t*)p;                 p += align16(TR * 2);
-    unsigned long long* gaddr = (unsigned long long*)p;  p += nb * 8;
-    uint16_t* lstart = (uint16_t*)p;
+    unsigned long long* gaddr = (unsigned long long*)p;
     if (scan_failed(scan_err)) return;
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    // tile walk: walk 0 -- XCD x owns tiles [x*per, (x+1)*per), its gx
-    // workgroups on gx adjacent tiles at a time; walk 1 -- all 8 gx
-    // workgroups on 8 gx adjacent tiles at a time (one region of the input)
+    // tile walk: XCD x owns tiles [x*per, (x+1)*per), its gx workgroups on
+    // gx adjacent tiles at a time, so the lines that adjacent tiles' runs
+    // share meet in one L2 (A/B: all 8 XCDs on one region of the input at a
+    // time measured no better)
     const int64_t per = (T + 7) >> 3;
     const int gx = (int)(gridDim.x >> 3), kx = (int)(blockIdx.x >> 3), xx = (int)(blockIdx.x & 7);
-    const int64_t first = walk ? (int64_t)xx * gx + kx : (int64_t)xx * per + kx;
-    const int64_t stride = walk ? 8 * (int64_t)gx : gx;
-    const int64_t last = walk ? T : min(T, (int64_t)xx * per + per);
+    const int64_t first = (int64_t)xx * per + kx;
+    const int64_t stride = gx;
+    const int64_t last = min(T, (int64_t)xx * per + per);
     const int mb = min(tid, nb - 1);
     struct Set {
         uint32_t v[RPW][NDW];
@@ -1089,12 +950,14 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
             load_row_dw<NDW>(src + row * RB, S.v[q]);
         }
     };
+    // (A/B, round 4: a branch-free scatter, which let the compiler keep the
+    // next tile's loads in flight through the store phase instead of
+    // draining them in the store loop's preheader, measured SLOWER: 1.14 vs
+    // 1.10 ms, with or without a fully unrolled store loop -- the load and
+    // store phases are not latency-serialised, profiles/round4/ab_notes.md.)
     auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
         const int tr = (int)min((int64_t)TR, n - t * TR);
-        if (tid < nb) {
-            lstart[tid] = (uint16_t)S.ls;
-            gaddr[tid] = (unsigned long long)(dst + (S.seg - (long long)S.ls) * (long long)RB);
-        }
+        if (tid < nb) gaddr[tid] = (unsigned long long)(dst + (S.seg - (long long)S.ls) * (long long)RB);
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
@@ -1108,7 +971,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
         __syncthreads();
         const int nbytes = tr * RB;
         // (the image pack's two-address unit store, store_img_unit, measured
-        // 12 % slower here; an unrolled store loop, no gain)
+        // 12 % slower here)
         for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
             const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
             const int bf = ibin[x / RB];
@@ -1122,7 +985,7 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
                 }
             }
         }
-        __syncthreads();   // the image, ibin, lstart and gaddr are reused by the next tile
+        __syncthreads();   // the image, ibin and gaddr are reused by the next tile
     };
     Set A, B;
     int64_t t = first;
@@ -1140,18 +1003,18 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
-// LDS of the ranked pack: the tile image, its row bins, per-bin output
-// addresses and tile starts.
+// LDS of the ranked pack: the tile image, its row bins and per-bin output
+// addresses.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
-    return align16(tile_rows * (int)row_bytes) + align16(tile_rows * 2) + nbins * 8 + nbins * 2;
+    return align16(tile_rows * (int)row_bytes) + align16(tile_rows * 2) + nbins * 8;
 }
 // Ranked tiles: 4096 rows when their image fits the LDS (36-byte rows: 157 KiB),
 // else 2048.  Longer tiles halve the [bins][tiles] histogram the scan walks and
 // the per-tile fixed work (A/B: profiles/round2/ab_notes.md).
 int ranked_tile_rows(int64_t row_bytes, int nbins) {
     if (row_bytes < 1 || row_bytes % 4 || row_bytes > 64 || nbins < 1 || nbins > 1024) return 0;
-    if (g_tune.rank_rows == 0 && ranked_lds_bytes(4096, row_bytes, nbins) <= 160 * 1024) return 4096;
-    if (g_tune.rank_rows == 4096 && ranked_lds_bytes(4096, row_bytes, nbins) <= 160 * 1024) return 4096;
+    const int want = hooks().rank_rows;
+    if (want != 2048 && ranked_lds_bytes(4096, row_bytes, nbins) <= 160 * 1024) return 4096;
     return ranked_lds_bytes(kFineTR, row_bytes, nbins) <= 160 * 1024 ? kFineTR : 0;
 }
 
@@ -1175,8 +1038,7 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
         ensure_lds(k, lds);                                                                   \
         hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(1024), (size_t)lds, s,               \
                            (const uint8_t*)src, n, ids, ranks, tile_starts, nbins,            \
-                           ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err,                      \
-                           g_tune.ranked_walk);                                               \
+                           ws.offsets, ws.T, (uint8_t*)dst, ws.scan_err);                     \
         e = hipGetLastError();                                                                \
     }
 #define MGR_PR(RB_)                                                                           \
@@ -1213,8 +1075,8 @@ static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const 
     // pack_img 1: rows of >= 24 bytes (A/B: 36 B 0.90 vs 1.05 ms, 40 B 0.97 vs
     // 1.00, 24 B 0.70 vs 0.71; 12 B 0.56 vs 0.48 -- the LDS passes cost more
     // than narrow units for small rows); 2: every size it takes (tests)
-    const int64_t min_rb = g_tune.pack_img >= 2 ? 12 : 24;
-    if (!g_tune.pack_img || ((uintptr_t)src & 15) || (a & 3) || row_bytes % 16 == 0 ||
+    const int64_t min_rb = hooks().pack_img_all ? 12 : 24;
+    if (((uintptr_t)src & 15) || (a & 3) || row_bytes % 16 == 0 ||
         row_bytes < min_rb || row_bytes > 60 || nb > 64 || tile_rows > 1024 ||
         dest_bytes(nb) != 1)
         return hipErrorNotSupported;
@@ -1233,8 +1095,7 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
                          int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side) {
     if constexpr (W >= 4) {
-        if (g_tune.pack_many && nb > 64 && nb <= 1024 && row_bytes <= 64 &&
-            tile_rows == many_tile_rows(nb)) {
+        if (nb > 64 && nb <= 1024 && row_bytes <= 64 && tile_rows == many_round_rows(nb)) {
             const hipError_t e = dest_bytes(nb) == 1
                 ? pack_many_t<W, uint8_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s)
                 : pack_many_t<W, uint16_t>(src, row_bytes, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s);
@@ -1291,16 +1152,8 @@ static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n
     // profiler: narrow (< 4-byte) rows apart
     const int kid = row_bytes < 4 ? K_PACK_NARROW : K_PACK;
     prof_begin(s, kid);
-    hipError_t e = hipErrorNotSupported;
-    if (g_tune.pack_compact && nbins == 2 && drop_bin == 1 && redirect_bin < 0) {
-        if ((a & 15) == 0) e = compact_t<16>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
-        else if ((a & 7) == 0) e = compact_t<8>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
-        else if ((a & 3) == 0) e = compact_t<4>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
-        else e = compact_t<1>(src, row_bytes, n, dest, tile_rows, ws, dst, s);
-    }
-    if (e == hipErrorNotSupported)
-        e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin,
-                     redirect_dst, s, side);
+    hipError_t e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
+                            redirect_bin, redirect_dst, s, side);
     if (e != hipErrorNotSupported) {
         prof_end(s, kid);
         return e;

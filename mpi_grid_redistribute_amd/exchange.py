@@ -43,6 +43,33 @@ def check_counts(send_counts, recv_counts):
                        f"send counts {list(send_counts)}, receive counts {list(recv_counts)}")
 
 
+def count_skew(matrix):
+    """Load imbalance of a redistribution from its count matrix ``C[s][d]`` =
+    rows source ``s`` sends destination ``d`` (the counts redist.py:199's
+    alltoall moves; SURVEY §8d config 4: skewed Alltoallv counts).
+    ``recv_max_over_mean`` = the most rows any destination receives over the
+    mean per destination (1.0 = balanced; the slowest rank's exchange and
+    unpack scale with it); ``entry_max_over_mean`` = the largest single
+    message over the mean message.  A 1 x D matrix is one GPU's partition into
+    D virtual destinations."""
+    c = np.asarray(matrix, dtype=np.int64)
+    if c.ndim == 1:
+        c = c.reshape(1, -1)
+    if c.ndim != 2 or c.size == 0:
+        raise ValueError("count matrix must be [sources][destinations]")
+    if (c < 0).any():
+        raise ValueError("negative counts (a failed scan)")
+    recv = c.sum(axis=0)
+    rmean = float(recv.mean())
+    emean = float(c.mean())
+    return {"sources": int(c.shape[0]), "destinations": int(c.shape[1]),
+            "total_rows": int(c.sum()), "recv_max": int(recv.max()), "recv_min": int(recv.min()),
+            "recv_mean": rmean,
+            "recv_max_over_mean": float(recv.max()) / rmean if rmean > 0 else None,
+            "entry_max": int(c.max()),
+            "entry_max_over_mean": float(c.max()) / emean if emean > 0 else None}
+
+
 def plan_layout(send_counts, recv_counts, rank, redirect_self):
     """Send/receive offsets in rows.  Receives in source-rank order (S7).
     With ``redirect_self`` the self segment never enters the send buffer
@@ -105,6 +132,20 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
     return outs, lay
 
 
+_COMM_STREAMS = {}
+
+
+def _comm_stream(device):
+    """The side stream the pipelined exchange posts its row messages on: one
+    per device for the process (not one per call)."""
+    d = torch.device(device)
+    idx = d.index if d.index is not None else torch.cuda.current_device()
+    st = _COMM_STREAMS.get(idx)
+    if st is None:
+        st = _COMM_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
 def exchange_pipelined(transport, row_bytes, bin_counts, rank, device, chunk_offsets, pack_chunk,
                        nchunks, extra_rows=None, scratch=None):
     """exchange() with the pack and the row transfers overlapped: the tiles are
@@ -114,41 +155,43 @@ def exchange_pipelined(transport, row_bytes, bin_counts, rank, device, chunk_off
     message -- while chunk c + 1 is being packed (the messages run on a
     stream of their own, ordered after chunk c's pack by an event).
 
-    ``chunk_offsets()`` -> host int64 [nchunks + 1][size]: the first row of
-    every bin at each chunk boundary in the packed (bin-major) layout, i.e.
-    the scan's offsets at the boundary tiles (mgr_tile_offsets).
+    ``chunk_offsets()`` -> int64 [nchunks + 1][size] (device tensor, or host
+    array in the CPU tests): the first row of every bin at each chunk boundary
+    in the packed (bin-major) layout, i.e. the scan's offsets at the boundary
+    tiles (mgr_tile_offsets), read without a host sync.
     ``pack_chunk(c, sends, outs, redirect_bin, out_offsets)`` packs chunk c of
     every field (the self rows straight into the output, as exchange()'s
-    pack).  The per-chunk counts travel to the peers first (k int64 each way
-    per peer), so every receive is posted with its exact size.  Output bytes
-    and order are exactly exchange()'s (receives in source-rank order, S7)."""
-    sc, rc = transport.exchange_counts(bin_counts)
-    size = len(sc)
-    for p in range(size):
-        transport.note("send", p, 8)
-        transport.note("recv", p, 8)
-    check_counts(sc, rc)
+    pack).  One count message per peer carries [total, chunk 0, ..., chunk
+    k-1] (k + 1 int64 each way, one group, ONE host sync per call), so every
+    receive is posted with its exact size.  A rank whose chunk counts do not
+    add up to its totals (or whose scan failed) sends -1 totals: every rank
+    then raises at the same point, before any row message is posted.  Output
+    bytes and order are exactly exchange()'s (receives in source-rank order,
+    S7)."""
+    size = transport.size
+    k = int(nchunks)
+    counts = torch.as_tensor(bin_counts).to(torch.int64).reshape(-1)
+    dev = counts.device
+    off = torch.as_tensor(chunk_offsets()).to(device=dev, dtype=torch.int64).reshape(k + 1, size)
+    cs_d = off[1:] - off[:-1]                                  # [chunk][peer] rows sent
+    ok = (cs_d.sum(dim=0) == counts).all()
+    msg = torch.empty((size, k + 1), dtype=torch.int64, device=dev)
+    msg[:, 0] = torch.where(ok, counts, torch.full_like(counts, -1))
+    msg[:, 1:] = cs_d.t()
+    sh, rh = transport.exchange_count_rows(msg)
+    for p in range(size):   # [total, k chunk counts] each way per peer
+        transport.note("send", p, 8 * (k + 1))
+        transport.note("recv", p, 8 * (k + 1))
+    sc, rc = sh[:, 0].copy(), rh[:, 0].copy()
+    check_counts(sc, rc)       # a -1 from any rank (failed scan, bad chunks): all raise
+    cs = np.ascontiguousarray(sh[:, 1:].T)                     # [chunk][peer] rows sent
+    cr = np.ascontiguousarray(rh[:, 1:])                       # [peer][chunk] rows received
+    cr[rank] = cs[:, rank]
+    if not np.array_equal(cr.sum(axis=1), rc):   # a peer's message is self-consistent
+        raise MgrError(f"peers' chunk counts {cr.sum(axis=1)} do not add up to {rc}")
     # the self rows always go straight into the output (the pack's redirect),
     # whatever the transport: only the other peers' pieces travel
     lay = plan_layout(sc, rc, rank, True)
-    off = np.asarray(chunk_offsets(), dtype=np.int64).reshape(nchunks + 1, size)
-    cs = np.diff(off, axis=0)                                  # [chunk][peer] rows sent
-    if not np.array_equal(cs.sum(axis=0), sc):
-        raise MgrError(f"chunk offsets do not add up to the send counts: {cs.sum(axis=0)} vs {sc}")
-    # every peer's chunk counts for this rank (k int64 each way per peer)
-    send_c = torch.from_numpy(np.ascontiguousarray(cs.T)).to(device)      # [peer][chunk]
-    recv_c = torch.zeros_like(send_c)
-    ops = []
-    for j in range(1, size):   # ring order, as the row exchange
-        to, frm = (rank + j) % size, (rank - j) % size
-        ops.append(("send", to, send_c[to].view(torch.uint8)))
-        ops.append(("recv", frm, recv_c[frm].view(torch.uint8)))
-    transport.note_p2p(ops)
-    transport.p2p(ops)
-    cr = recv_c.cpu().numpy()                                  # [peer][chunk] rows received
-    cr[rank] = cs[:, rank]
-    if not np.array_equal(cr.sum(axis=1), rc):
-        raise MgrError(f"peers' chunk counts {cr.sum(axis=1)} do not add up to {rc}")
     extra = int(extra_rows(lay.total_recv)) if extra_rows is not None else 0
     outs, sends = [], []
     for f, rb in enumerate(row_bytes):
@@ -161,7 +204,7 @@ def exchange_pipelined(transport, row_bytes, bin_counts, rank, device, chunk_off
     offs = [int(lay.recv_offsets[rank]) * rb for rb in row_bytes]
     gpu = isinstance(device, torch.device) and device.type == "cuda" or str(device).startswith("cuda")
     compute = torch.cuda.current_stream() if gpu else None
-    comm = torch.cuda.Stream(device=device) if gpu else None
+    comm = _comm_stream(device) if gpu else None
     sent_c = np.zeros(size, dtype=np.int64)     # rows of each peer's segment already sent
     recv_at = np.zeros(size, dtype=np.int64)    # rows of each source already received
     for c in range(nchunks):

@@ -43,9 +43,17 @@ from .exchange import check_counts, exchange, exchange_pipelined
 from .halo import DeviceSelect, exchange_overload, halo_capacity, thresholds
 
 
+_WRITE_BACK = {"changed": _lib.MGR_WRITE_BACK_CHANGED, "all": _lib.MGR_WRITE_BACK_ALL}
+
+
 class _Plan:
     """Owns one native mgr_plan (geometry + number of destinations), or with
     ``fine`` a fine-cell plan (mgr_plan_create_fine, prod(fine) bins)."""
+
+    def set_write_back(self, mode):
+        if mode not in _WRITE_BACK:
+            raise ValueError(f"write_back must be one of {sorted(_WRITE_BACK)} (got {mode!r})")
+        _lib.call("mgr_plan_set_write_back", self.h, _WRITE_BACK[mode])
 
     def __init__(self, grid_topology: np.ndarray, box_length: np.ndarray, nbins: int,
                  fine=None):
@@ -247,6 +255,17 @@ def _scratch(n, nbins, max_row_bytes, dev, cache=None, dest=True, tag="", tile_r
     return tile_rows, ws, d
 
 
+def exchange_chunks_for(size, row_bytes):
+    """Product default of the pipelined exchange's chunk count: 4 chunks on
+    more than one rank (each chunk's rows travel while the next packs), 1 on
+    one rank (nothing travels).  Rank-independent by construction (world
+    size and the fields' row bytes are the same on every rank), as the
+    protocol requires: the per-chunk counts are part of the count message.
+    A size threshold is deliberately absent: the count of chunks cannot depend
+    on this rank's row count (an empty rank must agree with a full one)."""
+    return 4 if int(size) > 1 and int(row_bytes) > 0 else 1
+
+
 class MPIGridRedistributor:
     """Redistributes data by position onto a Cartesian grid of ranks
     (redist.py:15-61).  ``comm``: an ``RcclComm`` (one process per GPU), a
@@ -284,8 +303,17 @@ class MPIGridRedistributor:
         self._dev = device()
         self._scratch = Scratch(self._dev)
         # > 1: the pack and the row exchange overlap in this many chunks of
-        # tiles (exchange_pipelined); 1: pack everything, then one exchange
-        self.exchange_chunks = 1
+        # tiles (exchange_pipelined); 1: pack everything, then one exchange;
+        # None: the product default (exchange_chunks_for: 4 on > 1 rank)
+        self.exchange_chunks = None
+
+    def set_write_back(self, mode):
+        """How the periodic wrap writes ``position`` back (redist.py:68 mutates
+        it in place): "changed" (default) stores a 64-row slab only if one of
+        its coordinates changed, "all" stores every slab -- the same bytes in
+        memory either way; "all" is the cost of fresh input (bench.py).  Per
+        redistributor (mgr_plan_set_write_back), not process-wide."""
+        self._plan.set_write_back(mode)
 
     # ------------------------------------------------------ binning (L1)
     def get_cell_indexes_from_position(self, position, periodic=True):
@@ -626,8 +654,10 @@ class MPIGridRedistributor:
         T = (n + tile_rows - 1) // tile_rows
         # the chunk count is part of the exchange protocol: the same on every
         # rank whatever its row count (a rank with fewer tiles than chunks --
-        # an empty one included -- packs empty chunks)
-        k = max(1, int(self.exchange_chunks))
+        # an empty one included -- packs empty chunks); the size rule reads
+        # only rank-independent inputs
+        k = (exchange_chunks_for(P, sum(hint)) if self.exchange_chunks is None
+             else max(1, int(self.exchange_chunks)))
         if k > 1 and P > 1:
             # pipelined: pack the tiles in k chunks, each chunk's pieces travel
             # while the next is packed (exchange_pipelined)
@@ -638,7 +668,7 @@ class MPIGridRedistributor:
                 arr = (ctypes.c_int64 * (k + 1))(*bounds)
                 _lib.call("mgr_tile_offsets", _lib.ptr(ws), n, nb, tile_rows, arr, k + 1,
                           _lib.ptr(out), stream)
-                return out.view(k + 1, nb)[:, :P].cpu().numpy()
+                return out.view(k + 1, nb)[:, :P]   # device: read with the count message
 
             def pack_chunk(c, sends, outs, redirect_bin, offs):
                 t0, t1 = bounds[c], bounds[c + 1]
@@ -661,6 +691,7 @@ class MPIGridRedistributor:
                                            bin_counts[:P], self.rank, self._dev, chunk_offsets,
                                            pack_chunk, k, extra_rows=extra_rows,
                                            scratch=self._scratch.get)
+            self._last_layout = lay
             return outs, lay.total_recv
         known = None
         if deferred is not None and P == 1 and not drop:
@@ -669,7 +700,18 @@ class MPIGridRedistributor:
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
                              self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
                              pack_all=pack_all if side_ids else None, known_rows=known)
+        self._last_layout = lay
         return outs, lay.total_recv
+
+    @property
+    def last_counts(self):
+        """(send_counts, recv_counts) of the last redistribution on this rank:
+        host int64 arrays of rows sent to / received from every rank (this
+        rank's row and column of the count matrix, redist.py:199's alltoall;
+        ``exchange.count_skew`` turns the gathered matrix into the load
+        imbalance).  None before the first call."""
+        lay = getattr(self, "_last_layout", None)
+        return None if lay is None else (lay.send_counts.copy(), lay.recv_counts.copy())
 
     @property
     def last_traffic(self):
@@ -725,6 +767,10 @@ class GridPartitioner:
         self._cache = {}
         self._fine_plans = {}
         self._fine_buf = None
+
+    def set_write_back(self, mode):
+        """"changed" (default) / "all": MPIGridRedistributor.set_write_back."""
+        self._plan.set_write_back(mode)
 
     def buffers(self, n, row_bytes):
         key = (int(n), int(row_bytes))

@@ -304,13 +304,13 @@ def case_cell_number(mgr, comm):
 
 
 def case_scan_failure(mgr, comm):
-    """Every rank's scan gives up at once (knob scan_spins = -1): all ranks
+    """Every rank's scan gives up at once (test hook scan_spins = -1): all ranks
     raise together at the count exchange, nobody hangs in the row exchange."""
     from mpi_grid_redistribute_amd import _lib
     topo = TOPO[WORLD]
     pos, data = rank_inputs(7, [200_000] * WORLD)
     R = mgr.MPIGridRedistributor(comm, topo, BOX)
-    _lib.tune("scan_spins", -1)
+    _lib.test_hook("scan_spins", -1)
     try:
         R.redistribute_by_position(data[RANK], pos[RANK])
     except _lib.MgrError as e:
@@ -318,9 +318,60 @@ def case_scan_failure(mgr, comm):
     else:
         raise AssertionError("a failed scan did not raise")
     finally:
-        _lib.tune("scan_spins", 1 << 24)
+        _lib.test_hook("scan_spins", 1 << 24)
     # the communicator still works afterwards
     assert case_random(mgr, comm, [1000] * WORLD, 8, False) >= 0
+
+
+def case_full_size(mgr, comm, kind, n):
+    """BASELINE configs 3 / 4 at their full per-GPU size (125M rows per rank,
+    32-byte records [x, y, z, id], uniform or clustered), the product path
+    (redistribute_by_position over RCCL) checked by properties, every rank's
+    input regenerated from its seed (the ids encode source rank and row):
+      * sources in rank order (S7), each source's run in increasing id order
+        (stable);
+      * per-source row counts == the C oracle's bincount of that source's
+        wrapped positions, and every received row's oracle cell is this rank;
+      * every received row's 32 bytes == the source record with that id;
+      * this rank's positions wrapped in place exactly as the C oracle wraps."""
+    from oracle import c_oracle
+    topo = TOPO[WORLD]
+    seed = 20261015
+
+    def gen(r):
+        if kind == "uniform":
+            return mgr.synth_uniform(n, seed=seed, gid0=r * n)
+        return mgr.synth_clustered(n, seed=seed, gid0=r * n)
+
+    pos, rec = gen(RANK)
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    out = R.redistribute_by_position(rec, pos)
+    torch.cuda.synchronize()
+    wrapped = pos.cpu().numpy()
+    del pos, rec
+    ids = out.view(torch.int64)[:, 3]
+    src = torch.div(ids, n, rounding_mode="floor")
+    assert bool((src[1:] >= src[:-1]).all()), "sources not in rank order (S7)"
+    total = 0
+    for s in range(WORLD):
+        ps, rs = gen(s)
+        ph = ps.cpu().numpy()
+        del ps
+        cells = c_oracle.bin_positions(ph, topo, BOX)        # wraps ph in place
+        if s == RANK:
+            assert np.array_equal(wrapped.view(np.uint64), ph.view(np.uint64)), "wrapped positions"
+        sel = src == s
+        run = ids[sel] - s * n
+        cnt = int(np.count_nonzero(cells == RANK))
+        assert run.numel() == cnt, f"source {s}: {run.numel()} rows, oracle {cnt}"
+        assert bool((run[1:] > run[:-1]).all()), f"source {s}: order not stable"
+        run_h = run.cpu().numpy()
+        assert bool((cells[run_h] == RANK).all()), f"source {s}: rows of another cell"
+        assert torch.equal(out[sel], rs[run]), f"source {s}: row bytes"
+        total += cnt
+        del rs, run, sel, cells, ph
+    assert total == out.shape[0]
+    return total
 
 
 def main():
@@ -334,6 +385,17 @@ def main():
     log("creating RcclComm")
     comm = mgr.RcclComm.from_torch_distributed()
     log(f"RcclComm up (device {dev}, shared={SHARED})")
+    cases = []
+    if os.environ.get("MGR_TEST_SET") == "fullsize":
+        n = int(os.environ.get("MGR_FULL_N", 125_000_000))
+        cases = [("cfg3_uniform_full", lambda: case_full_size(mgr, comm, "uniform", n)),
+                 ("cfg4_clustered_full", lambda: case_full_size(mgr, comm, "clustered", n))]
+    else:
+        cases = _parity_cases(mgr, comm)
+    return _run_cases(cases, comm, out_path, results)
+
+
+def _parity_cases(mgr, comm):
     cases = []
     for name in G.redist_cases():
         if int(G.load(name)["size"]) == WORLD:
@@ -381,6 +443,10 @@ def main():
              lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], True, 24)),
         ]
     cases.append(("cell_number_dropped_ids", lambda: case_cell_number(mgr, comm)))
+    return cases
+
+
+def _run_cases(cases, comm, out_path, results):
     for name, fn in cases:
         t0 = time.perf_counter()
         # a rank that fails before a collective leaves its peers waiting in

@@ -8,10 +8,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mgr.h")
+INSTRUMENT = os.path.join(ROOT, "include", "mgr_instrument.h")
 
 
-def header_functions():
-    text = open(HEADER).read()
+def header_functions(path=HEADER):
+    text = open(path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(mgr_[a-z0-9_]+)\s*\(", text)))
 
@@ -34,6 +35,36 @@ def test_every_declared_symbol_exported(lib):
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
     assert set(_lib.SIGNATURES) == set(header_functions())
+    # the instrumentation header: exported, bound, and not in the boundary
+    inst = header_functions(INSTRUMENT)
+    for name in inst:
+        assert hasattr(lib, name), name
+    assert set(_lib.INSTRUMENT_SIGNATURES) == set(inst)
+    assert not set(inst) & set(header_functions())
+
+
+def test_test_hooks_validate(lib):
+    from mpi_grid_redistribute_amd import _lib
+    with pytest.raises(_lib.MgrError):
+        _lib.test_hook("no_such_hook", 1)
+    with pytest.raises(_lib.MgrError):
+        _lib.test_hook("rank_rows", 1000)              # only 0 / 2048 / 4096
+    for k, v in _lib.HOOK_DEFAULTS.items():            # every hook takes its default
+        _lib.test_hook(k, v)
+    assert not hasattr(lib, "mgr_tune")                # no process-wide product knobs
+
+
+def test_plan_write_back_option(lib):
+    import numpy as np
+    topo = np.array([2, 2, 2], dtype=np.int64)
+    box = np.array([1.0, 1.0, 1.0])
+    h = ctypes.c_void_p()
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    assert lib.mgr_plan_create(3, vp(topo), vp(box), 2, 8, ctypes.byref(h)) == 0
+    assert lib.mgr_plan_set_write_back(h, 1) == 0 and lib.mgr_plan_set_write_back(h, 0) == 0
+    assert lib.mgr_plan_set_write_back(h, 2) < 0
+    assert lib.mgr_plan_set_write_back(None, 1) < 0
+    assert lib.mgr_plan_destroy(h) == 0
 
 
 def test_library_is_gfx950():

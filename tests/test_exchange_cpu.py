@@ -349,3 +349,60 @@ def test_rccl_schedule_order_and_self_copy():
     assert ops[-1] == (C, 0, 0, 0, 0, 16)
     with pytest.raises(_lib.MgrError):
         _lib.exchange_schedule(0, 2, [8], [-1, 3], [0, 0], [0, 1], [0, 0])
+
+
+def _gloo_pipelined_bad_worker(rank, size, port, bad_rank):
+    """One rank's chunk offsets do not add up to its counts: it sends -1
+    totals in the one count message, so EVERY rank raises there (none is left
+    waiting inside a row message)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        from mpi_grid_redistribute_amd._lib import MgrError
+        from mpi_grid_redistribute_amd.exchange import exchange_pipelined
+        topo = [size, 1, 1]
+        pos, data = make_rank_inputs(size, seed=77)
+        rb = data[0].dtype.itemsize
+        dest = ro.cell_number_from_position(ro.Geometry(topo, BOX, size, rank), pos[rank].copy())
+        offs_fn, pack_chunk, counts = chunked_oracle_pack(data[rank], dest, size, rb, 3)
+        if rank == bad_rank:
+            good = offs_fn()
+            bad = good.copy()
+            bad[1, 0] += 1                     # chunk 0 / chunk 1 boundary off by one row
+            bad[3, 1] -= 1                     # and the totals no longer add up
+            offs_fn = lambda: bad  # noqa: E731
+        comm = TorchDistComm()
+        with pytest.raises(MgrError):
+            exchange_pipelined(comm, [rb], counts, rank, "cpu", offs_fn, pack_chunk, 3)
+        comm.barrier()                          # every rank got here: nobody hangs
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,bad_rank", [(2, 1), (3, 0)])
+def test_gloo_pipelined_failure_agreed(size, bad_rank):
+    mp.spawn(_gloo_pipelined_bad_worker, args=(size, _free_port(), bad_rank), nprocs=size,
+             join=True)
+
+
+def test_count_skew_hand_built():
+    """the count matrix's max/mean (exchange.count_skew)
+    on a hand-built skewed layout: 4 sources x 4 destinations, destination 2
+    receives most rows."""
+    from mpi_grid_redistribute_amd.exchange import count_skew
+    c = np.array([[10, 0, 90, 0],
+                  [5, 5, 80, 10],
+                  [0, 0, 100, 0],
+                  [25, 15, 50, 10]])
+    s = count_skew(c)
+    recv = c.sum(axis=0)                          # 40, 20, 320, 20 -> mean 100
+    assert s["recv_max"] == 320 and s["recv_min"] == 20
+    assert s["recv_mean"] == 100.0 and s["recv_max_over_mean"] == 3.2
+    assert s["entry_max"] == 100 and s["entry_max_over_mean"] == 100 / c.mean()
+    assert s["sources"] == 4 and s["destinations"] == 4 and s["total_rows"] == recv.sum()
+    # one GPU: a 1 x D row of virtual destinations; balanced -> 1.0
+    assert count_skew([7, 7, 7, 7])["recv_max_over_mean"] == 1.0
+    assert count_skew(np.zeros((2, 3), dtype=np.int64))["recv_max_over_mean"] is None
+    with pytest.raises(ValueError):
+        count_skew([[1, -1]])                     # a failed scan's -1 counts

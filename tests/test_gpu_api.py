@@ -102,13 +102,13 @@ def test_stack_unstack_position(dim):
 
 
 def test_scan_failure_is_loud():
-    """A look-back that gives up (knob scan_spins = -1) must not yield wrong
+    """A look-back that gives up (test hook scan_spins = -1) must not yield wrong
     offsets: the counts come back -1, the pack writes nothing, and the API
     raises at its count read."""
     n = 1 << 20
     pos, rec = mgr.synth_uniform(n, seed=5)
     P = GridPartitioner([2, 2, 2], [1.0] * 3)
-    _lib.tune("scan_spins", -1)
+    _lib.test_hook("scan_spins", -1)
     try:
         out, counts = P.partition_device(rec.reshape(-1), 32, pos)
         out.fill_(0xAB)
@@ -119,7 +119,7 @@ def test_scan_failure_is_loud():
         with pytest.raises(_lib.MgrError, match="scan failed"):
             P.partition_by_position(rec.cpu().numpy(), pos.cpu().numpy())
     finally:
-        _lib.tune("scan_spins", 1 << 24)
+        _lib.test_hook("scan_spins", 1 << 24)
     out, counts = P.partition_device(rec.reshape(-1), 32, pos)
     assert (counts.cpu().numpy() > 0).all()
 
@@ -127,13 +127,13 @@ def test_scan_failure_is_loud():
 def test_single_rank_scan_failure_raises():
     pos, rec = mgr.synth_uniform(1 << 20, seed=6)
     R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
-    _lib.tune("scan_spins", -1)
+    _lib.test_hook("scan_spins", -1)
     try:
         with pytest.raises(_lib.MgrError, match="scan failed"):
             R.redistribute_by_cell_number(rec, torch.zeros(1 << 20, dtype=torch.int64,
                                                            device="cuda"))
     finally:
-        _lib.tune("scan_spins", 1 << 24)
+        _lib.test_hook("scan_spins", 1 << 24)
 
 
 def test_halo_scan_failure_raises():
@@ -145,12 +145,12 @@ def test_halo_scan_failure_raises():
     pos = rng.random((n, 3))
     data = np.arange(n)
     R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
-    _lib.tune("scan_spins", -1)
+    _lib.test_hook("scan_spins", -1)
     try:
         with pytest.raises(_lib.MgrError, match="scan failed"):
             R.exchange_overload_by_position(data, pos, [0.1, 0.1, 0.1])
     finally:
-        _lib.tune("scan_spins", 1 << 24)
+        _lib.test_hook("scan_spins", 1 << 24)
     out = R.exchange_overload_by_position(data, pos, [0.1, 0.1, 0.1])
     assert len(out) > 0
 
@@ -166,12 +166,12 @@ def test_one_rank_halo_deferred_count_check_raises(ol):
     data = np.arange(n)
     R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
     ol = [ol] * 3
-    _lib.tune("scan_spins", -1)
+    _lib.test_hook("scan_spins", -1)
     try:
         with pytest.raises(_lib.MgrError, match="scan failed"):
             R.redistribute_by_position(data, pos.copy(), overload_lengths=ol)
     finally:
-        _lib.tune("scan_spins", 1 << 24)
+        _lib.test_hook("scan_spins", 1 << 24)
     out = R.redistribute_by_position(data, pos.copy(), overload_lengths=ol)
     assert len(out) > n
 

@@ -195,41 +195,12 @@ def test_ranked_sort_tile_sizes(rank_rows, row_bytes):
     exp = data[np.argsort(ids, kind="stable")]
     R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
     pos = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
-    _lib.tune("rank_rows", rank_rows)
+    _lib.test_hook("rank_rows", rank_rows)
     try:
         got, off = R.fine_cell_sort(torch.from_numpy(data).cuda(), pos, [8, 8, 8],
                                     fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
     finally:
-        _lib.tune("rank_rows", 0)
-    assert np.array_equal(got.cpu().numpy(), exp)
-    assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
-
-
-RANKED_DEFAULTS = {"ranked_walk": 0, "rank_orm": 1}
-
-
-@pytest.mark.parametrize("knobs", [{"ranked_walk": 1}, {"rank_orm": 0},
-                                   {"ranked_walk": 1, "rank_orm": 0}])
-@pytest.mark.parametrize("row_bytes", [4, 12, 36])
-def test_ranked_pack_variants(knobs, row_bytes):
-    """Every ranked-pack / rank_ids variant (the all-XCD tile walk;
-    ballot-match ranking) gives the same stable sort."""
-    rng = np.random.default_rng(row_bytes + 7 * len(knobs))
-    n = 200_003
-    ids = rng.integers(0, 512, n).astype(np.uint16)
-    ids[rng.random(n) < 0.2] = 300
-    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
-    exp = data[np.argsort(ids, kind="stable")]
-    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
-    pos = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
-    for k, v in knobs.items():
-        _lib.tune(k, v)
-    try:
-        got, off = R.fine_cell_sort(torch.from_numpy(data).cuda(), pos, [8, 8, 8],
-                                    fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
-    finally:
-        for k in knobs:
-            _lib.tune(k, RANKED_DEFAULTS[k])
+        _lib.test_hook("rank_rows", 0)
     assert np.array_equal(got.cpu().numpy(), exp)
     assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
 

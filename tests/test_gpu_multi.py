@@ -37,6 +37,18 @@ def _free_port():
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_multi_rank(world, tmp_path):
+    _run_world(world, tmp_path, {})
+
+
+def test_rccl_full_size_cfg3_cfg4(tmp_path):
+    """BASELINE configs 3 and 4 at their full per-GPU size: 125M rows per rank
+    (uniform, then clustered), world 2, the product path over RCCL, checked by
+    properties against the C oracle (rccl_worker.case_full_size)."""
+    _run_world(2, tmp_path, {"MGR_TEST_SET": "fullsize", "MGR_CASE_TIMEOUT": "300"},
+               timeout=900)
+
+
+def _run_world(world, tmp_path, extra_env, timeout=TIMEOUT_S):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     shared = torch.cuda.device_count() < world
@@ -51,21 +63,23 @@ def test_rccl_multi_rank(world, tmp_path):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    MGR_TEST_OUT=str(tmp_path / f"rank{r}.json"),
                    MGR_TEST_SHARED_GPU="1" if shared else "0")
-        logs.append(open(os.path.join(logdir, f"multi_w{world}_rank{r}.log"), "w"))
+        env.update(extra_env)
+        tag = extra_env.get("MGR_TEST_SET", "")
+        logs.append(open(os.path.join(logdir, f"multi_w{world}{tag}_rank{r}.log"), "w"))
         procs.append(subprocess.Popen([sys.executable, "-u", "-m", "tests.rccl_worker"], cwd=ROOT,
                                       env=env, start_new_session=True, stdout=logs[-1],
                                       stderr=subprocess.STDOUT))
     codes = []
     try:
         for p in procs:
-            codes.append(p.wait(timeout=TIMEOUT_S))
+            codes.append(p.wait(timeout=timeout))
     except subprocess.TimeoutExpired:
         for p in procs:
             if p.poll() is None:
                 os.killpg(p.pid, signal.SIGKILL)
         for p in procs:
             p.wait()
-        pytest.fail(f"world {world}: ranks did not finish within {TIMEOUT_S} s")
+        pytest.fail(f"world {world}: ranks did not finish within {timeout} s")
     finally:
         for fh in logs:
             fh.close()

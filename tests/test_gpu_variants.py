@@ -1,9 +1,12 @@
-"""GPU parity of every kernel variant the tuning knobs select (mgr_tune).
+"""GPU parity of every path the test hooks force (include/mgr_instrument.h
+mgr_test_hook) and of the per-plan write-back option.
 
-The shipped defaults are covered by test_gpu_parity.py; here each non-default
-variant (XCD-contiguous tile order, unconditional position write-back, tile
-shapes, scan chunking, the generic pack) must give the same bytes on the same inputs: the C
-oracle on seeded inputs, and the reference's own golden fixtures.
+The shipped defaults are covered by test_gpu_parity.py; here each fallback
+the product reaches on other inputs (unstaged bin slabs, run-time geometry,
+the generic pack, the image pack's narrow rows), every tile shape and scan
+chunking, and the unconditional position write-back must give the same bytes
+on the same inputs: the C oracle on seeded inputs, and the reference's own
+golden fixtures.
 """
 import numpy as np
 import pytest
@@ -18,49 +21,24 @@ pytestmark = pytest.mark.gpu
 mgr = pytest.importorskip("mpi_grid_redistribute_amd")
 from mpi_grid_redistribute_amd import GridPartitioner, MPIGridRedistributor, _lib  # noqa: E402
 
-DEFAULTS = {"xcd_pack": 16, "xcd_bin": 0, "bin_skip_clean": 1, "bin_waves": 0, "pack_coop": 1,
-            "many_rows": 0, "bin_staged": 1, "tile_rounds": 0,
-            "pack_many": 1, "scan_chunk": 2048, "pack_img": 1, "many_super": 1,
-            "scan_max_chunks": 1024, "pack_sel": 1, "pack_compact": 1, "bin_geo": 1, "rank_rows": 0,
-            "img_rpw": 2, "ranked_walk": 0,
-            "rank_orm": 1}
 VARIANTS = [
-    {"img_rpw": 1},
-    {"img_rpw": 1, "tile_rounds": 1},
-    {"img_rpw": 2, "tile_rounds": 16, "pack_sel": 0},
-    {"bin_geo": 0},
-    {"bin_geo": 0, "bin_skip_clean": 0},
-    {"xcd_pack": 1, "xcd_bin": 1},
-    {"bin_skip_clean": 0},
-    {"tile_rounds": 8},
-    {"bin_waves": 16, "xcd_pack": 1},
-    {"bin_waves": 8, "bin_skip_clean": 0},
-    {"bin_waves": 2},
-    {"bin_skip_clean": 0, "bin_staged": 0},
-    {"bin_waves": 1, "xcd_bin": 1},
-    {"xcd_pack": 0},
-    {"pack_coop": 0},
-    {"pack_coop": 0, "xcd_pack": 0},
-    {"pack_many": 0},
-    {"xcd_pack": 4},
-    {"xcd_pack": 64, "tile_rounds": 1},
     {"tile_rounds": 1},
+    {"tile_rounds": 8},
+    {"tile_rounds": 16},
+    {"bin_generic": 1},
+    {"bin_generic": 1, "write_back": "all"},
+    {"write_back": "all"},
+    {"bin_unstaged": 1},
+    {"bin_unstaged": 1, "write_back": "all", "tile_rounds": 1},
+    {"pack_generic": 1},
+    {"pack_generic": 1, "tile_rounds": 1},
     {"scan_chunk": 256, "tile_rounds": 1},
     {"scan_chunk": 4096},
-    {"pack_img": 0},
-    {"pack_sel": 0},
-    {"pack_compact": 0},
-    {"many_super": 4},
+    {"scan_chunk": 65536},
     {"scan_max_chunks": 4096},
     {"scan_max_chunks": 8, "scan_chunk": 256},
-    {"many_super": 16, "xcd_pack": 0},
-    {"pack_img": 1, "tile_rounds": 16},
-    {"pack_img": 1, "xcd_pack": 0, "tile_rounds": 1},
-    {"scan_chunk": 65536},
-    {"many_rows": 4096},
-    {"many_rows": 2048, "many_super": 2},
-    {"many_rows": 1024},
-    {"many_rows": 1024, "many_super": 4},
+    {"pack_img_all": 1},
+    {"pack_img_all": 1, "tile_rounds": 16},
 ]
 
 
@@ -69,10 +47,16 @@ def variant(request):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     for k, v in request.param.items():
-        _lib.tune(k, v)
+        if k != "write_back":
+            _lib.test_hook(k, v)
     yield request.param
-    for k, v in DEFAULTS.items():
-        _lib.tune(k, v)
+    for k, v in _lib.HOOK_DEFAULTS.items():
+        _lib.test_hook(k, v)
+
+
+def _wb(obj, variant):
+    obj.set_write_back(variant.get("write_back", "changed"))
+    return obj
 
 
 @pytest.mark.parametrize("topo,row_bytes", [([2, 2, 2], 32), ([2, 2, 2], 36), ([7], 8),
@@ -92,7 +76,7 @@ def test_partition_variant_vs_c_oracle(variant, topo, row_bytes):
     cell = c_oracle.bin_positions(exp_pos, topo, box)
     nb = int(np.prod(topo))
     exp, exp_off = c_oracle.partition(data, cell, nb)
-    P = GridPartitioner(topo, box)
+    P = _wb(GridPartitioner(topo, box), variant)
     tpos = torch.from_numpy(pos).cuda()
     out, off = P.partition_by_position(torch.from_numpy(data).cuda(), tpos)
     assert G.same_bytes(tpos.cpu().numpy(), exp_pos)
@@ -116,7 +100,7 @@ def test_golden_variant(variant, case):
         data = [d.copy() for d in G.per_rank(f, "data", size)]
 
     def fn(comm, r):
-        return MPIGridRedistributor(comm, topo, box).redistribute_by_position(
+        return _wb(MPIGridRedistributor(comm, topo, box), variant).redistribute_by_position(
             data[r], pos[r], periodic=periodic)
 
     outs = run_ranks(size, fn)
@@ -138,16 +122,14 @@ def test_cellnum_drop_variant(variant):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), r
 
 
-@pytest.mark.parametrize("img_rpw", [1, 2])
 @pytest.mark.parametrize("row_bytes", [12, 20, 24, 28, 36, 40, 44, 52, 56, 60])
 @pytest.mark.parametrize("topo", [[2, 2, 2], [4, 4, 4], [7], [1]])
-def test_image_pack_row_sizes(row_bytes, topo, img_rpw):
+def test_image_pack_row_sizes(row_bytes, topo):
     """pack_img (16-byte image pack) for every row size it takes, ragged n,
     1..64 bins, against the C oracle."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
-    _lib.tune("pack_img", 2)     # every row size the image pack takes
-    _lib.tune("img_rpw", img_rpw)
+    _lib.test_hook("pack_img_all", 1)     # every row size the image pack takes
     try:
         rng = np.random.default_rng(row_bytes * 31 + len(topo))
         n = 50_003 + 7 * row_bytes
@@ -163,8 +145,7 @@ def test_image_pack_row_sizes(row_bytes, topo, img_rpw):
         assert np.array_equal(off.cpu().numpy(), exp_off)
         assert np.array_equal(out.cpu().numpy(), exp)
     finally:
-        _lib.tune("pack_img", DEFAULTS["pack_img"])
-        _lib.tune("img_rpw", DEFAULTS["img_rpw"])
+        _lib.test_hook("pack_img_all", 0)
 
 
 @pytest.mark.parametrize("case", ["halo_p8_f64_rec32.npz", "halo_p2_f32_rec36.npz",
@@ -179,9 +160,26 @@ def test_halo_variant(variant, case):
     pos = [p.copy() for p in G.per_rank(f, "pos_in", size)]
 
     def fn(comm, r):
-        return MPIGridRedistributor(comm if size > 1 else None, topo, box).redistribute_by_position(
-            data[r], pos[r], overload_lengths=ol)
+        R = _wb(MPIGridRedistributor(comm if size > 1 else None, topo, box), variant)
+        return R.redistribute_by_position(data[r], pos[r], overload_lengths=ol)
 
     outs = run_ranks(size, fn)
     for r in range(size):
         assert G.same_bytes(outs[r], f[f"r{r}_out"]), (case, r)
+
+
+@pytest.mark.parametrize("row_bytes", [4, 7, 12, 32, 36, 72])
+def test_one_rank_cell_number_drops(row_bytes):
+    """One rank, ids outside [0, 1) dropped (S6): the 2-bin selection with a
+    drop bin through the coop / image packs (the selection variant that loads
+    only kept rows) and the generic pack for > 64-byte rows."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from oracle import redist_oracle as ro
+    rng = np.random.default_rng(row_bytes)
+    n = 90_001
+    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
+    ids = rng.integers(-1, 3, n)                     # -1, 1, 2 dropped; 0 kept
+    exp = ro.redistribute_by_cell_number_all_ranks(1, [data], [ids])[0]
+    got = MPIGridRedistributor(None, [1], [1.0]).redistribute_by_cell_number(data, ids)
+    assert np.array_equal(got, exp)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Config-5 kernel A/B (GPU): per-kernel HIP-event times of the source-side
 partition of 64M 36-byte records with and without the fine-cell side field,
-and of the destination-side fine sort, for tuning-knob variants
-(CF5_VARIANTS, JSON list; CF5_REPEAT interleaved repeats)."""
+and of the destination-side fine sort, for test-hook variants
+(CF5_VARIANTS, JSON list, include/mgr_instrument.h; CF5_REPEAT interleaved
+repeats).  Library builds are compared by scripts/gpu_libs_ab.sh."""
 import json
 import os
 import sys
@@ -56,19 +57,15 @@ def main():
     for _ in range(repeat):
         for v in variants:
             for k, x in v.items():
-                _lib.tune(k, x)
+                _lib.test_hook(k, x)
             res = {"variant": v,
                    "src_plain": timed(lambda: part.partition_device(flat, 36, pos)),
                    "src_fine": timed(lambda: part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])),
                    "dst_sort": timed(lambda: R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=fids))}
             print(json.dumps(res), flush=True)
             for k in v:
-                _lib.tune(k, DEFAULTS[k])
+                _lib.test_hook(k, _lib.HOOK_DEFAULTS[k])
 
-
-DEFAULTS = {"scan_max_chunks": 1024, "scan_chunk": 2048, "img_rpw": 2, "bin_geo": 1, "rank_rows": 0, "bin_waves": 0, "pack_img": 1, "tile_rounds": 0, "xcd_pack": 16,
-            "bin_staged": 1, "bin_skip_clean": 1, "ranked_walk": 0,
-            "rank_orm": 1}
 
 if __name__ == "__main__":
     main()

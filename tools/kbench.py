@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Kernel A/B microbenchmark (GPU): per-kernel HIP-event times of the local
-stage (bin_count, scan, pack) on BASELINE config 2 for tuning-knob variants,
-next to torch's device copy of the same payload as a practical HBM ceiling."""
+stage (bin_count, scan, pack) on BASELINE config 2 (KB_VARIANTS: JSON list
+of {"topo", "input", "rec"} workloads and test hooks, include/mgr_instrument.h),
+next to torch's device copy of the same payload as a practical HBM ceiling.
+Library builds are compared by scripts/gpu_libs_ab.sh."""
 import json
 import os
 import sys
@@ -22,8 +24,9 @@ def run(variant):
     clustered = variant.pop("input", "uniform") == "clustered"
     rb = variant.pop("rec", 32)
     for k, v in variant.items():
-        _lib.tune(k, v)
+        _lib.test_hook(k, v)
     part = mgr.GridPartitioner(topo, [1.0] * len(topo))
+    part.set_write_back("all")   # every step writes the wrapped positions back (bench.py)
     if rb == 36:   # config 5 record: f32 pos x3, vel x3, mass, i64 id; position = its view
         rec = torch.zeros((N, 36), dtype=torch.uint8, device="cuda")
         f = rec.view(torch.float32)
@@ -57,12 +60,8 @@ def run(variant):
         out[k] = round(ms / max(cnt, 1), 4)
     out["bin_GBps"] = round(49 * N / (out["bin_count"] / 1e3) / 1e9, 1)
     out["pack_GBps"] = round((2 * rb + 1) * N / (out["pack"] / 1e3) / 1e9, 1)
-    for k, v in {"bin_staged": 1, "tile_rounds": 0, "pack_coop": 1,
-                 "xcd_pack": 16, "xcd_bin": 0, "bin_skip_clean": 1,
-                 "bin_waves": 0, "pack_many": 1, "scan_chunk": 2048,
-                 "pack_img": 1, "many_super": 1, "scan_max_chunks": 1024, "pack_sel": 1,
-                 "pack_compact": 1, "many_rows": 0, "bin_geo": 1, "img_rpw": 2, "ranked_walk": 0}.items():
-        _lib.tune(k, v)
+    for k, v in _lib.HOOK_DEFAULTS.items():
+        _lib.test_hook(k, v)
     del part, pos, rec, flat
     torch.cuda.empty_cache()
     return out
