@@ -237,9 +237,9 @@ class RcclComm(Transport):
         _lib.call("mgr_exchange_counts", self._h, _lib.ptr(send_counts), _lib.ptr(recv), stream)
         P = self.size
         self._pinned[:P].copy_(send_counts, non_blocking=True)
-        self._pinned[P:].copy_(recv, non_blocking=True)
+        self._pinned[P:2 * P].copy_(recv, non_blocking=True)
         torch.cuda.current_stream().synchronize()
-        host = self._pinned.numpy().copy()
+        host = self._pinned[:2 * P].numpy().copy()
         return host[:P], host[P:]
 
     def exchange_count_rows(self, send):

@@ -439,9 +439,12 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
     clear_scan_flags(scan_flags);
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const int64_t tile = xcd_tile(blockIdx.x, T);
-    for (int i = tid; i < NW * nbins; i += NT) {
-        wt[i] = 0;
-        mk[i] = 0ull;
+    {   // zero the peer words and running counts in 16-byte stores (the LDS
+        // regions are 16-byte aligned: nbins * 8 per wave, then the counts)
+        typedef unsigned int z4_t __attribute__((ext_vector_type(4)));
+        const int nz = (NW * nbins * 8 + align16(NW * nbins * 2)) / 16;
+        z4_t* z = (z4_t*)smem;
+        for (int i = tid; i < nz; i += NT) z[i] = z4_t{0u, 0u, 0u, 0u};
     }
     unsigned b[RPW];
     bool oob = false;   // ids >= nbins: clamped, reported through *bad
@@ -491,12 +494,7 @@ __global__ __launch_bounds__(NW * 64) void rank_ids_kernel(
             run += c[ww2];
         }
         if (bb < nbins) counts[(int64_t)bb * T + tile] = run;
-        int incl = run;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
+        const int incl = wave_incl_dpp(run);
         if (lane == 63) s_wsum[w] = incl;
         __syncthreads();
         int wpre = 0, wall = 0;

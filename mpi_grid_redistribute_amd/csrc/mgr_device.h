@@ -615,6 +615,39 @@ __device__ __forceinline__ int wave_excl(int v, int* total) {
     return x - v;
 }
 
+// inclusive prefix over the wave's 64 lanes by DPP (row shifts inside each
+// 16-lane row, then the row broadcasts of lanes 15 and 31): no LDS round
+// trips, where __shfl_up lowers to a chain of ds_bpermute_b32.
+__device__ __forceinline__ int wave_incl_dpp(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// exclusive prefix over the wave's lanes of small values (v < 2^BITS), by
+// bit-sliced ballots: prefix = sum_i 2^i * (lanes below with bit i) -- BITS
+// ballots and lane-mask popcounts (v_mbcnt), no LDS.  wave_excl's __shfl_up
+// chain lowers to 7 dependent ds_bpermute_b32 round trips, which made the
+// halo's per-set list building latency-bound.
+template <int BITS>
+__device__ __forceinline__ int wave_excl_small(unsigned v, int* total) {
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < BITS; ++i) {
+        const unsigned long long b = __ballot((v >> i) & 1u);
+        const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+        pre += (int)below << i;
+        tot += __popcll(b) << i;
+    }
+    *total = tot;
+    return pre;
+}
+
 // XCD-contiguous tile order.  Workgroups are dealt to the 8 XCDs round-robin
 // (blockIdx % 8 labels the XCD, MI355X_MICROARCH.md "Workgroup dispatch"), so
 // tile = blockIdx would put neighbouring tiles on different L2s.  This

@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
             uint32_t m = set_mask_t<NB>(fp, masks.m[k], nbits);
             if (!__ballot(m != 0u)) continue;   // an empty set costs no prefix
             int total;
-            int pos = wave_excl(__popc(m), &total);
+            int pos = wave_excl_small<5>(__popc(m), &total);   // popc(m) <= 16
             if (!total) continue;
             if (fill + total > kSelCap) {
                 flush(fill);
@@ -523,13 +523,7 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     if (scan_failed(scan_err)) return;
     for (int j = 0; j < w; ++j) tbase += s_cnt[j * 64 + lane];
     // wave image order: exclusive prefix of the wave's bin counts
-    int incl = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    const int excl = incl - cnt;
+    const int excl = wave_incl_dpp(cnt) - cnt;
     int slot[RPW];
     int run = excl;   // lane b: bin b's next image slot, round by round
 #pragma unroll
@@ -1003,6 +997,63 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
+// One row of NDW dwords (4-byte aligned) from registers: 16-byte stores and a tail.
+template <int NDW>
+__device__ __forceinline__ void store_row_dw(unsigned long long a, const uint32_t (&v)[NDW]) {
+    int i = 0;
+#pragma unroll
+    for (; i + 4 <= NDW; i += 4) gstore<u32x4_a4>(a + 4 * i, u32x4_a4{v[i], v[i + 1], v[i + 2], v[i + 3]});
+    if constexpr (NDW % 4 == 3) {
+        gstore<u32x3_a4>(a + 4 * i, u32x3_a4{v[i], v[i + 1], v[i + 2]});
+    } else if constexpr (NDW % 4 == 2) {
+        gstore<u32x2_a4>(a + 4 * i, u32x2_a4{v[i], v[i + 1]});
+    } else if constexpr (NDW % 4 == 1) {
+        gstore<uint32_t>(a + 4 * i, v[i]);
+    }
+}
+
+// Direct ranked pack: every row goes from registers straight to its output
+// slot (tile start of its bin + its slot from mgr_rank_ids), no LDS image --
+// so workgroups are small (256 threads, RPT rows per thread, several
+// workgroups per ranked tile) and many run per CU; the rows of one (bin,
+// tile) run are written by one workgroup within a few microseconds, so their
+// partial lines merge in L2.  LDS holds only the tile's per-bin output
+// addresses (<= 1024 bins).
+template <int RB, int RPT>
+__global__ __launch_bounds__(256) void pack_ranked_direct_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
+    const uint16_t* __restrict__ slots, const uint16_t* __restrict__ tile_starts, int nb,
+    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err) {
+    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
+    constexpr int NDW = RB / 4, ROWS = 256 * RPT;
+    __shared__ unsigned long long gaddr[1024];
+    if (scan_failed(scan_err)) return;
+    const int parts = tile_rows / ROWS;
+    const int64_t wg = xcd_tile(blockIdx.x, T * parts);   // a tile's parts and its
+    const int64_t tile = wg / parts;                      // neighbours on one XCD
+    const int64_t row0 = wg * (int64_t)ROWS;
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    uint32_t v[RPT][NDW];
+    unsigned b[RPT], sl[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t r = min(row0 + (int64_t)(w * RPT + q) * 64 + lane, n - 1);
+        b[q] = min((unsigned)ids[r], (unsigned)(nb - 1));   // ids >= nb: clamped (mgr_rank_ids reports them)
+        sl[q] = slots[r];
+        load_row_dw<NDW>(src + r * RB, v[q]);
+    }
+    for (int bb = tid; bb < nb; bb += 256)
+        gaddr[bb] = (unsigned long long)(dst + (offsets[(int64_t)bb * T + tile] -
+                                                (long long)tile_starts[tile * nb + bb]) * (long long)RB);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t row = row0 + (int64_t)(w * RPT + q) * 64 + lane;
+        if (row < n) store_row_dw<NDW>(gaddr[b[q]] + (unsigned long long)sl[q] * RB, v[q]);
+    }
+}
+
 // LDS of the ranked pack: the tile image, its row bins and per-bin output
 // addresses.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
@@ -1027,11 +1078,34 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
         return hipErrorNotSupported;
     const int lds = ranked_lds_bytes(tile_rows, row_bytes, nbins);
     if (lds > 160 * 1024) return hipErrorNotSupported;
+    prof_begin(s, K_PACK_FINE);
+    hipError_t e = hipErrorNotSupported;
+#ifdef MGR_RANKED_DIRECT
+    if (nbins <= 1024) {
+        constexpr int RPT = MGR_RANKED_DIRECT;
+        const int64_t grid = ws.T * (tile_rows / (256 * RPT));
+#define MGR_PRD(RB_)                                                                          \
+        case RB_:                                                                             \
+            hipLaunchKernelGGL((pack_ranked_direct_kernel<RB_, RPT>), dim3((unsigned)grid),   \
+                               dim3(256), 0, s, (const uint8_t*)src, n, ids, ranks,          \
+                               tile_starts, nbins, ws.offsets, ws.T, tile_rows, (uint8_t*)dst,\
+                               ws.scan_err);                                                  \
+            e = hipGetLastError();                                                            \
+            break;
+        switch ((int)row_bytes) {
+            MGR_PRD(4) MGR_PRD(8) MGR_PRD(12) MGR_PRD(16) MGR_PRD(20) MGR_PRD(24) MGR_PRD(28)
+            MGR_PRD(32) MGR_PRD(36) MGR_PRD(40) MGR_PRD(44) MGR_PRD(48) MGR_PRD(52) MGR_PRD(56)
+            MGR_PRD(60) MGR_PRD(64)
+            default: break;
+        }
+#undef MGR_PRD
+        prof_end(s, K_PACK_FINE);
+        return e;
+    }
+#endif
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;
-    prof_begin(s, K_PACK_FINE);
-    hipError_t e = hipErrorNotSupported;
 #define MGR_PRT(RB_, TR_)                                                                     \
     {                                                                                         \
         auto k = pack_ranked_kernel<RB_, TR_>;                                                \
