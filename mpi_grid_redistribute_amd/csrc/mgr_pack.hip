@@ -305,13 +305,8 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
             wave_sync();
         };
         int fill = 0;
-        for (int k = 0; k < nsets; ++k) {
-            if (!((live >> k) & 1u)) continue;
-            uint32_t m = set_mask_t<NB>(fp, masks.m[k], nbits);
-            if (!__ballot(m != 0u)) continue;   // an empty set costs no prefix
-            int total;
-            int pos = wave_excl_small<5>(__popc(m), &total);   // popc(m) <= 16
-            if (!total) continue;
+        // list set k's rows (row order) at the list's end; flush first if full
+        auto emit = [&](int k, uint32_t m, int pos, int total) __attribute__((always_inline)) {
             if (fill + total > kSelCap) {
                 flush(fill);
                 fill = 0;
@@ -327,6 +322,21 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
                 list[pos++] = (uint16_t)((16 * lane + j) | (k << 10));
             }
             fill += total;
+        };
+        // two sets per wave prefix: the lanes' member counts (<= 16 each,
+        // <= 1024 per wave) of sets k and k + 1 in the two 16-bit halves of one
+        // DPP scan (a __shfl_up scan was 7 dependent LDS round trips per set)
+        for (int k = 0; k < nsets; k += 2) {
+            const bool l0 = (live >> k) & 1u, l1 = k + 1 < nsets && ((live >> (k + 1)) & 1u);
+            const uint32_t m0 = l0 ? set_mask_t<NB>(fp, masks.m[k], nbits) : 0u;
+            const uint32_t m1 = l1 ? set_mask_t<NB>(fp, masks.m[k + 1], nbits) : 0u;
+            if (!__ballot((m0 | m1) != 0u)) continue;   // empty sets cost no prefix
+            const int packed = (int)(__popc(m0) | (__popc(m1) << 16));
+            const int incl = wave_incl_dpp(packed);
+            const int excl = incl - packed;
+            const int tot = __builtin_amdgcn_readlane(incl, 63);
+            if (tot & 0xffff) emit(k, m0, excl & 0xffff, tot & 0xffff);
+            if (tot >> 16) emit(k + 1, m1, excl >> 16, tot >> 16);
         }
         if (fill) flush(fill);
     }
@@ -944,11 +954,14 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
             load_row_dw<NDW>(src + row * RB, S.v[q]);
         }
     };
-    // (A/B, round 4: a branch-free scatter, which let the compiler keep the
-    // next tile's loads in flight through the store phase instead of
-    // draining them in the store loop's preheader, measured SLOWER: 1.14 vs
-    // 1.10 ms, with or without a fully unrolled store loop -- the load and
-    // store phases are not latency-serialised, profiles/round4/ab_notes.md.)
+    // (A/Bs, round 4, profiles/round4/ab_notes.md: a branch-free scatter,
+    // which let the compiler keep the next tile's loads in flight through the
+    // store phase, measured SLOWER (1.14 vs 1.10 ms, with or without a fully
+    // unrolled store loop); so did the rows stored straight from registers
+    // to their slots by small workgroups, no LDS image (1.50-1.96 ms).  With
+    // every store sent sequentially to the tile's own region this kernel
+    // takes 0.95 ms: the one 1024-thread workgroup per CU that the image
+    // needs is the ceiling, the run scatter adds 0.15 ms.)
     auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
         const int tr = (int)min((int64_t)TR, n - t * TR);
         if (tid < nb) gaddr[tid] = (unsigned long long)(dst + (S.seg - (long long)S.ls) * (long long)RB);
@@ -997,63 +1010,6 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
-// One row of NDW dwords (4-byte aligned) from registers: 16-byte stores and a tail.
-template <int NDW>
-__device__ __forceinline__ void store_row_dw(unsigned long long a, const uint32_t (&v)[NDW]) {
-    int i = 0;
-#pragma unroll
-    for (; i + 4 <= NDW; i += 4) gstore<u32x4_a4>(a + 4 * i, u32x4_a4{v[i], v[i + 1], v[i + 2], v[i + 3]});
-    if constexpr (NDW % 4 == 3) {
-        gstore<u32x3_a4>(a + 4 * i, u32x3_a4{v[i], v[i + 1], v[i + 2]});
-    } else if constexpr (NDW % 4 == 2) {
-        gstore<u32x2_a4>(a + 4 * i, u32x2_a4{v[i], v[i + 1]});
-    } else if constexpr (NDW % 4 == 1) {
-        gstore<uint32_t>(a + 4 * i, v[i]);
-    }
-}
-
-// Direct ranked pack: every row goes from registers straight to its output
-// slot (tile start of its bin + its slot from mgr_rank_ids), no LDS image --
-// so workgroups are small (256 threads, RPT rows per thread, several
-// workgroups per ranked tile) and many run per CU; the rows of one (bin,
-// tile) run are written by one workgroup within a few microseconds, so their
-// partial lines merge in L2.  LDS holds only the tile's per-bin output
-// addresses (<= 1024 bins).
-template <int RB, int RPT>
-__global__ __launch_bounds__(256) void pack_ranked_direct_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
-    const uint16_t* __restrict__ slots, const uint16_t* __restrict__ tile_starts, int nb,
-    const int64_t* __restrict__ offsets, int64_t T, int tile_rows, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err) {
-    static_assert(RB % 4 == 0 && RB <= 64, "ranked pack row size");
-    constexpr int NDW = RB / 4, ROWS = 256 * RPT;
-    __shared__ unsigned long long gaddr[1024];
-    if (scan_failed(scan_err)) return;
-    const int parts = tile_rows / ROWS;
-    const int64_t wg = xcd_tile(blockIdx.x, T * parts);   // a tile's parts and its
-    const int64_t tile = wg / parts;                      // neighbours on one XCD
-    const int64_t row0 = wg * (int64_t)ROWS;
-    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    uint32_t v[RPT][NDW];
-    unsigned b[RPT], sl[RPT];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int64_t r = min(row0 + (int64_t)(w * RPT + q) * 64 + lane, n - 1);
-        b[q] = min((unsigned)ids[r], (unsigned)(nb - 1));   // ids >= nb: clamped (mgr_rank_ids reports them)
-        sl[q] = slots[r];
-        load_row_dw<NDW>(src + r * RB, v[q]);
-    }
-    for (int bb = tid; bb < nb; bb += 256)
-        gaddr[bb] = (unsigned long long)(dst + (offsets[(int64_t)bb * T + tile] -
-                                                (long long)tile_starts[tile * nb + bb]) * (long long)RB);
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int64_t row = row0 + (int64_t)(w * RPT + q) * 64 + lane;
-        if (row < n) store_row_dw<NDW>(gaddr[b[q]] + (unsigned long long)sl[q] * RB, v[q]);
-    }
-}
-
 // LDS of the ranked pack: the tile image, its row bins and per-bin output
 // addresses.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
@@ -1080,29 +1036,6 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if (lds > 160 * 1024) return hipErrorNotSupported;
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
-#ifdef MGR_RANKED_DIRECT
-    if (nbins <= 1024) {
-        constexpr int RPT = MGR_RANKED_DIRECT;
-        const int64_t grid = ws.T * (tile_rows / (256 * RPT));
-#define MGR_PRD(RB_)                                                                          \
-        case RB_:                                                                             \
-            hipLaunchKernelGGL((pack_ranked_direct_kernel<RB_, RPT>), dim3((unsigned)grid),   \
-                               dim3(256), 0, s, (const uint8_t*)src, n, ids, ranks,          \
-                               tile_starts, nbins, ws.offsets, ws.T, tile_rows, (uint8_t*)dst,\
-                               ws.scan_err);                                                  \
-            e = hipGetLastError();                                                            \
-            break;
-        switch ((int)row_bytes) {
-            MGR_PRD(4) MGR_PRD(8) MGR_PRD(12) MGR_PRD(16) MGR_PRD(20) MGR_PRD(24) MGR_PRD(28)
-            MGR_PRD(32) MGR_PRD(36) MGR_PRD(40) MGR_PRD(44) MGR_PRD(48) MGR_PRD(52) MGR_PRD(56)
-            MGR_PRD(60) MGR_PRD(64)
-            default: break;
-        }
-#undef MGR_PRD
-        prof_end(s, K_PACK_FINE);
-        return e;
-    }
-#endif
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;
