@@ -190,6 +190,7 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
 // gather.  Rows wider than 64 units are copied one after the other, lanes
 // across the row.
 constexpr int kSelCap = 2048;   // LDS entries per wave (>= kSelChunk)
+static_assert(kSelCap >= kSelChunk, "a set of one chunk must fit an empty list");
 constexpr int kSelDepth = 4;    // copy instructions in flight per field (8: 1.17 vs 1.10 ms)
 constexpr int kSelFields = 3;
 struct SelFields {
@@ -304,41 +305,41 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
             }
             wave_sync();
         };
-        int fill = 0;
-        // list set k's rows (row order) at the list's end; flush first if full
-        auto emit = [&](int k, uint32_t m, int pos, int total) __attribute__((always_inline)) {
-            if (fill + total > kSelCap) {
-                flush(fill);
-                fill = 0;
+        // the sets' lists, flushed when the next set does not fit: ONE call
+        // site of flush (its copy loops are most of the kernel's code; inlined
+        // at two or three sites the kernel ran 2x slower)
+        int k = 0;
+        for (;;) {
+            int fill = 0;
+            bool full = false;
+            for (; k < nsets; ++k) {
+                if (!((live >> k) & 1u)) continue;
+                uint32_t m = set_mask_t<NB>(fp, masks.m[k], nbits);
+                if (!__ballot(m != 0u)) continue;   // an empty set costs no prefix
+                int total;
+                // bit-sliced ballot prefix (A/B: 1.122 vs 1.162 ms with the
+                // __shfl_up scan)
+                int pos = wave_excl_small<5>(__popc(m), &total);   // popc(m) <= 16
+                if (!total) continue;
+                if (fill + total > kSelCap) {   // (fill > 0: a set is <= kSelChunk rows)
+                    full = true;
+                    break;                       // set k again after the flush
+                }
+                if (lane == 0) {
+                    start[k] = fill;
+                    cnt[k] = total;
+                }
+                pos += fill;
+                while (m) {
+                    const int j = __builtin_ctz(m);
+                    m &= m - 1u;
+                    list[pos++] = (uint16_t)((16 * lane + j) | (k << 10));
+                }
+                fill += total;
             }
-            if (lane == 0) {
-                start[k] = fill;
-                cnt[k] = total;
-            }
-            pos += fill;
-            while (m) {
-                const int j = __builtin_ctz(m);
-                m &= m - 1u;
-                list[pos++] = (uint16_t)((16 * lane + j) | (k << 10));
-            }
-            fill += total;
-        };
-        // two sets per wave prefix: the lanes' member counts (<= 16 each,
-        // <= 1024 per wave) of sets k and k + 1 in the two 16-bit halves of one
-        // DPP scan (a __shfl_up scan was 7 dependent LDS round trips per set)
-        for (int k = 0; k < nsets; k += 2) {
-            const bool l0 = (live >> k) & 1u, l1 = k + 1 < nsets && ((live >> (k + 1)) & 1u);
-            const uint32_t m0 = l0 ? set_mask_t<NB>(fp, masks.m[k], nbits) : 0u;
-            const uint32_t m1 = l1 ? set_mask_t<NB>(fp, masks.m[k + 1], nbits) : 0u;
-            if (!__ballot((m0 | m1) != 0u)) continue;   // empty sets cost no prefix
-            const int packed = (int)(__popc(m0) | (__popc(m1) << 16));
-            const int incl = wave_incl_dpp(packed);
-            const int excl = incl - packed;
-            const int tot = __builtin_amdgcn_readlane(incl, 63);
-            if (tot & 0xffff) emit(k, m0, excl & 0xffff, tot & 0xffff);
-            if (tot >> 16) emit(k + 1, m1, excl >> 16, tot >> 16);
+            if (fill) flush(fill);
+            if (!full) break;
         }
-        if (fill) flush(fill);
     }
 }
 
@@ -1010,6 +1011,73 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
+#ifdef MGR_RANKED_HALF
+// Ranked pack in two slot halves: one 512-thread workgroup per 4096-row
+// ranked tile holds the tile's rows in registers (8 per thread) and builds
+// the image of slots [0, 2048) then [2048, 4096) in one 80 KiB LDS half, so
+// two workgroups share a CU (their load and store phases interleave) while
+// the ranked tiles -- and so the (bin, tile) runs -- stay 4096 rows long.
+template <int RB, int TR>
+__global__ __launch_bounds__(512) void pack_ranked_half_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
+    const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
+    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ scan_err) {
+    constexpr int NT = 512, RPT = TR / NT, NDW = RB / 4, HALF = TR / 2;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* img = (uint32_t*)smem;
+    uint16_t* ibin = (uint16_t*)(smem + align16(HALF * RB));
+    unsigned long long* gaddr = (unsigned long long*)(smem + align16(HALF * RB) + align16(HALF * 2));
+    if (scan_failed(scan_err)) return;
+    const int tid = threadIdx.x;
+    const int64_t tile = xcd_tile(blockIdx.x, T);
+    const int tr = (int)min((int64_t)TR, n - tile * TR);
+    uint32_t v[RPT][NDW];
+    unsigned b[RPT], sl[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        const int64_t r = min(tile * TR + q * NT + tid, n - 1);
+        b[q] = min((unsigned)ids[r], (unsigned)(nb - 1));
+        sl[q] = q * NT + tid < tr ? (unsigned)ranks[r] : 0xFFFFu;
+        load_row_dw<NDW>(src + r * RB, v[q]);
+    }
+    for (int bb = tid; bb < nb; bb += NT)
+        gaddr[bb] = (unsigned long long)(dst + (offsets[(int64_t)bb * T + tile] -
+                                                (long long)tile_starts[tile * nb + bb]) * (long long)RB);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int lo = h * HALF, hi = min(tr, lo + HALF);
+        if (lo >= tr) break;
+        __syncthreads();   // gaddr written; the previous half's image stored
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int ls = (int)sl[q] - lo;
+            if (ls >= 0 && ls < HALF) {
+#pragma unroll
+                for (int i = 0; i < NDW; ++i) img[ls * NDW + i] = v[q][i];
+                ibin[ls] = (uint16_t)b[q];
+            }
+        }
+        __syncthreads();
+        const int nbytes = (hi - lo) * RB;
+        const unsigned long long xo = (unsigned long long)lo * RB;
+        for (int x = 16 * tid; x < nbytes; x += 16 * NT) {
+            const u32x4_t qv = *(const u32x4_t*)((const uint8_t*)img + x);
+            const int bf = ibin[x / RB];
+            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+                gstore<u32x4_a4>(gaddr[bf] + xo + x, qv);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xo + xd, qv[d]);
+                }
+            }
+        }
+    }
+}
+#endif
+
 // LDS of the ranked pack: the tile image, its row bins and per-bin output
 // addresses.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
@@ -1036,6 +1104,19 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if (lds > 160 * 1024) return hipErrorNotSupported;
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
+#ifdef MGR_RANKED_HALF
+    if (tile_rows == 4096 && nbins <= 1024 && row_bytes == 36) {
+        const int hl = align16(2048 * 36) + align16(2048 * 2) + nbins * 8;
+        auto k = pack_ranked_half_kernel<36, 4096>;
+        ensure_lds(k, hl);
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(512), (size_t)hl, s, (const uint8_t*)src,
+                           n, ids, ranks, tile_starts, nbins, ws.offsets, ws.T, (uint8_t*)dst,
+                           ws.scan_err);
+        e = hipGetLastError();
+        prof_end(s, K_PACK_FINE);
+        return e;
+    }
+#endif
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;

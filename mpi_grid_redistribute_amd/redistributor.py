@@ -213,17 +213,36 @@ class Scratch:
     few.  Buffers are kept per CUDA stream (the current stream at the call):
     calls on one stream run in order and reuse them safely; a call on another
     stream gets buffers of its own, so calls overlapping on two streams never
-    share a workspace or a send buffer."""
+    share a workspace or a send buffer.  Memory: one full set per stream used,
+    for at most MAX_STREAMS streams -- a call on a further stream first waits
+    for the least recently used stream and frees its set."""
 
     GROWTH = 1.25
+    MAX_STREAMS = 4
 
     def __init__(self, dev):
         self.dev = dev
         self.bufs = {}
+        self.streams = {}          # stream handle -> torch stream, least recently used first
+
+    def _stream_key(self):
+        st = torch.cuda.current_stream(self.dev)
+        key = st.cuda_stream
+        if key in self.streams:
+            self.streams[key] = self.streams.pop(key)     # most recently used last
+            return key
+        while len(self.streams) >= self.MAX_STREAMS:
+            old_key, old = next(iter(self.streams.items()))
+            old.synchronize()                             # its calls are done with the set
+            del self.streams[old_key]
+            for k in [k for k in self.bufs if k[1] == old_key]:
+                del self.bufs[k]
+        self.streams[key] = st
+        return key
 
     def get(self, name, nbytes):
         nbytes = max(int(nbytes), 1)
-        key = (name, torch.cuda.current_stream(self.dev).cuda_stream)
+        key = (name, self._stream_key())
         b = self.bufs.get(key)
         if b is None or b.numel() < nbytes:
             if b is not None:
@@ -235,6 +254,7 @@ class Scratch:
 
     def release(self):
         self.bufs.clear()
+        self.streams.clear()
 
 
 def _scratch(n, nbins, max_row_bytes, dev, cache=None, dest=True, tag="", tile_rows=None):

@@ -199,3 +199,24 @@ def test_no_device_allocation_after_warmup():
         del out
     torch.cuda.synchronize()
     assert torch.cuda.memory_stats()["segment.all.allocated"] == seg0
+
+
+def test_scratch_per_stream_capped():
+    """Calls on many streams keep at most Scratch.MAX_STREAMS sets of scratch
+    buffers (the least recently used stream is waited for and its set freed),
+    and every call's result stays correct."""
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    R2 = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    n = 200_003
+    pos, rec = mgr.synth_uniform(n, seed=77)
+    want = R2.redistribute_by_position(rec.clone(), pos.clone())
+    streams = [torch.cuda.Stream() for _ in range(R._scratch.MAX_STREAMS + 3)]
+    outs = []
+    for st in streams:
+        with torch.cuda.stream(st):
+            outs.append(R.redistribute_by_position(rec.clone(), pos.clone()))
+        assert len(R._scratch.streams) <= R._scratch.MAX_STREAMS
+        assert len({k[1] for k in R._scratch.bufs}) <= R._scratch.MAX_STREAMS
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, want)

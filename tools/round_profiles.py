@@ -18,7 +18,7 @@ import pmc_summary  # noqa: E402
 
 SRC, DST = sys.argv[1], sys.argv[2]
 TRAFFIC = "profiles/traffic.json"
-LINES = ("cfg2", "cfg5", "cfg3x", "halo")
+LINES = ("cfg2", "cfg4", "cfg5", "cfg3x", "halo")
 # rocprof kernel short name -> bench profiler name
 NAMES = {"bin_count_kernel": "bin_count", "pack_coop_kernel": "pack", "pack_img_kernel": "pack",
          "pack_kernel": "pack", "pack_ranked_kernel": "pack_fine", "pack_fine_kernel": "pack_fine",
