@@ -67,6 +67,26 @@ def _p2p(transport, ops):
     transport.p2p(ops)
 
 
+# The multi-rank halo's count messages carry a failure bit beside the size: a
+# selection scan that gave up (-1 counts) is announced as size 0 with the bit
+# set, so every message of the exchange keeps consistent sizes on both sides
+# (nobody waits for a message that will not come), and the ranks agree on the
+# failure ONCE, after the last message, instead of after every count exchange.
+_FAIL = 1 << 62
+
+
+def _encode_counts(c):
+    """Device int64 counts -> message words: size (>= 0), plus _FAIL on every
+    word when any count is negative (a failed scan poisons all of them)."""
+    bad = (c < 0).any()
+    return torch.where(bad, torch.full_like(c, _FAIL), c.clamp(min=0))
+
+
+def _decode(words):
+    w = np.asarray(words, dtype=np.int64)
+    return w & (_FAIL - 1), bool((w >> 62).any())
+
+
 def _agree_counts(transport, sent, received):
     """check_counts on every rank at once: a -1 count (a selection scan that
     gave up) reaches only the neighbours of the failed rank, so the ranks
@@ -315,7 +335,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
     lh, lcount = sel.msel(flags, n, list(range(S)), "_local")
     # 2. local counts to the neighbours (step 1 then step 2 of every dimension)
     send_l = torch.zeros(S, dtype=torch.int64, device=dev)
-    send_l.copy_(lcount)
+    send_l.copy_(_encode_counts(lcount))
     for d, (a, b, keep_a, keep_b) in enumerate(nb):
         if not keep_a:
             send_l[2 * d].zero_()
@@ -330,9 +350,12 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                 ("recv", a, recv_l[2 * d + 1:2 * d + 2].view(torch.uint8))]
     _p2p(transport, ops)
     ls, rl = sel.to_host([send_l, recv_l])                   # host sync 1
-    # a failed selection scan reports -1 counts (here or, through the count
-    # messages, at a neighbour): every rank agrees and raises together
-    _agree_counts(transport, ls, rl)
+    # a failed selection scan (here, or at a neighbour through its messages)
+    # travels as the failure bit; sizes stay consistent, the ranks agree at
+    # the end of the exchange
+    ls, f1 = _decode(ls)
+    rl, f2 = _decode(rl)
+    failed = f1 or f2
 
     # the append-only overload store: data (+ positions) + flags
     st = [None] * F
@@ -417,7 +440,9 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
             recv_g = torch.zeros(2, dtype=torch.int64, device=dev)
             if m:
                 gh, gcount = sel.msel(store(FL, 0, m).view(torch.int16), m, [sa, sb], "_ghost")
-                send_g.copy_(gcount)
+                send_g.copy_(_encode_counts(gcount))
+            if failed:   # keep announcing it: the neighbours' neighbours learn too
+                send_g.fill_(_FAIL)
             if not keep_a:
                 send_g[0].zero_()
             if not keep_b:
@@ -427,7 +452,10 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                            ("send", b, send_g[1:2].view(torch.uint8)),
                            ("recv", a, recv_g[1:2].view(torch.uint8))])
             gc, rg = sel.to_host([send_g, recv_g])            # host sync per dimension
-            _agree_counts(transport, gc, rg)
+            gc, f1 = _decode(gc)
+            rg, f2 = _decode(rg)
+            # (sizes stay as announced -- the neighbours post receives of them)
+            failed = failed or f1 or f2
         nla, nlb = local_pieces(d)
         nga, ngb = int(gc[0]), int(gc[1])
         # what it receives: from_b (step 1) and from_a (step 2), each a local
@@ -473,6 +501,9 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                     ops.append(("recv", frm, store(f, at + rl_, rg_)))
         _p2p(transport, ops)
         m = new_m
+    # one agreement per call: every rank raises together if any scan failed
+    if transport.any_failed(failed):
+        check_counts([-1], [])
     if not m:
         empty = torch.empty(0, dtype=torch.uint8, device=dev)
         return empty, (empty if carry_pos else None), 0, in_arena

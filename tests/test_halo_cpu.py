@@ -267,16 +267,21 @@ def test_threaded_halo_traffic(case):
         assert extra % 8 == 0 and 0 < extra <= 8 * 4 * dim, (r, extra)
 
 
-def test_halo_failed_selection_raises():
-    """A selection scan that failed on one rank (-1 counts) makes every rank
-    raise at the count exchange (the -1 travels to the neighbours), instead of
-    posting messages of mismatched sizes."""
+@pytest.mark.parametrize("fail_tag", ["_local", "_ghost"])
+def test_halo_failed_selection_raises(fail_tag):
+    """A selection scan that failed on one rank (-1 counts) -- of its local
+    rows, or of the rows received in an earlier dimension -- makes every rank
+    raise: the failure travels as a bit in the count messages (sizes stay
+    consistent, every message still matches) and the ranks agree once at the
+    end of the exchange."""
     from mpi_grid_redistribute_amd._lib import MgrError
 
     class FailingSelect(CpuSelect):
         def msel(self, flags, n, bits, tag):
             sets, counts = super().msel(flags, n, bits, tag)
-            return sets, torch.full_like(counts, -1)
+            if tag == fail_tag:
+                counts = torch.full_like(counts, -1)
+            return sets, counts
 
     f = G.load("halo_p8_f64_rec32.npz")
     size = int(f["size"])
