@@ -69,7 +69,7 @@ def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512):
     }
 
 
-def xgmi_report(traffic, exch, dist, world):
+def xgmi_report(traffic, exch, dist, world, chunks):
     """Per-direction xGMI figures of one step: this rank's bytes sent to and
     received from other ranks (MPIGridRedistributor.last_traffic: the
     exchange's real layout, every field and side field, the halo's messages)
@@ -87,7 +87,11 @@ def xgmi_report(traffic, exch, dist, world):
         vals = t.tolist()
     send, recv, ms, speers, rpeers = vals
     out = {"unit": "GB/s", "ms_per_step": ms, "link_peak_per_direction": XGMI_LINK_GBS_PER_DIR,
-           "bytes_from": "exchange layout (MPIGridRedistributor.last_traffic), max over ranks"}
+           "bytes_from": "exchange layout (MPIGridRedistributor.last_traffic), max over ranks",
+           # which exchange the figures come from: the pipelined one (k chunk
+           # messages per peer, exchange.exchange_pipelined) or one message
+           "path": (f"pipelined, {chunks} chunks per peer (exchange_pipelined)" if chunks > 1
+                    else "one message per peer (exchange)")}
     for name, b, k in (("send", send, speers), ("recv", recv, rpeers)):
         peak = k * XGMI_LINK_GBS_PER_DIR
         ach = b / (ms / 1e3) / 1e9 if ms > 0 else 0.0
@@ -400,7 +404,7 @@ def main():
         skew = count_skew(torch.stack(rows).cpu().numpy())
     xgmi = None
     if multi and "exchange" in kernels:
-        xgmi = xgmi_report(R.last_traffic, kernels["exchange"], dist, world)
+        xgmi = xgmi_report(R.last_traffic, kernels["exchange"], dist, world, chunks)
     # per-kernel algorithmic bytes per launch: per-row figure x the rows one
     # launch processes (n: every launch of these kernels covers this rank's
     # rows -- received rows at N > 1 are ~n for the uniform inputs), or the

@@ -628,6 +628,16 @@ __device__ __forceinline__ int wave_incl_dpp(int x) {
     return x;
 }
 
+// a 64-bit value of lane l (uniform l), by two readlanes
+__device__ __forceinline__ long long readlane64(long long v, int l) {
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned long long)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)((unsigned long long)v >> 32), l);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+    return (unsigned long long)readlane64((long long)v, l);
+}
+
 // exclusive prefix over the wave's lanes of small values (v < 2^BITS), by
 // bit-sliced ballots: prefix = sum_i 2^i * (lanes below with bit i) -- BITS
 // ballots and lane-mask popcounts (v_mbcnt), no LDS.  wave_excl's __shfl_up

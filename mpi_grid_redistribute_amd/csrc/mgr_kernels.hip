@@ -321,9 +321,10 @@ __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __re
         }
 #pragma unroll
         for (int k = 0; k < kMaxSets; ++k) {
-            if (k >= nsets) break;
-            const int t = wave_sum(c[k]);
-            if (lane == 0) counts[(int64_t)k * T + tile] = t;
+            if (k < nsets) {
+                const int t = wave_sum(c[k]);
+                if (lane == 0) counts[(int64_t)k * T + tile] = t;
+            }
         }
     }
 }

@@ -200,34 +200,60 @@ struct SelFields {
     uint8_t* dst[kSelFields][kMaxSets];
 };
 
+// Lanes without a row (past the list's end, or past cap) store to a per-wave
+// slot of this buffer, so every copy group issues exactly kSelDepth loads and
+// kSelDepth stores: the counts s_waitcnt works with stay static.
+__device__ uint4 g_sel_trash[256][64];
+
 template <int W>
 __device__ __forceinline__ void sel_copy(const uint8_t* __restrict__ src, int64_t row_bytes,
                                          uint8_t* const* dst, const long long* at,
                                          const int* start, const uint16_t* list, int fill,
-                                         int lane, long long cap) {
-    using U = typename Unit<W>::T;
+                                         int lane, long long cap, uint8_t* trash) {
+    // global address space throughout: pointers read from LDS or by readlane
+    // are generic to the compiler, and a flat access counts on lgkmcnt too, so
+    // every LDS read of the list waited for all copies in flight
+    using U = __attribute__((address_space(1))) typename Unit<W>::T;
     const int64_t upr = row_bytes / W;
-    const U* __restrict__ sp = (const U*)src;
+    const U* sp = (const U*)src;
     if (upr <= 64) {
         const int per = 64 / (int)upr;   // rows per copy instruction
         const int lr = lane / (int)upr;
         const int u = lane - lr * (int)upr;
-        for (int i0 = 0; i0 < fill; i0 += kSelDepth * per) {
-            U v[kSelDepth];
-            U* o[kSelDepth];
+        const int step = kSelDepth * per;
+        const int ng = (fill + step - 1) / step;
+        // group g: kSelDepth loads into v, targets into o (entry 0 of the
+        // list, a row of this chunk, stands in for a lane without a row)
+        auto load = [&](int g, typename Unit<W>::T (&v)[kSelDepth], U* (&o)[kSelDepth]) {
 #pragma unroll
             for (int q = 0; q < kSelDepth; ++q) {
-                const int i = i0 + q * per + lr;
+                const int i = g * step + q * per + lr;
                 const bool ok = lr < per && i < fill;
                 const unsigned e = list[ok ? i : 0];
                 const int k = (int)(e >> 10);
                 const long long row = at[k] + (i - start[k]);
-                o[q] = ok && row < cap ? (U*)dst[k] + row * upr + u : nullptr;
+                o[q] = ok && row < cap ? (U*)dst[k] + row * upr + u : (U*)trash;
                 v[q] = sp[(int64_t)(e & 1023u) * upr + u];
             }
+        };
+        auto store = [&](const typename Unit<W>::T (&v)[kSelDepth], U* const (&o)[kSelDepth]) {
 #pragma unroll
-            for (int q = 0; q < kSelDepth; ++q)
-                if (o[q]) *o[q] = v[q];
+            for (int q = 0; q < kSelDepth; ++q) *o[q] = v[q];
+        };
+        // two groups in flight: group g+1's loads are issued before group g's
+        // stores, so waiting for a group's loads never waits for the stores
+        // before it (one vmcnt counts loads and stores, retired in order)
+        typename Unit<W>::T va[kSelDepth], vb[kSelDepth];
+        U* oa[kSelDepth];
+        U* ob[kSelDepth];
+        load(0, va, oa);
+        for (int g = 0;; g += 2) {
+            load(g + 1, vb, ob);
+            store(va, oa);
+            if (g + 1 >= ng) break;
+            load(g + 2, va, oa);
+            store(vb, ob);
+            if (g + 2 >= ng) break;
         }
     } else {
         for (int i = 0; i < fill; ++i) {
@@ -256,6 +282,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
     if (tile >= T || scan_failed(scan_err)) return;
     const int64_t row0 = tile * (int64_t)tile_rows;
     const int rows = (int)min((int64_t)tile_rows, n - row0);
+    uint8_t* trash = (uint8_t*)&g_sel_trash[tile & 255][lane];
     uint16_t* list = list_s[w];
     long long* at = at_s[w];
     int* start = start_s[w];
@@ -275,6 +302,15 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
     }
     wave_sync();
     const int nbits = mask_bits(masks, nsets);
+    // Per-lane copies of what the loops index at run time (lane k: set k's
+    // mask; lane f: field f's source, row bytes, unit width), read by
+    // readlane: a kernel-argument array indexed at run time is a memory load
+    // whose s_waitcnt vmcnt(0) drained every copy and prefetch in flight --
+    // once per set and per field of every chunk.
+    const unsigned lmask = lane < nsets ? (unsigned)masks.m[lane] : 0u;
+    const unsigned long long lsrc = lane < nf ? (unsigned long long)fs.src[lane] : 0ull;
+    const long long lrb = lane < nf ? fs.row_bytes[lane] : 0;
+    const int lwl = lane < nf ? fs.wlog[lane] : 0;
     uint32_t fn[kSelWords];   // the next chunk's flags, loaded a chunk ahead
     chunk_flags(flags, row0, min(kSelChunk, rows), lane, fn);
     for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
@@ -288,14 +324,15 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
         auto flush = [&](int fill) {
             wave_sync();
             for (int f = 0; f < nf; ++f) {
-                const uint8_t* sp = fs.src[f] + (row0 + c0) * fs.row_bytes[f];
+                const long long rb = readlane64(lrb, f);
+                const uint8_t* sp = (const uint8_t*)readlane64(lsrc, f) + (row0 + c0) * rb;
                 uint8_t* const* d = dst_s[w][f];
-                switch (fs.wlog[f]) {
-                    case 4: sel_copy<16>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
-                    case 3: sel_copy<8>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
-                    case 2: sel_copy<4>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
-                    case 1: sel_copy<2>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
-                    default: sel_copy<1>(sp, fs.row_bytes[f], d, at, start, list, fill, lane, cap); break;
+                switch (__builtin_amdgcn_readlane(lwl, f)) {
+                    case 4: sel_copy<16>(sp, rb, d, at, start, list, fill, lane, cap, trash); break;
+                    case 3: sel_copy<8>(sp, rb, d, at, start, list, fill, lane, cap, trash); break;
+                    case 2: sel_copy<4>(sp, rb, d, at, start, list, fill, lane, cap, trash); break;
+                    case 1: sel_copy<2>(sp, rb, d, at, start, list, fill, lane, cap, trash); break;
+                    default: sel_copy<1>(sp, rb, d, at, start, list, fill, lane, cap, trash); break;
                 }
             }
             wave_sync();
@@ -314,7 +351,7 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
             bool full = false;
             for (; k < nsets; ++k) {
                 if (!((live >> k) & 1u)) continue;
-                uint32_t m = set_mask_t<NB>(fp, masks.m[k], nbits);
+                uint32_t m = set_mask_t<NB>(fp, (unsigned)__builtin_amdgcn_readlane((int)lmask, k), nbits);
                 if (!__ballot(m != 0u)) continue;   // an empty set costs no prefix
                 int total;
                 // bit-sliced ballot prefix (A/B: 1.122 vs 1.162 ms with the
@@ -1011,73 +1048,6 @@ __global__ __launch_bounds__(1024) void pack_ranked_kernel(
     }
 }
 
-#ifdef MGR_RANKED_HALF
-// Ranked pack in two slot halves: one 512-thread workgroup per 4096-row
-// ranked tile holds the tile's rows in registers (8 per thread) and builds
-// the image of slots [0, 2048) then [2048, 4096) in one 80 KiB LDS half, so
-// two workgroups share a CU (their load and store phases interleave) while
-// the ranked tiles -- and so the (bin, tile) runs -- stay 4096 rows long.
-template <int RB, int TR>
-__global__ __launch_bounds__(512) void pack_ranked_half_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids,
-    const uint16_t* __restrict__ ranks, const uint16_t* __restrict__ tile_starts, int nb,
-    const int64_t* __restrict__ offsets, int64_t T, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ scan_err) {
-    constexpr int NT = 512, RPT = TR / NT, NDW = RB / 4, HALF = TR / 2;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* img = (uint32_t*)smem;
-    uint16_t* ibin = (uint16_t*)(smem + align16(HALF * RB));
-    unsigned long long* gaddr = (unsigned long long*)(smem + align16(HALF * RB) + align16(HALF * 2));
-    if (scan_failed(scan_err)) return;
-    const int tid = threadIdx.x;
-    const int64_t tile = xcd_tile(blockIdx.x, T);
-    const int tr = (int)min((int64_t)TR, n - tile * TR);
-    uint32_t v[RPT][NDW];
-    unsigned b[RPT], sl[RPT];
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        const int64_t r = min(tile * TR + q * NT + tid, n - 1);
-        b[q] = min((unsigned)ids[r], (unsigned)(nb - 1));
-        sl[q] = q * NT + tid < tr ? (unsigned)ranks[r] : 0xFFFFu;
-        load_row_dw<NDW>(src + r * RB, v[q]);
-    }
-    for (int bb = tid; bb < nb; bb += NT)
-        gaddr[bb] = (unsigned long long)(dst + (offsets[(int64_t)bb * T + tile] -
-                                                (long long)tile_starts[tile * nb + bb]) * (long long)RB);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int lo = h * HALF, hi = min(tr, lo + HALF);
-        if (lo >= tr) break;
-        __syncthreads();   // gaddr written; the previous half's image stored
-#pragma unroll
-        for (int q = 0; q < RPT; ++q) {
-            const int ls = (int)sl[q] - lo;
-            if (ls >= 0 && ls < HALF) {
-#pragma unroll
-                for (int i = 0; i < NDW; ++i) img[ls * NDW + i] = v[q][i];
-                ibin[ls] = (uint16_t)b[q];
-            }
-        }
-        __syncthreads();
-        const int nbytes = (hi - lo) * RB;
-        const unsigned long long xo = (unsigned long long)lo * RB;
-        for (int x = 16 * tid; x < nbytes; x += 16 * NT) {
-            const u32x4_t qv = *(const u32x4_t*)((const uint8_t*)img + x);
-            const int bf = ibin[x / RB];
-            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
-                gstore<u32x4_a4>(gaddr[bf] + xo + x, qv);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xo + xd, qv[d]);
-                }
-            }
-        }
-    }
-}
-#endif
-
 // LDS of the ranked pack: the tile image, its row bins and per-bin output
 // addresses.
 static int ranked_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
@@ -1104,19 +1074,6 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if (lds > 160 * 1024) return hipErrorNotSupported;
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
-#ifdef MGR_RANKED_HALF
-    if (tile_rows == 4096 && nbins <= 1024 && row_bytes == 36) {
-        const int hl = align16(2048 * 36) + align16(2048 * 2) + nbins * 8;
-        auto k = pack_ranked_half_kernel<36, 4096>;
-        ensure_lds(k, hl);
-        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(512), (size_t)hl, s, (const uint8_t*)src,
-                           n, ids, ranks, tile_starts, nbins, ws.offsets, ws.T, (uint8_t*)dst,
-                           ws.scan_err);
-        e = hipGetLastError();
-        prof_end(s, K_PACK_FINE);
-        return e;
-    }
-#endif
     int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;

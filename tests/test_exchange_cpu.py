@@ -406,3 +406,16 @@ def test_count_skew_hand_built():
     assert count_skew(np.zeros((2, 3), dtype=np.int64))["recv_max_over_mean"] is None
     with pytest.raises(ValueError):
         count_skew([[1, -1]])                     # a failed scan's -1 counts
+
+
+def test_bench_xgmi_report_names_its_path():
+    """bench.py's xGMI figures say which exchange produced them."""
+    import bench
+    traffic = {"send_bytes": 1e9, "recv_bytes": 2e9, "send_peers": 2, "recv_peers": 1}
+    exch = {"avg_ms": 1.0, "launches": 4, "steps": 2}   # 2 ms of RCCL groups per step
+    r = bench.xgmi_report(traffic, exch, None, 1, 4)
+    assert r["path"].startswith("pipelined, 4 chunks")
+    assert r["ms_per_step"] == 2.0
+    assert abs(r["send"]["achieved"] - 500.0) < 1e-9 and r["send"]["peers"] == 2
+    assert abs(r["recv"]["achieved"] - 1000.0) < 1e-9
+    assert bench.xgmi_report(traffic, exch, None, 1, 1)["path"].startswith("one message")
