@@ -362,3 +362,23 @@ def test_halo_one_rank_vs_oracle(case):
     want = pos_o[(out - 1) // 3]
     assert np.array_equal(np.asarray(opos).view(np.uint8), want.view(np.uint8))
     assert np.array_equal(np.asarray(p).view(np.uint8), pos_o.view(np.uint8))   # wrapped in place
+
+
+@pytest.mark.parametrize("dim,rec", [(1, 8), (2, 36), (3, 7), (3, 100)])
+def test_one_rank_halo_dims_vs_oracle(dim, rec):
+    """One rank in 1, 2 and 3 dimensions with odd and wide records (the
+    selection pack's byte, 4-byte and row-by-row copies), against the oracle,
+    positions returned."""
+    rng = np.random.default_rng(dim * 100 + rec)
+    n = 150_001
+    topo, box = [1] * dim, [1.0] * dim
+    ol = [0.05, 0.11, 0.07][:dim]
+    pos = rng.uniform(-0.3, 1.3, (n, dim))
+    data = rng.integers(0, 256, (n, rec), dtype=np.uint8)
+    pos_o = pos.copy()
+    exp = ro.redistribute_by_position_overload_all_ranks(topo, box, 1, [data], [pos_o], ol)[0]
+    R = MPIGridRedistributor(None, topo, box)
+    out, opos = R.redistribute_by_position(data, pos, overload_lengths=ol, return_positions=True)
+    assert G.same_bytes(out, exp)
+    assert G.same_bytes(pos, pos_o)
+    assert len(opos) == len(out)
