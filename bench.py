@@ -49,7 +49,7 @@ N_CFG5_PER_GPU = 512_000_000 // 8    # config 5: 512M over 8 GPUs
 
 # Algorithmic bytes per row of one launch (DESIGN.md §4 Measurement): what
 # the kernel must read and write at least, per row it processes.
-def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512):
+def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1):
     if cfg == 5:
         ts = 2.0 * fine_bins / fine_tile_rows        # u16 tile starts per row
         return {
@@ -59,9 +59,12 @@ def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512):
             "pack_fine": 2 + 2 + ts + 36 + 36,   # mgr_pack_ranked: ids, ranks, starts, record
         }
     if halo:
+        # one rank keeps its rows in order: the selections read the binning's
+        # flags in place, no flag field travels with the pack
+        fl = 2 + 2 if world > 1 else 0
         return {
             "bin_count": 24 + 24 + 1 + 2,    # positions in + wrapped out, dest, face flags
-            "pack": 1 + 32 + 2 + 32 + 2,     # dest, record + flags in, record + flags out
+            "pack": 1 + 32 + 32 + fl,        # dest, record in + out (+ flags in + out)
         }
     return {
         "bin_count": 24 + 24 + 1,            # read pos, write wrapped pos, write dest
@@ -410,7 +413,7 @@ def main():
     # rows -- received rows at N > 1 are ~n for the uniform inputs), or the
     # host-counted bytes of the halo's selections
     fine_tr = int(_lib.load().mgr_ranked_tile_rows(36, 512)) if cfg == 5 else 2048
-    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr).items():
+    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world).items():
         if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
             kernels[k]["alg_bytes_per_launch"] = b * n
     for k, e in kernels.items():

@@ -419,3 +419,12 @@ def test_bench_xgmi_report_names_its_path():
     assert abs(r["send"]["achieved"] - 500.0) < 1e-9 and r["send"]["peers"] == 2
     assert abs(r["recv"]["achieved"] - 1000.0) < 1e-9
     assert bench.xgmi_report(traffic, exch, None, 1, 1)["path"].startswith("one message")
+
+
+def test_bench_halo_pack_bytes_by_world():
+    """The halo line's pack carries the 2-byte flag field only between ranks
+    (one rank reads the binning's flags in place)."""
+    import bench
+    assert bench.row_bytes_per_kernel(3, True, world=1)["pack"] == 65
+    assert bench.row_bytes_per_kernel(3, True, world=2)["pack"] == 69
+    assert bench.row_bytes_per_kernel(3, False)["pack"] == 65
