@@ -44,11 +44,12 @@ def main():
         if os.path.exists(bj):
             bench = (json.load(open(bj)) or {}).get("kernels", {})
         for k, c in sorted(d.items()):
-            if "SQ_WAVE_CYCLES" not in c or c.get("SQ_WAVES", 0) < 1:
-                continue
+            if "SQ_WAVE_CYCLES" not in c or c.get("SQ_WAVES", 0) < 1 or k not in NAMES:
+                continue   # this library's kernels only (not the input generators, torch, RCCL)
             wc = c["SQ_WAVE_CYCLES"]
             rd, wr = c.get("SQ_INSTS_VMEM_RD", 0.0), c.get("SQ_INSTS_VMEM_WR", 0.0)
-            alg = bench.get(NAMES.get(k, ""), {}).get("alg_bytes_per_launch")
+            name = "bin_fine" if (line, k) == ("cfg5", "bin_count_kernel") else NAMES.get(k, "")
+            alg = bench.get(name, {}).get("alg_bytes_per_launch")
             bpi = f"{alg / (rd + wr):.0f}" if alg and rd + wr else "--"
             lds = c.get("SQ_ACTIVE_INST_LDS", 0.0)
             conf = f"{c.get('SQ_LDS_BANK_CONFLICT', 0.0) / lds:.2f}" if lds else "--"
