@@ -216,12 +216,28 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
     const bool failed = s_poison != 0;
     const long long total = s_excl + agg;
     if (bin_counts) {
+        // Every bin's total from the inclusive words at the bin ends.  Each
+        // chunk counted itself done AFTER storing its word, but relaxed
+        // atomics on two locations are not ordered for another reader: the
+        // done count can be seen before the word.  So the words are polled
+        // (bounded, like every look-back) rather than read once -- one look
+        // could read a bin end's aggregate as its prefix (a wrong count).
         for (int bb = threadIdx.x; bb < nbins; bb += kBlock) {
-            const long long st = bb == 0 ? 0 : (long long)(flag_poll(&flags[bb * cpb - 1], 2, 0) & kScanVal);
-            const long long en = bb == nbins - 1
-                                     ? total
-                                     : (long long)(flag_poll(&flags[(bb + 1) * cpb - 1], 2, 0) & kScanVal);
-            bin_counts[bb] = failed ? -1 : en - st;
+            bool bad = failed;
+            long long st = 0, en = total;
+            if (bb > 0) {
+                const uint64_t w = flag_poll(&flags[bb * cpb - 1], 2, spins);
+                st = (long long)(w & kScanVal);
+                bad |= (w & kScanPoison) != 0;
+            }
+            if (bb < nbins - 1) {
+                const uint64_t w = flag_poll(&flags[(bb + 1) * cpb - 1], 2, spins);
+                en = (long long)(w & kScanVal);
+                bad |= (w & kScanPoison) != 0;
+            }
+            if (bad && !failed)
+                __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bin_counts[bb] = bad ? -1 : en - st;
         }
     }
     if (threadIdx.x == 0) bin_starts[nbins] = failed ? -1 : total;
