@@ -184,14 +184,15 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
 // masks and a wave prefix list the set's rows in row order in LDS (u16 entry:
 // chunk row | set << 10), the sets one after the other; then one copy loop
 // per field moves every listed row -- 64 / upr rows per instruction, W-byte
-// units (the widest the field's alignment allows), four instructions in
-// flight -- to its set's next output row.  A single chain of loads per chunk
-// and few registers keep enough waves and bytes in flight for a sparse
-// gather.  Rows wider than 64 units are copied one after the other, lanes
-// across the row.
+// units (the widest the field's alignment allows), groups of kSelDepth
+// instructions, two groups in flight -- to its set's next output row.  Rows
+// wider than 64 units are copied one after the other, lanes across the row.
+// The gathers read whole lines for sparse rows (PMC: 3.3 GB read for 1.3 GB
+// of rows at the halo's density), so the kernel runs near the HBM rate of
+// the lines it must touch (profiles/round4/ab_notes.md).
 constexpr int kSelCap = 2048;   // LDS entries per wave (>= kSelChunk)
 static_assert(kSelCap >= kSelChunk, "a set of one chunk must fit an empty list");
-constexpr int kSelDepth = 4;    // copy instructions in flight per field (8: 1.17 vs 1.10 ms)
+constexpr int kSelDepth = 4;    // copy instructions per group (round 3: 8 in flight, 1.17 vs 1.10 ms)
 constexpr int kSelFields = 3;
 struct SelFields {
     const uint8_t* src[kSelFields];
