@@ -43,11 +43,23 @@ typedef enum {
     MGR_EUNSUPPORTED = -4 /* valid request this build does not implement   */
 } mgr_status;
 
+/* Element types.  Positions: MGR_F16, MGR_F32, MGR_F64, MGR_I32, MGR_I64
+ * (the reference bins any numpy column, redist.py:68-69).  box_length: any
+ * of these and the narrower integers below (numpy's promotion of
+ * position % box and position / box depends on the box's dtype, S9/S11a).
+ * rank ids: MGR_F32, MGR_F64, MGR_I32, MGR_I64.                           */
 typedef enum {
     MGR_F32 = 1,
     MGR_F64 = 2,
     MGR_I32 = 3,
-    MGR_I64 = 4
+    MGR_I64 = 4,
+    MGR_F16 = 5,
+    MGR_I8 = 6,
+    MGR_I16 = 7,
+    MGR_U8 = 8,   /* also numpy bool (same promotions against positions)  */
+    MGR_U16 = 9,
+    MGR_U32 = 10,
+    MGR_U64 = 11
 } mgr_dtype;
 
 typedef struct mgr_plan mgr_plan; /* grid geometry of one rank            */
@@ -59,9 +71,14 @@ const char* mgr_version(void);
 /* ---------------------------------------------------------------- plan --
  * Replaces MPIGridRedistributor.__init__ (redist.py:16-61): row-major cell
  * offsets (redist.py:53-58), the box and topology.  box_dtype is the numpy
- * dtype of the caller's box_length (redist.py:46): with float32 positions a
- * float32 box makes the wrap and the quotient float32 (numpy promotion), any
- * other combination computes in float64 (S9, S11a).  nbins = number of
+ * dtype of the caller's box_length (redist.py:46); with the positions' dtype
+ * it decides, as numpy 2.2.6's promotion does, the type the wrap
+ * (position % box) and the quotient (position / box) compute in: e.g.
+ * float32 positions with a float32 / float16 / int8 / int16 box compute in
+ * float32, with a float64 / int32 / int64 box in float64 (S9, S11a); integer
+ * positions with an integer box wrap in integer arithmetic.  Integer box
+ * lengths are passed as doubles and must be integral with |L| < 2^53.
+ * nbins = number of
  * destinations = comm size (redist.py:42, :196); cells >= nbins are invalid
  * (redist.py:43-44 asserts prod(topology) <= size).                        */
 int mgr_plan_create(int dim, const int64_t* grid_topology, const double* box_length,
@@ -103,7 +120,11 @@ int mgr_dest_bytes(int nbins);
  *      wrap of every index and the row-major dot.
  * Bit-exact with numpy 2.2.6 (NaN/out-of-range bins
  * like x86's INT64_MIN).  pos: n rows, row r coordinate d at
- * pos[r*row_stride + d] (elements), dtype MGR_F32 or MGR_F64.
+ * pos[r*row_stride + d] (elements), dtype MGR_F16, MGR_F32, MGR_F64,
+ * MGR_I32 or MGR_I64.  Integer and float16 positions follow numpy's
+ * promotion (see mgr_plan_create): the wrap is computed in the promoted type
+ * and cast back on the in-place write-back (float -> int by x86 truncation,
+ * -> float16 rounded to nearest even), the bin reads the stored value back.
  *
  * mgr_bin_count : writes dest[r] (mgr_dest_bytes(nbins) wide) and the per
  *                 tile histogram into the workspace; feeds mgr_scan.

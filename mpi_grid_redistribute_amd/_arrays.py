@@ -16,7 +16,14 @@ import torch
 
 from . import _lib
 
-_POS_CODES = {torch.float32: _lib.MGR_F32, torch.float64: _lib.MGR_F64}
+# position dtypes the binning kernels take (redist.py:68-69 bins any numpy
+# column; these are the ones with a kernel, everything else is refused)
+_POS_CODES = {torch.float16: _lib.MGR_F16, torch.float32: _lib.MGR_F32,
+              torch.float64: _lib.MGR_F64, torch.int32: _lib.MGR_I32, torch.int64: _lib.MGR_I64}
+_NP_POS_CODES = {np.dtype(np.float16): _lib.MGR_F16, np.dtype(np.float32): _lib.MGR_F32,
+                 np.dtype(np.float64): _lib.MGR_F64, np.dtype(np.int32): _lib.MGR_I32,
+                 np.dtype(np.int64): _lib.MGR_I64}
+_POS_NAMES = "float16/float32/float64/int32/int64"
 _ID_CODES = {torch.int32: _lib.MGR_I32, torch.int64: _lib.MGR_I64, torch.float32: _lib.MGR_F32,
              torch.float64: _lib.MGR_F64}
 
@@ -95,7 +102,7 @@ class Positions:
             if obj.dim() != 2 or obj.shape[1] < dim:
                 raise ValueError(f"position must be (N, >= {dim}), got {tuple(obj.shape)}")
             if obj.dtype not in _POS_CODES:
-                raise TypeError(f"position dtype {obj.dtype} not supported (float32/float64)")
+                raise TypeError(f"position dtype {obj.dtype} not supported ({_POS_NAMES})")
             t = obj
             if not t.is_cuda or t.stride(1) != 1 or t.stride(0) < dim:
                 t = obj.to(dev).contiguous()
@@ -111,10 +118,10 @@ class Positions:
             raise TypeError("position must be a numpy array or a torch tensor")
         if a.ndim != 2 or a.shape[1] < dim:
             raise ValueError(f"position must be (N, >= {dim}), got {a.shape}")
-        if a.dtype not in (np.float32, np.float64):
-            raise TypeError(f"position dtype {a.dtype} not supported (float32/float64)")
+        if a.dtype not in _NP_POS_CODES:
+            raise TypeError(f"position dtype {a.dtype} not supported ({_POS_NAMES})")
         self.n = int(a.shape[0])
-        self.code = _lib.MGR_F32 if a.dtype == np.float32 else _lib.MGR_F64
+        self.code = _NP_POS_CODES[a.dtype]
         isz = a.dtype.itemsize
         if (data_rows is not None and data_rows.kind == "numpy" and self.n
                 and np.shares_memory(a, data_rows.host)):
@@ -161,10 +168,28 @@ def id_array(obj, dev):
     return t, _ID_CODES[t.dtype]
 
 
+def pos_code(dtype):
+    """mgr_dtype code of a position dtype (numpy or torch), or TypeError."""
+    code = _POS_CODES.get(dtype) if isinstance(dtype, torch.dtype) else _NP_POS_CODES.get(
+        np.dtype(dtype))
+    if code is None:
+        raise TypeError(f"position dtype {dtype} not supported ({_POS_NAMES})")
+    return code
+
+
+_BOX_CODES = {"f2": _lib.MGR_F16, "f4": _lib.MGR_F32, "f8": _lib.MGR_F64, "i1": _lib.MGR_I8,
+              "i2": _lib.MGR_I16, "i4": _lib.MGR_I32, "i8": _lib.MGR_I64, "u1": _lib.MGR_U8,
+              "b1": _lib.MGR_U8, "u2": _lib.MGR_U16, "u4": _lib.MGR_U32, "u8": _lib.MGR_U64}
+
+
 def box_dtype_code(box: np.ndarray):
-    """numpy dtype of box_length -> how numpy promotes the position math (S9, S11a)."""
-    if box.dtype in (np.float16, np.float32):
-        return _lib.MGR_F32
-    if np.issubdtype(box.dtype, np.floating):
-        return _lib.MGR_F64
-    return _lib.MGR_I64
+    """numpy dtype of box_length (redist.py:46 keeps the caller's) -> mgr_dtype:
+    with the positions' dtype it decides how numpy promotes the wrap and the
+    quotient (S9, S11a; mgr_capi.hip promote).  bool promotes like uint8."""
+    code = _BOX_CODES.get(box.dtype.kind + str(box.dtype.itemsize))
+    if code is None:
+        raise TypeError(f"box_length dtype {box.dtype} not supported (float16/32/64, "
+                        "(u)int8-64, bool)")
+    if box.dtype.kind in "iub" and box.size and np.abs(box.astype(np.float64)).max() >= 2.0 ** 53:
+        raise NotImplementedError("integer box lengths of 2^53 or more")
+    return code

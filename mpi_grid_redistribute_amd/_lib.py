@@ -19,6 +19,9 @@ LIB_PATH = os.path.join(_HERE, "libmgr.so")
 
 MGR_OK = 0
 MGR_F32, MGR_F64, MGR_I32, MGR_I64 = 1, 2, 3, 4
+MGR_F16, MGR_I8, MGR_I16, MGR_U8, MGR_U16, MGR_U32, MGR_U64 = 5, 6, 7, 8, 9, 10, 11
+# element bytes of the position dtypes (mgr_bin_count & co.)
+POS_ITEMSIZE = {MGR_F16: 2, MGR_F32: 4, MGR_F64: 8, MGR_I32: 4, MGR_I64: 8}
 UNIQUE_ID_BYTES = 128
 
 _P = ctypes.c_void_p
@@ -173,7 +176,8 @@ def test_hook(key, value):
 
 HOOK_DEFAULTS = {"tile_rounds": 0, "scan_chunk": 2048, "scan_max_chunks": 1024,
                  "scan_spins": 1 << 24, "pack_img_all": 0, "rank_rows": 0, "bin_unstaged": 0,
-                 "bin_generic": 0, "pack_generic": 0}
+                 "bin_generic": 0, "pack_generic": 0, "scan_delay_bin": -1,
+                 "scan_delay_sleeps": 0, "scan_end_spins": -1}
 
 
 # --------------------------------------------------------------- profiler

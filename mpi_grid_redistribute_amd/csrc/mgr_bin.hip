@@ -358,15 +358,41 @@ static hipError_t bin_count_d(const Geom& g, void* pos, int64_t n, int64_t strid
     return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fo);
 }
 
-hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+// int32 / int64 / float16 positions (bin_coord_ext): each lane reads its own
+// row (no slab staging: float16 rows need not be 4-byte multiples), run-time
+// dimensionality -- the general path of every plan.
+template <typename PosT, typename DestT>
+static hipError_t bin_count_ext(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
+                                void* dest, int tile_rows, const Workspace& ws, hipStream_t s,
+                                const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
+    return periodic ? bin_count_t<PosT, true, DestT, 0, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo)
+                    : bin_count_t<PosT, false, DestT, 0, 0>(g, pos, n, stride, dest, tile_rows, ws, s, fg, hg, fo);
+}
+template <typename PosT>
+static hipError_t bin_count_ext_d(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
+                                  void* dest, int tile_rows, const Workspace& ws, hipStream_t s,
+                                  const FineGeom* fg, const HaloGeom* hg, uint16_t* fo) {
+    if (dest_bytes(g.nbins) == 1)
+        return bin_count_ext<PosT, uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fo);
+    return bin_count_ext<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fo);
+}
+
+hipError_t launch_bin_count(const Geom& g, void* pos, int pos_dtype, int64_t n, int64_t stride,
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
                             hipStream_t s, const FineGeom* fg, uint16_t* fine_out,
                             const HaloGeom* hg) {
     if (n <= 0) return hipSuccess;
     const int kid = fg ? K_BIN_FINE : K_BIN_COUNT;
     prof_begin(s, kid);
-    hipError_t e = pos_f32 ? bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out)
-                           : bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out);
+    hipError_t e;
+    switch (pos_dtype) {
+        case MGR_F32: e = bin_count_d<float>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_F64: e = bin_count_d<double>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_I32: e = bin_count_ext_d<int32_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_I64: e = bin_count_ext_d<int64_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_F16: e = bin_count_ext_d<f16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        default: e = hipErrorInvalidValue;
+    }
     prof_end(s, kid);
     return e;
 }
@@ -572,12 +598,19 @@ static hipError_t cell_ids_t(const Geom& g, void* pos, int64_t n, int64_t stride
     return hipGetLastError();
 }
 
-hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_dtype, int64_t n, int64_t stride,
                            int periodic, int64_t* cell, int64_t* idx, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     prof_begin(s, K_CELL_IDS);
-    hipError_t e = pos_f32 ? cell_ids_t<float>(g, pos, n, stride, periodic, cell, idx, s)
-                           : cell_ids_t<double>(g, pos, n, stride, periodic, cell, idx, s);
+    hipError_t e;
+    switch (pos_dtype) {
+        case MGR_F32: e = cell_ids_t<float>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_F64: e = cell_ids_t<double>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_I32: e = cell_ids_t<int32_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_I64: e = cell_ids_t<int64_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_F16: e = cell_ids_t<f16_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        default: e = hipErrorInvalidValue;
+    }
     prof_end(s, K_CELL_IDS);
     return e;
 }

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <string>
@@ -129,16 +130,82 @@ extern "C" {
 const char* mgr_last_error(void) { return g_err.c_str(); }
 const char* mgr_version(void) { return MGR_VERSION_STRING; }
 
+// numpy 2.2.6 dtype promotion (NEP 50, array with a numpy scalar of the box
+// dtype: both strongly typed) over the element types of mgr_dtype.
+struct Kind {
+    char k;   // 'f', 'i', 'u'
+    int bytes;
+};
+static bool dtype_kind(int t, Kind* out) {
+    switch (t) {
+        case MGR_F16: *out = {'f', 2}; return true;
+        case MGR_F32: *out = {'f', 4}; return true;
+        case MGR_F64: *out = {'f', 8}; return true;
+        case MGR_I8: *out = {'i', 1}; return true;
+        case MGR_I16: *out = {'i', 2}; return true;
+        case MGR_I32: *out = {'i', 4}; return true;
+        case MGR_I64: *out = {'i', 8}; return true;
+        case MGR_U8: *out = {'u', 1}; return true;
+        case MGR_U16: *out = {'u', 2}; return true;
+        case MGR_U32: *out = {'u', 4}; return true;
+        case MGR_U64: *out = {'u', 8}; return true;
+        default: return false;
+    }
+}
+static int dtype_of(Kind k) {
+    if (k.k == 'f') return k.bytes == 2 ? MGR_F16 : k.bytes == 4 ? MGR_F32 : MGR_F64;
+    if (k.k == 'i') return k.bytes == 1 ? MGR_I8 : k.bytes == 2 ? MGR_I16 : k.bytes == 4 ? MGR_I32 : MGR_I64;
+    return k.bytes == 1 ? MGR_U8 : k.bytes == 2 ? MGR_U16 : k.bytes == 4 ? MGR_U32 : MGR_U64;
+}
+// numpy's result type of a op b for two of these element types.
+static int promote(int a, int b) {
+    Kind x, y;
+    if (!dtype_kind(a, &x) || !dtype_kind(b, &y)) return 0;
+    if (x.k == 'f' || y.k == 'f') {
+        // an integer joins a float as the smallest float holding it exactly
+        // (8-bit -> float16, 16-bit -> float32, wider -> float64)
+        auto fw = [](Kind q) { return q.k == 'f' ? q.bytes : q.bytes == 1 ? 2 : q.bytes == 2 ? 4 : 8; };
+        return dtype_of({'f', std::max(fw(x), fw(y))});
+    }
+    if (x.k == y.k) return dtype_of({x.k, std::max(x.bytes, y.bytes)});
+    const Kind s = x.k == 'i' ? x : y, u = x.k == 'i' ? y : x;   // signed, unsigned
+    if (s.bytes > u.bytes) return dtype_of(s);
+    if (u.bytes < 8) return dtype_of({'i', 2 * u.bytes});
+    return MGR_F64;   // int64 with uint64
+}
+static bool is_pos_dtype(int t) {
+    return t == MGR_F16 || t == MGR_F32 || t == MGR_F64 || t == MGR_I32 || t == MGR_I64;
+}
+
+// The per-call modes of a plan's geometry for positions of pos_dtype: the
+// type of position % box (wmode) and of position / box (dmode: true
+// division, float64 for two integers); compute_f32 = the float32 positions'
+// path computes both in float32.
+static void pos_modes(mgr::Geom& g, int pos_dtype) {
+    g.wmode = promote(pos_dtype, g.box_dtype);
+    Kind w;
+    dtype_kind(g.wmode, &w);
+    g.dmode = w.k == 'f' ? g.wmode : MGR_F64;
+    g.compute_f32 = pos_dtype == MGR_F32 && g.wmode == MGR_F32;
+}
+
 // Box geometry of a plan: L, 2L, fast-wrap and exact power-of-two division
-// flags per dimension, and the per-dimension cell counts n[d].
+// flags per dimension, integer lengths of an integer box, and the
+// per-dimension cell counts n[d].
 static int fill_box(mgr::Geom& g, int dim, const int64_t* n, const double* box, int box_dtype) {
-    if (box_dtype != MGR_F32 && box_dtype != MGR_F64 && box_dtype != MGR_I64 && box_dtype != MGR_I32)
-        return fail(MGR_EINVAL, "box_dtype %d", box_dtype);
+    Kind bk;
+    if (!dtype_kind(box_dtype, &bk)) return fail(MGR_EINVAL, "box_dtype %d", box_dtype);
     g.dim = dim;
-    g.compute_f32 = box_dtype == MGR_F32;
+    g.box_dtype = box_dtype;
+    pos_modes(g, MGR_F64);   // per call: pos_modes for the positions' dtype
     for (int d = 0; d < dim; ++d) {
         if (n[d] < 1) return fail(MGR_EINVAL, "grid_topology[%d] = %lld < 1", d, (long long)n[d]);
         const double L = box[d];
+        if (bk.k != 'f') {
+            if (!(L == floor(L) && fabs(L) < 9007199254740992.0))
+                return fail(MGR_EINVAL, "integer box_length[%d] = %g: not an integer below 2^53", d, L);
+            g.Li[d] = (int64_t)L;
+        }
         g.L[d] = L;
         g.twoL[d] = L + L;
         g.fast[d] = (L > 0.0) && isfinite(L + L);
@@ -259,8 +326,8 @@ static int check_tile(int tile_rows) {
 
 static int check_pos(const mgr_plan* plan, const void* pos, int dtype, int64_t n, int64_t stride) {
     if (!plan) return fail(MGR_EINVAL, "null plan");
-    if (dtype != MGR_F32 && dtype != MGR_F64)
-        return fail(MGR_EINVAL, "positions must be float32 or float64 (dtype %d)", dtype);
+    if (!is_pos_dtype(dtype))
+        return fail(MGR_EINVAL, "positions must be float16/32/64 or int32/64 (dtype %d)", dtype);
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (n > 0 && !pos) return fail(MGR_EINVAL, "null positions");
     if (stride < plan->g.dim) return fail(MGR_EINVAL, "row_stride %lld < dim %d", (long long)stride, plan->g.dim);
@@ -274,9 +341,9 @@ int mgr_bin_count(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int
     if ((rc = check_tile(tile_rows))) return rc;
     if (n > 0 && (!dest || !workspace)) return fail(MGR_EINVAL, "null dest/workspace");
     mgr::Geom g = plan->g;
-    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    pos_modes(g, pos_dtype);
     const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
-    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
+    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype, n, row_stride, periodic, dest,
                                  tile_rows, ws, (hipStream_t)stream));
     return MGR_OK;
 }
@@ -292,11 +359,11 @@ int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* po
     for (int d = 0; d < plan->g.dim; ++d)
         if (memcmp(&fine_plan->g.L[d], &plan->g.L[d], sizeof(double)) ||
             fine_plan->g.n[d] != plan->g.n[d] * fine_plan->g.fmod[d] ||
-            fine_plan->g.compute_f32 != plan->g.compute_f32)
+            fine_plan->g.box_dtype != plan->g.box_dtype)
             return fail(MGR_EINVAL, "fine_plan is not over this plan's box and topology (dim %d)", d);
     if (n > 0 && (!dest || !workspace || !fine_ids)) return fail(MGR_EINVAL, "null dest/fine_ids/workspace");
     mgr::Geom g = plan->g;
-    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    pos_modes(g, pos_dtype);
     mgr::FineGeom fg;
     memset(&fg, 0, sizeof fg);
     for (int d = 0; d < g.dim; ++d) {
@@ -308,7 +375,7 @@ int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* po
     fg.nbins = fine_plan->g.nbins;
     if (!fine_plan->g.fast32) g.fast32 = 0;   // the fine indexes must fit 32 bits too
     const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
-    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
+    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype, n, row_stride, periodic, dest,
                                  tile_rows, ws, (hipStream_t)stream, &fg, fine_ids));
     return MGR_OK;
 }
@@ -324,7 +391,7 @@ int mgr_bin_count_halo(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n
     if (!cell_length || !overload_lengths) return fail(MGR_EINVAL, "null cell/overload lengths");
     if (n > 0 && (!dest || !workspace || !flags)) return fail(MGR_EINVAL, "null dest/flags/workspace");
     mgr::Geom g = plan->g;
-    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
+    pos_modes(g, pos_dtype);
     mgr::HaloGeom hg;
     memset(&hg, 0, sizeof hg);
     for (int d = 0; d < g.dim; ++d) {
@@ -332,7 +399,7 @@ int mgr_bin_count_halo(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n
         hg.ol[d] = overload_lengths[d];
     }
     const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
-    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, dest,
+    HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype, n, row_stride, periodic, dest,
                                  tile_rows, ws, (hipStream_t)stream, nullptr, flags, &hg));
     return MGR_OK;
 }
@@ -454,8 +521,8 @@ int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int6
     int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
     if (rc) return rc;
     mgr::Geom g = plan->g;
-    if (pos_dtype == MGR_F64) g.compute_f32 = 0;
-    HIP_OK(mgr::launch_cell_ids(g, pos, pos_dtype == MGR_F32, n, row_stride, periodic, cell_out,
+    pos_modes(g, pos_dtype);
+    HIP_OK(mgr::launch_cell_ids(g, pos, pos_dtype, n, row_stride, periodic, cell_out,
                                 idx_out, (hipStream_t)stream));
     return MGR_OK;
 }
@@ -593,14 +660,14 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
 // ------------------------------------------------------ halo (f1)
 int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
                    const double* hi, const double* lo, uint16_t* flags, void* stream) {
-    if (pos_dtype != MGR_F32 && pos_dtype != MGR_F64)
-        return fail(MGR_EINVAL, "positions must be float32 or float64 (dtype %d)", pos_dtype);
+    if (!is_pos_dtype(pos_dtype))
+        return fail(MGR_EINVAL, "positions must be float16/32/64 or int32/64 (dtype %d)", pos_dtype);
     if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d", dim);
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (row_stride < dim) return fail(MGR_EINVAL, "row_stride %lld < dim %d", (long long)row_stride, dim);
     if (!hi || !lo) return fail(MGR_EINVAL, "null thresholds");
     if (n > 0 && (!pos || !flags)) return fail(MGR_EINVAL, "null argument");
-    HIP_OK(mgr::launch_halo_flags(pos, pos_dtype == MGR_F32, n, row_stride, dim, hi, lo, flags,
+    HIP_OK(mgr::launch_halo_flags(pos, pos_dtype, n, row_stride, dim, hi, lo, flags,
                                   (hipStream_t)stream));
     return MGR_OK;
 }

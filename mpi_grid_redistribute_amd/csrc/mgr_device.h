@@ -129,9 +129,94 @@ __device__ __forceinline__ long long floormod_i64(long long a, long long n) {
     return r;
 }
 
+// ---- float16 positions: numpy 2.2.6's software half conversions (its
+// half.hpp, restated): round to nearest even, overflow to inf, subnormals
+// kept; a NaN keeps its sign and shifted payload and is NEVER quieted (a
+// payload that would shift out becomes 1, so it stays a NaN).  numpy's half
+// arithmetic is the float32 operation rounded back (checked against numpy on
+// 2M random bit patterns, NaNs included).  Bit manipulation only: nothing
+// depends on the GPU's own half conversion or denormal modes.
+struct f16_t {
+    uint16_t u;
+};
+
+__device__ __forceinline__ float h2f(uint16_t h) {
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    if (e == 0x1fu) return __uint_as_float(s | 0x7f800000u | (m << 13));
+    if (e == 0) return __uint_as_float(s | __float_as_uint((float)m * 0x1p-24f));   // exact
+    return __uint_as_float(s | ((e + 112u) << 23) | (m << 13));
+}
+__device__ __forceinline__ double h2d(uint16_t h) {
+    if (((h >> 10) & 0x1fu) == 0x1fu)
+        return __longlong_as_double((long long)(((unsigned long long)(h & 0x8000u) << 48) |
+                                                0x7ff0000000000000ull |
+                                                ((unsigned long long)(h & 0x3ffu) << 42)));
+    return (double)h2f(h);   // exact
+}
+// Round the magnitude `mag` (an integer in units of 2^-shift half-ulps) to
+// nearest even: the kept bits r = mag >> shift, ties by the low bit of r.
+template <typename U>
+__device__ __forceinline__ uint32_t rne_shift(U mag, int shift) {
+    const U r = mag >> shift, rem = mag & (((U)1 << shift) - 1), half = (U)1 << (shift - 1);
+    return (uint32_t)(r + ((rem > half || (rem == half && (r & 1))) ? 1 : 0));
+}
+__device__ __forceinline__ uint16_t f2h(float x) {
+    const uint32_t f = __float_as_uint(x), s = (f >> 16) & 0x8000u, a = f & 0x7fffffffu;
+    if (a >= 0x7f800000u) {   // inf / NaN
+        if (a == 0x7f800000u) return (uint16_t)(s | 0x7c00u);
+        uint32_t r = 0x7c00u + ((a & 0x7fffffu) >> 13);
+        if (r == 0x7c00u) ++r;
+        return (uint16_t)(s | r);
+    }
+    if (a >= 0x477ff000u) return (uint16_t)(s | 0x7c00u);          // >= 65520: inf
+    if (a >= 0x38800000u) return (uint16_t)(s | rne_shift<uint32_t>(a - 0x38000000u, 13));  // normal
+    if (a < 0x33000000u) return (uint16_t)s;                        // <= 2^-25 (tie to 0) and below
+    const int e = (int)(a >> 23);                                   // subnormal half: units of 2^-24
+    return (uint16_t)(s | rne_shift<uint32_t>((a & 0x7fffffu) | 0x800000u, 126 - e));
+}
+__device__ __forceinline__ uint16_t d2h(double x) {   // direct, no double rounding via float
+    const unsigned long long d = (unsigned long long)__double_as_longlong(x);
+    const uint32_t s = (uint32_t)(d >> 48) & 0x8000u;
+    const unsigned long long a = d & 0x7fffffffffffffffull;
+    if (a >= 0x7ff0000000000000ull) {
+        if (a == 0x7ff0000000000000ull) return (uint16_t)(s | 0x7c00u);
+        uint32_t r = 0x7c00u + (uint32_t)((a & 0xfffffffffffffull) >> 42);
+        if (r == 0x7c00u) ++r;
+        return (uint16_t)(s | r);
+    }
+    if (a >= 0x40effe0000000000ull) return (uint16_t)(s | 0x7c00u);                 // >= 65520
+    if (a >= 0x3f10000000000000ull)                                                  // >= 2^-14
+        return (uint16_t)(s | rne_shift<unsigned long long>(a - 0x3f00000000000000ull, 42));
+    if (a < 0x3e60000000000000ull) return (uint16_t)s;                              // <= 2^-25
+    const int e = (int)(a >> 52);
+    return (uint16_t)(s | rne_shift<unsigned long long>((a & 0xfffffffffffffull) | (1ull << 52),
+                                                        1051 - e));
+}
+
+// x86 cvttsd2si (numpy's float -> int casts on the in-place write-back of
+// integer positions): NaN / out of range -> the "integer indefinite" MIN.
+__device__ __forceinline__ int trunc_i32(double v) {
+    return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : INT_MIN;
+}
+
+template <typename P>
+constexpr bool kExtPos = std::is_same<P, int32_t>::value || std::is_same<P, int64_t>::value ||
+                         std::is_same<P, f16_t>::value;
+
+// A stored position as numpy promotes it against a float64 scalar (the
+// quotient of integer positions, the halo's float64 comparisons).
+template <typename PosT>
+__device__ __forceinline__ double pos_as_f64(PosT v) {
+    if constexpr (std::is_same<PosT, f16_t>::value) return h2d(v.u);
+    else if constexpr (std::is_same<PosT, float>::value) return f32_to_f64_x86(v);
+    else return (double)v;   // int64: round to nearest, as numpy's cast
+}
+
 template <typename PosT>
 __device__ __forceinline__ bool same_bits(PosT a, PosT b) {
-    if constexpr (sizeof(PosT) == 8) return __double_as_longlong((double)a) == __double_as_longlong((double)b);
+    if constexpr (std::is_same<PosT, f16_t>::value) return a.u == b.u;
+    else if constexpr (std::is_integral<PosT>::value) return a == b;
+    else if constexpr (sizeof(PosT) == 8) return __double_as_longlong((double)a) == __double_as_longlong((double)b);
     else return __float_as_uint((float)a) == __float_as_uint((float)b);
 }
 
@@ -148,11 +233,119 @@ __device__ __forceinline__ bool same_bits(PosT a, PosT b) {
 //     float64 comparisons of redist.py:271-276 for the rank the row lands on.
 constexpr int kSideNone = 0, kSideFine = 1, kSideHalo = 2;
 
+// The index stage of one coordinate, every position dtype alike: k =
+// trunc(q * n) (and kf = trunc(q * n_fine)) from the quotient, the integer
+// wrap of :90, the fine / halo side value from xs (the stored coordinate as
+// float64).
+template <int SIDE>
+__device__ __forceinline__ long long coord_index(long long k, long long kf, double xs,
+                                                 const Geom& g, int d, long long* raw,
+                                                 const FineGeom* fg, const HaloGeom* hg,
+                                                 long long* side) {
+    if (raw) *raw = k;
+    const long long n = g.n[d];
+    if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
+    if (g.fine) k %= g.fmod[d];   // fine-cell plan: index inside the rank's cell
+    if (SIDE == kSideFine) {
+        const long long nf = fg->n[d];
+        if (!(kf >= 0 && kf < nf)) kf = floormod_i64(floormod_i64(kf, nf) + nf, nf);
+        // kf % f without a 64-bit division: kf - f*k when the coarse index k
+        // is kf's cell (always, up to rounding at a cell face), else the
+        // remainder itself
+        const long long f = fg->fmod[d];
+        long long m = kf - f * k;
+        if (!(m >= 0 && m < f)) m = kf % f;
+        *side = m;
+    }
+    if (SIDE == kSideHalo) {
+        // limits (redist.py:110-111): k * cl and (k + 1) * cl, int64 * float64
+        const double hi = (double)(k + 1) * hg->cl[d] - hg->ol[d];
+        const double lo = (double)k * hg->cl[d] + hg->ol[d];
+        *side = (xs > hi ? 1 : 0) | (xs < lo ? 2 : 0);
+    }
+    return k;
+}
+
+// One coordinate of an int32 / int64 / float16 position (kExtPos): numpy
+// 2.2.6's promotion of `position[:, d] % box[d]` (Geom::wmode) and of
+// `position[:, d] / box[d]` (Geom::dmode), mgr_capi.hip pos_modes:
+//   * integer positions, integer box: integer floor-mod at the promoted width
+//     (the `+ L` wraps like numpy's), stored back truncated to the column's
+//     width; the quotient is float64 (true division);
+//   * integer positions, float box: the wrap in float64, stored back by x86
+//     truncation (NaN / out of range -> INT_MIN), the quotient float64 from the
+//     stored integer;
+//   * float16 positions: the wrap in float64 / float32 rounded to float16 on
+//     the write-back (as S9 for float32), or -- box float16 / int8 / uint8 --
+//     every operation in float32 rounded to float16 (numpy's half arithmetic);
+//     the quotient in float64, float32 or float16 alike, then * n in float64.
+// The general path only (no fast in-box variant): these dtypes are for
+// parity with the reference's inputs, not the bench's hot configurations.
+static __device__ __forceinline__ long long wrap_int(long long x, long long L, bool w32) {
+    const long long m = floormod_i64(x, L);   // numpy: x % 0 == 0
+    long long s = (long long)((unsigned long long)m + (unsigned long long)L);
+    if (w32) s = (long long)(int)(unsigned)s;
+    return floormod_i64(s, L);
+}
+static __device__ __forceinline__ uint16_t wrap_f16(uint16_t x, float L) {
+    const float m = pymodf(h2f(x), L);
+    const uint16_t mh = f2h(m);
+    if (isnan(m)) return mh;   // a NaN propagates unchanged (x86)
+    const uint16_t yh = f2h(h2f(mh) + L);
+    return f2h(pymodf(h2f(yh), L));
+}
+
+template <typename PosT, bool kPeriodic, int SIDE>
+__device__ __forceinline__ long long bin_coord_ext(PosT* p, const Geom& g, int d, long long* raw,
+                                                   bool* dirty, const FineGeom* fg,
+                                                   const HaloGeom* hg, long long* side) {
+    const PosT in = *p;
+    PosT s = in;   // the stored value binning reads back (S2)
+    if (kPeriodic) {
+        if constexpr (std::is_same<PosT, f16_t>::value) {
+            if (g.wmode == MGR_F64)
+                s.u = d2h(wrap_f64(h2d(in.u), g.L[d], g.twoL[d], g.fast[d]));
+            else if (g.wmode == MGR_F32)
+                s.u = f2h(wrap_f32(h2f(in.u), g.Lf[d], g.twoLf[d], g.fastf[d]));
+            else
+                s.u = wrap_f16(in.u, g.Lf[d]);
+        } else {
+            if (g.wmode == MGR_F64) {
+                const double t = wrap_f64((double)in, g.L[d], g.twoL[d], g.fast[d]);
+                s = sizeof(PosT) == 4 ? (PosT)trunc_i32(t) : (PosT)trunc_i64(t);
+            } else {
+                s = (PosT)wrap_int((long long)in, g.Li[d], g.wmode == MGR_I32);
+            }
+        }
+        if (!same_bits(s, in)) { *p = s; *dirty = true; }
+    }
+    long long k, kf = 0;
+    const double xs = pos_as_f64(s);
+    double q = 0.0;   // the quotient as the float64 the `* n` promotes it to
+    if constexpr (std::is_same<PosT, f16_t>::value) {
+        if (g.dmode == MGR_F64) {
+            q = xs / g.L[d];
+        } else {   // the quotient in float32, or float16
+            float qf = h2f(s.u) / g.Lf[d];
+            if (g.dmode == MGR_F16) qf = h2f(f2h(qf));
+            q = (double)qf;
+        }
+    } else {
+        q = xs / g.L[d];   // integer positions: true division in float64
+    }
+    k = trunc_i64(q * g.nd[d]);
+    if (SIDE == kSideFine) kf = trunc_i64(q * fg->nd[d]);
+    return coord_index<SIDE>(k, kf, xs, g, d, raw, fg, hg, side);
+}
+
 template <typename PosT, bool kPeriodic, int SIDE = kSideNone>
 __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, long long* raw,
                                                bool* dirty, const FineGeom* fg = nullptr,
                                                const HaloGeom* hg = nullptr,
                                                long long* side = nullptr) {
+    if constexpr (kExtPos<PosT>) {
+        return bin_coord_ext<PosT, kPeriodic, SIDE>(p, g, d, raw, dirty, fg, hg, side);
+    } else {
     long long k, kf = 0;
     double xs = 0.0;   // the stored (wrapped) coordinate, as numpy compares it
     const PosT in = *p;
@@ -179,28 +372,8 @@ __device__ __forceinline__ long long bin_coord(PosT* p, const Geom& g, int d, lo
         if (SIDE == kSideFine) kf = trunc_i64(q * fg->nd[d]);
         if (SIDE == kSideHalo) xs = x;
     }
-    if (raw) *raw = k;
-    const long long n = g.n[d];
-    if (!(k >= 0 && k < n)) k = floormod_i64(floormod_i64(k, n) + n, n);
-    if (g.fine) k %= g.fmod[d];   // fine-cell plan: index inside the rank's cell
-    if (SIDE == kSideFine) {
-        const long long nf = fg->n[d];
-        if (!(kf >= 0 && kf < nf)) kf = floormod_i64(floormod_i64(kf, nf) + nf, nf);
-        // kf % f without a 64-bit division: kf - f*k when the coarse index k
-        // is kf's cell (always, up to rounding at a cell face), else the
-        // remainder itself
-        const long long f = fg->fmod[d];
-        long long m = kf - f * k;
-        if (!(m >= 0 && m < f)) m = kf % f;
-        *side = m;
+    return coord_index<SIDE>(k, kf, xs, g, d, raw, fg, hg, side);
     }
-    if (SIDE == kSideHalo) {
-        // limits (redist.py:110-111): k * cl and (k + 1) * cl, int64 * float64
-        const double hi = (double)(k + 1) * hg->cl[d] - hg->ol[d];
-        const double lo = (double)k * hg->cl[d] + hg->ol[d];
-        *side = (xs > hi ? 1 : 0) | (xs < lo ? 2 : 0);
-    }
-    return k;
 }
 
 // In-box fast path of bin_row: every coordinate in [0, L_d) with the fast
@@ -293,7 +466,7 @@ __device__ __forceinline__ long long bin_row(PosT* row, const Geom& g, long long
                                              bool* dirty, const FineGeom* fg = nullptr,
                                              const HaloGeom* hg = nullptr,
                                              long long* side = nullptr) {
-    if constexpr (DIM > 0) {
+    if constexpr (DIM > 0 && !kExtPos<PosT>) {
         long long c;
         if (!idx && (GEO != kGeoAny || g.fast32) &&
             bin_row_fast<PosT, kPeriodic, DIM, SIDE, GEO>(row, g, dirty, fg, hg, &c, side))

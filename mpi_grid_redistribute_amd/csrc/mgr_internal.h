@@ -49,6 +49,14 @@ struct Geom {
     int64_t fmod[MGR_MAX_DIM];           // fine cells per rank cell and dimension
     int fast32;                          // every n[d] < 2^30: in-box rows bin in 32-bit ints
     int write_back_all;                  // mgr_plan_set_write_back: every slab written back
+    int box_dtype;                       // the caller's box_length dtype (mgr_dtype)
+    // Per call, from the positions' dtype (mgr_capi.hip pos_modes; read by the
+    // int32 / int64 / float16 positions' path, bin_coord_ext): numpy's result
+    // type of `position[:, d] % box[d]` (MGR_F16/F32/F64/I32/I64) and of
+    // `position[:, d] / box[d]` (MGR_F16/F32/F64).
+    int wmode;
+    int dmode;
+    int64_t Li[MGR_MAX_DIM];             // integer box lengths (wmode I32 / I64)
 };
 
 // The fine cells a row falls in, inside its destination's cell (SURVEY f4,
@@ -96,7 +104,7 @@ void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);
 
 // Launchers (return hipError_t of the launch; validate arguments before calling).
-hipError_t launch_bin_count(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+hipError_t launch_bin_count(const Geom& g, void* pos, int pos_dtype, int64_t n, int64_t stride,
                             int periodic, void* dest, int tile_rows, const Workspace& ws,
                             hipStream_t s, const FineGeom* fg = nullptr,
                             uint16_t* side_out = nullptr, const HaloGeom* hg = nullptr);
@@ -114,7 +122,7 @@ hipError_t launch_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_r
 hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
                               const uint16_t* ranks, const uint16_t* tile_starts, int nbins,
                               int tile_rows, const Workspace& ws, void* dst, hipStream_t s);
-hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_f32, int64_t n, int64_t stride,
+hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_dtype, int64_t n, int64_t stride,
                            int periodic, int64_t* cell, int64_t* idx, hipStream_t s);
 hipError_t launch_bin_ids(const void* ids, int ids_dtype, int64_t n, int nbins, void* dest,
                           int tile_rows, const Workspace& ws, hipStream_t s);
@@ -133,14 +141,15 @@ int pack_tile_rows(int64_t row_bytes, int nbins);
 hipError_t launch_tile_offsets(const Workspace& ws, int nbins, const int64_t* tiles, int ntiles,
                                int64_t* out, hipStream_t s);
 int ranked_tile_rows(int64_t row_bytes, int nbins);
-hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
+hipError_t launch_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
 
 // Test hooks (include/mgr_instrument.h, mgr_test_hook): switches that make a
 // product-reachable fallback or shape run on inputs that would not take it,
 // so the parity tests reach every path.  None changes results.  Launches read
-// an immutable snapshot (hooks()); mgr_test_hook publishes a new one as a
-// whole, so a launch sees either the old or the new set, never a mix.  The
+// an immutable snapshot (hooks(), read ONCE per launcher: `const Hooks& h =
+// hooks();`); mgr_test_hook publishes a new one as a whole, so a launch sees
+// either the old or the new set, never a mix.  The
 // shipped configuration is the default-constructed snapshot.
 struct Hooks {
     int tile_rounds = 0;     // != 0: pack/bin tiles of 64 * tile_rounds rows
@@ -152,6 +161,18 @@ struct Hooks {
     int bin_unstaged = 0;    // bin kernel without LDS slab staging (the wide / unaligned fallback)
     int bin_generic = 0;     // bin kernel with run-time geometry also for simple plans
     int pack_generic = 0;    // wave-per-tile pack_kernel also for <= 64 bins (the > 64-B row path)
+    // scan race test: the chunk that ends bin scan_delay_bin counts itself
+    // done, then sleeps scan_delay_sleeps x s_sleep(127) before storing its
+    // inclusive word;
+    // scan_end_spins >= 0 bounds the last ticket's polls of the bin-end words
+    // (0 = one look: the pre-round-4 reader, which then reports the race)
+    int scan_delay_bin = -1;
+    int scan_delay_sleeps = 0;
+    int scan_end_spins = -1;
+};
+// The scan kernel's copy of the race-test hooks (kernel argument).
+struct ScanTest {
+    int delay_bin, delay_sleeps, end_spins;
 };
 const Hooks& hooks();
 int set_hook(const char* key, int64_t value);   // mgr_test_hook

@@ -53,6 +53,9 @@ int set_hook(const char* key, int64_t v) {
     else if (!strcmp(key, "bin_unstaged") && in(0, 1)) h->bin_unstaged = (int)v;
     else if (!strcmp(key, "bin_generic") && in(0, 1)) h->bin_generic = (int)v;
     else if (!strcmp(key, "pack_generic") && in(0, 1)) h->pack_generic = (int)v;
+    else if (!strcmp(key, "scan_delay_bin") && in(-1, MGR_MAX_BINS)) h->scan_delay_bin = (int)v;
+    else if (!strcmp(key, "scan_delay_sleeps") && in(0, 1 << 16)) h->scan_delay_sleeps = (int)v;
+    else if (!strcmp(key, "scan_end_spins") && in(-1, 1 << 30)) h->scan_end_spins = (int)v;
     else return -1;
     g_hooks.store(h.get(), std::memory_order_release);
     kept.push_back(std::move(h));
@@ -88,11 +91,12 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
                                                               int64_t* __restrict__ offsets,
                                                               int64_t* __restrict__ bin_starts,
                                                               int64_t* __restrict__ bin_counts,
-                                                              int spins) {
+                                                              int spins, ScanTest tst) {
     constexpr int TILE = ITEMS * kBlock;
     __shared__ long long s_w[kWaves];
     __shared__ long long s_excl;
     __shared__ int s_j, s_poison;
+    __shared__ uint64_t s_incl;   // the inclusive word (test hook: stored late)
     ScanCtl* ctl = scan_ctl(flags);
     if (threadIdx.x == 0) {
         s_j = (int)__hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED,
@@ -123,8 +127,13 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
         const int lane = threadIdx.x;
         long long excl = 0;
         uint64_t poison = 0;
+        // test hook: the chunk ending bin tst.delay_bin stores its inclusive
+        // word only after counting itself done
+        const bool late = tst.delay_bin >= 0 && j == (tst.delay_bin + 1) * cpb - 1 &&
+                          j != (int)gridDim.x - 1;
         if (j == 0) {
-            if (lane == 0) flag_store(&flags[0], kScanInc | (uint64_t)agg);
+            if (lane == 0 && !late) flag_store(&flags[0], kScanInc | (uint64_t)agg);
+            if (lane == 0) s_incl = kScanInc | (uint64_t)agg;
         } else {
             if (lane == 0) flag_store(&flags[j], kScanAgg | (uint64_t)agg);
             for (int base = j - 1;; base -= 64) {
@@ -143,7 +152,8 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
                 excl += x;
                 if (inc) break;
             }
-            if (lane == 0) flag_store(&flags[j], kScanInc | poison | (uint64_t)(excl + agg));
+            if (lane == 0 && !late) flag_store(&flags[j], kScanInc | poison | (uint64_t)(excl + agg));
+            if (lane == 0) s_incl = kScanInc | poison | (uint64_t)(excl + agg);
         }
         if (lane == 0) {
             s_excl = excl;
@@ -188,9 +198,18 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
     // fences (a release here costs an L2 write-back per workgroup)
     constexpr uint64_t kDoneMask = 0xFFFFFFFFull;
     if (j != (int)gridDim.x - 1) {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             __hip_atomic_fetch_add(&ctl->done, 1ull + (s_poison ? (1ull << 32) : 0ull),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tst.delay_bin >= 0 && j == (tst.delay_bin + 1) * cpb - 1) {
+                // test hook (scan_delay_bin): this chunk is seen done long
+                // before its inclusive word -- the visibility order relaxed
+                // atomics on two words allow -- so the last ticket must poll
+                // the bin-end words (tests/test_gpu_api.py scan race test)
+                for (int i = 0; i < tst.delay_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
+                flag_store(&flags[j], s_incl);
+            }
+        }
         return;
     }
     // The last ticket: wait until every other chunk is done (all of them hold
@@ -222,16 +241,17 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
         // done count can be seen before the word.  So the words are polled
         // (bounded, like every look-back) rather than read once -- one look
         // could read a bin end's aggregate as its prefix (a wrong count).
+        const int end_spins = tst.end_spins >= 0 ? tst.end_spins : spins;   // hook: 0 = one look
         for (int bb = threadIdx.x; bb < nbins; bb += kBlock) {
             bool bad = failed;
             long long st = 0, en = total;
             if (bb > 0) {
-                const uint64_t w = flag_poll(&flags[bb * cpb - 1], 2, spins);
+                const uint64_t w = flag_poll(&flags[bb * cpb - 1], 2, end_spins);
                 st = (long long)(w & kScanVal);
                 bad |= (w & kScanPoison) != 0;
             }
             if (bb < nbins - 1) {
-                const uint64_t w = flag_poll(&flags[(bb + 1) * cpb - 1], 2, spins);
+                const uint64_t w = flag_poll(&flags[(bb + 1) * cpb - 1], 2, end_spins);
                 en = (long long)(w & kScanVal);
                 bad |= (w & kScanPoison) != 0;
             }
@@ -247,8 +267,8 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
 // exchange_overload_by_position (redist.py:202-309) selects, per dimension
 // d, the rows with position[:, d] > limits[d,1] - ol[d] (sent to the right
 // neighbour, :271/:274) and position[:, d] < limits[d,0] + ol[d] (to the
-// left, :272/:275).  numpy compares the float32/float64 column against the
-// float64 threshold in float64 (exact), NaN selects nothing.
+// left, :272/:275).  numpy compares the column (float16/32/64, int32/64)
+// against the float64 threshold in float64 (pos_as_f64), NaN selects nothing.
 struct HaloThr { double hi[MGR_MAX_DIM]; double lo[MGR_MAX_DIM]; };
 
 // flags[r] bit 2d: coordinate d > hi[d]; bit 2d+1: coordinate d < lo[d].
@@ -261,8 +281,7 @@ __global__ __launch_bounds__(kBlock) void halo_flags_kernel(const PosT* __restri
     for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < n; r += step) {
         unsigned f = 0;
         for (int d = 0; d < dim; ++d) {
-            const double x = sizeof(PosT) == 4 ? f32_to_f64_x86((float)pos[r * stride + d])
-                                               : (double)pos[r * stride + d];
+            const double x = pos_as_f64(pos[r * stride + d]);
             f |= (x > t.hi[d] ? 1u : 0u) << (2 * d);
             f |= (x < t.lo[d] ? 1u : 0u) << (2 * d + 1);
         }
@@ -478,9 +497,10 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
         if (e == hipSuccess && bin_counts) e = hipMemsetAsync(bin_counts, 0, (size_t)nbins * 8, s);
         return e;
     }
-    const int64_t target = hooks().scan_chunk;         // counts per chunk (workgroup)
+    const Hooks& h = hooks();                         // one snapshot per launch
+    const int64_t target = h.scan_chunk;               // counts per chunk (workgroup)
     int64_t cpb = (ws.T + target - 1) / target;
-    int64_t cap = min((int64_t)hooks().scan_max_chunks, (int64_t)kScanFlags) / nbins;
+    int64_t cap = min((int64_t)h.scan_max_chunks, (int64_t)kScanFlags) / nbins;
     if (cap < 1) cap = 1;                             // nbins <= MGR_MAX_BINS = kScanFlags
     if (cpb > cap) cpb = cap;
     const int64_t chunk = (ws.T + cpb - 1) / cpb;
@@ -489,12 +509,20 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     auto k = chunk <= 8 * kBlock ? scan_onepass_kernel<8> : scan_onepass_kernel<16>;
     hipLaunchKernelGGL(k, dim3((unsigned)(nbins * cpb)), dim3(kBlock), 0, s, ws.counts, ws.T,
                        chunk, (int)cpb, nbins, ws.flags, ws.offsets, ws.bin_starts, bin_counts,
-                       hooks().scan_spins);
+                       h.scan_spins, ScanTest{h.scan_delay_bin, h.scan_delay_sleeps,
+                                              h.scan_end_spins});
     prof_end(s, K_SCAN);
     return hipGetLastError();
 }
 
-hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t stride, int dim,
+template <typename PosT>
+static void halo_flags_t(const void* pos, int64_t n, int64_t stride, int dim, const HaloThr& t,
+                         uint16_t* flags, hipStream_t s) {
+    hipLaunchKernelGGL(halo_flags_kernel<PosT>, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       (const PosT*)pos, n, stride, dim, t, flags);
+}
+
+hipError_t launch_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     HaloThr t;
@@ -503,12 +531,13 @@ hipError_t launch_halo_flags(const void* pos, int pos_f32, int64_t n, int64_t st
         t.lo[d] = d < dim ? lo[d] : 0.0;
     }
     prof_begin(s, K_HALO);
-    if (pos_f32)
-        hipLaunchKernelGGL(halo_flags_kernel<float>, dim3(grid_for(n)), dim3(kBlock), 0, s,
-                           (const float*)pos, n, stride, dim, t, flags);
-    else
-        hipLaunchKernelGGL(halo_flags_kernel<double>, dim3(grid_for(n)), dim3(kBlock), 0, s,
-                           (const double*)pos, n, stride, dim, t, flags);
+    switch (pos_dtype) {
+        case MGR_F32: halo_flags_t<float>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_F64: halo_flags_t<double>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_I32: halo_flags_t<int32_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_I64: halo_flags_t<int64_t>(pos, n, stride, dim, t, flags, s); break;
+        default: halo_flags_t<f16_t>(pos, n, stride, dim, t, flags, s); break;
+    }
     prof_end(s, K_HALO);
     return hipGetLastError();
 }

@@ -759,7 +759,8 @@ struct SideField {
 static int many_round_rows(int nbins) { return nbins <= 512 ? 2048 : 4096; }
 
 int pack_tile_rows(int64_t row_bytes, int nbins) {
-    if (hooks().tile_rounds > 0) return 64 * hooks().tile_rounds;
+    const int tr = hooks().tile_rounds;   // one snapshot
+    if (tr > 0) return 64 * tr;
     // <= 16 bins: 512-row tiles (bin: 4 waves x 2 rounds; pack: 8 waves x
     // 1 round; A/B against 1024 at 8 bins: bin -3 %, pack within noise);
     // <= 64 bins: 1024 rows (64 bins: pack 0.92 vs 1.07 ms at 512: longer

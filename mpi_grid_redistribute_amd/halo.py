@@ -317,7 +317,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
         hi, lo = thresholds(R, overload_lengths)
         flags = sel.flags(pos_flat, n, ncols, pos_code, dim, hi, lo)
     flags_flat = flags.reshape(-1).view(torch.uint8)[: 2 * n]
-    isz = 4 if pos_code == _lib.MGR_F32 else 8
+    isz = _lib.POS_ITEMSIZE[pos_code]
     srcs = [data_flat] + ([pos_flat] if carry_pos else []) + [flags_flat]
     rbs = [rbd] + ([ncols * isz] if carry_pos else []) + [2]
     F, FL = len(rbs), len(rbs) - 1                        # fields; the flags field

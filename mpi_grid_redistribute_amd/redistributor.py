@@ -37,7 +37,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._arrays import Positions, Rows, box_dtype_code, device, id_array
+from ._arrays import Positions, Rows, box_dtype_code, device, id_array, pos_code
 from .comm import SelfComm, as_transport
 from .exchange import check_counts, exchange, exchange_pipelined
 from .halo import DeviceSelect, exchange_overload, halo_capacity, thresholds
@@ -554,12 +554,7 @@ class MPIGridRedistributor:
         if not (isinstance(position, (np.ndarray, torch.Tensor)) and position.ndim == 2
                 and position.shape[1] >= self.dim):
             raise ValueError(f"position must be (N, >= {self.dim})")
-        if position.dtype in (np.float32, torch.float32):
-            code = _lib.MGR_F32
-        elif position.dtype in (np.float64, torch.float64):
-            code = _lib.MGR_F64
-        else:
-            raise TypeError(f"position dtype {position.dtype} not supported (float32/float64)")
+        code = pos_code(position.dtype)
         if prow.n != rows.n:
             raise ValueError(f"data has {rows.n} rows, position has {prow.n}")
         sel = DeviceSelect(self._dev, self._scratch)
@@ -617,7 +612,7 @@ class MPIGridRedistributor:
 
     @staticmethod
     def _pos_row_bytes(position, pos):
-        return int(position.shape[1]) * (4 if pos.code == _lib.MGR_F32 else 8)
+        return int(position.shape[1]) * _lib.POS_ITEMSIZE[pos.code]
 
     def redistribute_by_cell_number(self, data, rank_to_send):
         """redist.py:169-200: send row i to rank ``rank_to_send[i]``; ids
@@ -813,7 +808,7 @@ class GridPartitioner:
         (out_flat, fine_ids_out, bin_counts)."""
         n = int(pos_tensor.shape[0])
         tile_rows, ws, dest, out, counts = self.buffers(n, row_bytes)
-        code = _lib.MGR_F32 if pos_tensor.dtype == torch.float32 else _lib.MGR_F64
+        code = pos_code(pos_tensor.dtype)
         s = _lib.stream_handle(stream)
         if fine_cells is None:
             _lib.call("mgr_partition_by_position", self._plan.h, _lib.ptr(pos_tensor), code, n,

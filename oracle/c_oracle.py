@@ -45,12 +45,25 @@ def lib():
         L.oracle_local_partition_omp.argtypes = [_P, _I64, _I64, ctypes.c_int, _P, _P,
                                                  ctypes.c_int, _P, _I64, _P, _P, ctypes.c_int]
         L.oracle_local_partition_omp.restype = _I64
+        L.oracle_bin_ext.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _I64,
+                                     ctypes.c_int, _P, _P, ctypes.c_int, _P, _P]
+        L.oracle_bin_ext.restype = None
+        L.oracle_d2h.argtypes = [ctypes.c_double]
+        L.oracle_d2h.restype = ctypes.c_uint16
+        L.oracle_f2h.argtypes = [ctypes.c_float]
+        L.oracle_f2h.restype = ctypes.c_uint16
         _lib = L
     return _lib
 
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+# oracle_bin_ext dtype codes (the O_* of mgr_oracle.c)
+_CODES = {np.dtype(np.float32): 1, np.dtype(np.float64): 2, np.dtype(np.int32): 3,
+          np.dtype(np.int64): 4, np.dtype(np.float16): 5}
+_EXT = {np.dtype(np.int32): 3, np.dtype(np.int64): 4, np.dtype(np.float16): 5}
 
 
 def bin_positions(position, grid_topology, box_length, periodic=True, compute_f32=None,
@@ -62,6 +75,19 @@ def bin_positions(position, grid_topology, box_length, periodic=True, compute_f3
     topo = np.ascontiguousarray(np.asarray(grid_topology).astype(np.int64))
     box_arr = np.asarray(box_length)
     dim = len(topo)
+    if position.dtype in _EXT:
+        # numpy itself names the types the wrap and the quotient compute in
+        zp, zb = np.zeros(1, position.dtype), np.ones(1, box_arr.dtype)
+        wmode = _CODES[(zp % zb[0]).dtype]
+        dmode = _CODES[(zp / zb[0]).dtype]
+        box = np.ascontiguousarray(box_arr.astype(np.float64))
+        n = position.shape[0]
+        cell = np.empty(n, dtype=np.int64)
+        idx = np.empty((n, dim), dtype=np.int64) if want_idx else None
+        lib().oracle_bin_ext(_ptr(position), _EXT[position.dtype], wmode, dmode, n,
+                             position.strides[0] // position.itemsize, dim, _ptr(box), _ptr(topo),
+                             int(bool(periodic)), _ptr(cell), _ptr(idx))
+        return (cell, idx) if want_idx else cell
     is_f32 = position.dtype == np.float32
     assert is_f32 or position.dtype == np.float64
     if compute_f32 is None:

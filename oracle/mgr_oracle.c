@@ -131,6 +131,148 @@ void oracle_bin(void* pos, int pos_is_f32, int compute_f32, int64_t n, int64_t r
                           periodic, idx, 0);
 }
 
+/* ---- int32 / int64 / float16 positions (redist.py:68-69 on any numpy column).
+ * numpy 2.2.6 float16 conversions, restated from their documented behaviour:
+ * round to nearest even with overflow to inf; NaN keeps sign and payload
+ * (shifted), never quieted, forced nonzero; half arithmetic = the float32
+ * operation rounded back.  Written independently of the device version
+ * (mgr_device.h): plain value arithmetic for the rounding. */
+static float h2f(uint16_t h) {
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    float v;
+    uint32_t b;
+    if (e == 0x1fu) {
+        b = s | 0x7f800000u | (m << 13);
+        memcpy(&v, &b, 4);
+        return v;
+    }
+    v = e ? ldexpf((float)(m | 0x400u), (int)e - 25) : ldexpf((float)m, -24);
+    return (h & 0x8000u) ? -v : v;
+}
+static double h2d(uint16_t h) {
+    if (((h >> 10) & 0x1fu) == 0x1fu) {
+        const uint64_t b = ((uint64_t)(h & 0x8000u) << 48) | 0x7ff0000000000000ull |
+                           ((uint64_t)(h & 0x3ffu) << 42);
+        double v;
+        memcpy(&v, &b, 8);
+        return v;
+    }
+    return (double)h2f(h);
+}
+/* |x| (finite, < 65520) to float16 bits by value: scale to the half's ulp and
+ * round half to even with nearbyint (default rounding mode). */
+static uint16_t mag_to_half(double a) {
+    if (a < 0x1p-14) return (uint16_t)nearbyint(a * 0x1p24);     /* subnormal (or 0x400) */
+    int e;
+    frexp(a, &e);                      /* a = f * 2^e, f in [0.5, 1) */
+    const double ulp = ldexp(1.0, e - 11);
+    double q = nearbyint(a / ulp);     /* 1024..2048 significand units */
+    int he = e - 1 + 15;               /* biased half exponent of a */
+    if (q >= 2048.0) { q /= 2.0; he += 1; }
+    if (he >= 31) return 0x7c00u;
+    return (uint16_t)((he << 10) | ((int)q - 1024));
+}
+static uint16_t d2h(double x) {
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    const uint16_t s = (uint16_t)((b >> 48) & 0x8000u);
+    if (isnan(x)) {
+        uint16_t r = (uint16_t)(0x7c00u + ((b & 0xfffffffffffffull) >> 42));
+        if (r == 0x7c00u) r++;
+        return (uint16_t)(s | r);
+    }
+    const double a = fabs(x);
+    if (a >= 65520.0) return (uint16_t)(s | 0x7c00u);   /* also inf */
+    return (uint16_t)(s | mag_to_half(a));
+}
+static uint16_t f2h(float x) {
+    if (isnan(x)) {
+        uint32_t b;
+        memcpy(&b, &x, 4);
+        uint16_t r = (uint16_t)(0x7c00u + ((b & 0x7fffffu) >> 13));
+        if (r == 0x7c00u) r++;
+        return (uint16_t)(((b >> 16) & 0x8000u) | r);
+    }
+    return d2h((double)x);   /* float -> double is exact: one rounding */
+}
+/* numpy's float -> int32 cast on x86 (cvttsd2si, 32-bit): NaN / out of range -> INT32_MIN */
+static int32_t trunc_i32(double v) {
+    if (v > -2147483649.0 && v < 2147483648.0) return (int32_t)v;
+    return INT32_MIN;
+}
+
+uint16_t oracle_d2h(double x) { return d2h(x); }
+uint16_t oracle_f2h(float x) { return f2h(x); }
+double oracle_h2d(uint16_t h) { return h2d(h); }
+
+enum { O_F32 = 1, O_F64 = 2, O_I32 = 3, O_I64 = 4, O_F16 = 5 };
+
+/* Bin n rows of int32 / int64 / float16 positions (pos_dtype O_*).  wmode:
+ * numpy's type of position % box (O_F16/F32/F64/I32/I64), dmode: of
+ * position / box (O_F16/F32/F64) -- the caller takes both from numpy itself
+ * (c_oracle.bin_positions).  The wrap is stored back cast to the column's
+ * type; binning reads the stored value (S2). */
+void oracle_bin_ext(void* pos, int pos_dtype, int wmode, int dmode, int64_t n, int64_t row_stride,
+                    int dim, const double* box, const int64_t* topo, int periodic, int64_t* cell,
+                    int64_t* idx) {
+    int64_t offset[64];
+    int64_t off = 1;
+    for (int d = dim - 1; d >= 0; --d) { offset[d] = off; off *= topo[d]; }
+    for (int64_t r = 0; r < n; ++r) {
+        int64_t c = 0;
+        for (int d = 0; d < dim; ++d) {
+            const int64_t e = r * row_stride + d;
+            const double L = box[d];
+            const float Lf = (float)L;
+            double xs;   /* the stored value as float64 */
+            if (pos_dtype == O_F16) {
+                uint16_t* p = (uint16_t*)pos + e;
+                if (periodic) {
+                    if (wmode == O_F64) {
+                        *p = d2h(pymod(pymod(h2d(*p), L) + L, L));
+                    } else if (wmode == O_F32) {
+                        *p = f2h(pymodf(pymodf(h2f(*p), Lf) + Lf, Lf));
+                    } else {   /* half arithmetic: each step rounded to float16 */
+                        const uint16_t m = f2h(pymodf(h2f(*p), Lf));
+                        const uint16_t y = f2h(h2f(m) + Lf);
+                        *p = f2h(pymodf(h2f(y), Lf));
+                    }
+                }
+                xs = h2d(*p);
+                double q;
+                if (dmode == O_F64) q = xs / L;
+                else if (dmode == O_F32) q = (double)(h2f(*p) / Lf);
+                else q = (double)h2f(f2h(h2f(*p) / Lf));
+                const int64_t k = trunc_i64(q * (double)topo[d]);
+                if (idx) idx[r * dim + d] = k;
+                c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
+                continue;
+            }
+            int64_t x = pos_dtype == O_I32 ? (int64_t)((int32_t*)pos)[e] : ((int64_t*)pos)[e];
+            if (periodic) {
+                int64_t t;
+                if (wmode == O_F64) {
+                    const double w = pymod(pymod((double)x, L) + L, L);
+                    t = pos_dtype == O_I32 ? (int64_t)trunc_i32(w) : trunc_i64(w);
+                } else {   /* integer floor-mod at the promoted width; the + L wraps */
+                    const int64_t Li = (int64_t)L;
+                    uint64_t s = (uint64_t)floormod_i64(x, Li) + (uint64_t)Li;
+                    if (wmode == O_I32) s = (uint64_t)(int64_t)(int32_t)(uint32_t)s;
+                    t = floormod_i64((int64_t)s, Li);
+                }
+                if (pos_dtype == O_I32) ((int32_t*)pos)[e] = (int32_t)(uint32_t)(uint64_t)t;
+                else ((int64_t*)pos)[e] = t;
+                x = pos_dtype == O_I32 ? (int64_t)((int32_t*)pos)[e] : ((int64_t*)pos)[e];
+            }
+            xs = (double)x;
+            const int64_t k = trunc_i64(xs / L * (double)topo[d]);
+            if (idx) idx[r * dim + d] = k;
+            c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
+        }
+        cell[r] = c;
+    }
+}
+
 /*
  * The local stage on the host's cores (bench.py cpu_baseline_c): wrap + bin
  * of f64 positions and a stable partition of the rows, threaded: every

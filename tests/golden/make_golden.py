@@ -404,9 +404,175 @@ def make_fine(ref, rng):
     return n_files + 1
 
 
+BOX_KINDS = {  # how the caller spells box_length -> np.array(box_length) (redist.py:46)
+    "f64": lambda L: [float(L)], "int": lambda L: [int(L)],
+    "f32": lambda L: np.array([L], np.float32), "f16": lambda L: np.array([L], np.float16),
+    "i8": lambda L: np.array([L], np.int8), "i16": lambda L: np.array([L], np.int16),
+    "i32": lambda L: np.array([L], np.int32), "u32": lambda L: np.array([L], np.uint32),
+    "u64": lambda L: np.array([L], np.uint64),
+}
+
+
+def int_edge_values(L, rng, dt):
+    info = np.iinfo(dt)
+    L = int(L)
+    v = [0, -1, 1, L - 1, L, L + 1, -L, -L + 1, 2 * L, -2 * L, 6 * L - 1, -6 * L + 1,
+         info.min, info.max, info.min + 1, info.max - 1, 12345, -12345]
+    if dt == np.int64:
+        v += [2 ** 53 + 1, -(2 ** 53 + 1), 2 ** 62, -(2 ** 62), 2 ** 31, -(2 ** 31) - 1]
+    v = [x for x in v if info.min <= x <= info.max]
+    u = rng.integers(-6 * L, 6 * L + 1, 200)
+    w = rng.integers(info.min, info.max, 100, dtype=dt, endpoint=True)
+    return np.concatenate([np.array(v, dtype=dt), u.astype(dt), w])
+
+
+def f16_edge_values(L, rng):
+    h = np.float16(L)
+    v = np.array([0.0, -0.0, h, 2 * h, -h, -2 * h, 0.5 * h, 0.25 * h, -0.25 * h, -0.75 * h,
+                  2.6 * h, 65504.0, -65504.0, np.inf, -np.inf, np.nan, 1e-7, -1e-7,
+                  6.0e-8, -6.0e-8, 1000.0, -1000.0], dtype=np.float16)
+    near = np.array([np.nextafter(h, np.float16(0)), np.nextafter(h, np.float16(np.inf)),
+                     np.nextafter(np.float16(0), np.float16(1))], dtype=np.float16)
+    bits = np.array([0x7c01, 0xfc01, 0x7e00, 0xfe00, 0x7d55, 0x0001, 0x8001, 0x03ff, 0x0400],
+                    dtype=np.uint16).view(np.float16)
+    rnd = rng.integers(0, 1 << 16, 200).astype(np.uint16).view(np.float16)
+    u = rng.uniform(-6 * float(L), 6 * float(L), 200).astype(np.float16)
+    w = rng.uniform(0, float(L), 100).astype(np.float16)
+    return np.concatenate([v, near, bits, rnd, u, w])
+
+
+def make_bin_dtypes(ref, rng):
+    """Single-rank binning of int32 / int64 / float16 positions -- and of
+    float32 positions against the narrow boxes that keep numpy's arithmetic
+    in float32 -- across box dtypes (numpy 2.2.6 promotion of :68-69)."""
+    out = {}
+    combos = [(10, 3), (7, 2), (64, 4), (100, 7), (1, 1), (2.5, 2), (0.3, 3), (1000.0, 5)]
+    plan = {"i32": (np.int32, list(BOX_KINDS)), "i64": (np.int64, list(BOX_KINDS)),
+            "f16": (np.float16, list(BOX_KINDS)),
+            "f32": (np.float32, ["f16", "i8", "i16", "i32", "u32", "u64"])}
+    for ci, (L, n) in enumerate(combos):
+        integral = float(L) == int(L)
+        for pname, (pdt, boxes) in plan.items():
+            for bk in boxes:
+                if bk not in ("f64", "f32", "f16") and not integral:
+                    continue
+                if bk == "i8" and L > 127:
+                    continue
+                for periodic in (True, False):
+                    box = BOX_KINDS[bk](L)
+                    with np.errstate(all="ignore"):
+                        if pdt in (np.int32, np.int64):
+                            vals = int_edge_values(L, rng, pdt)
+                        elif pdt == np.float16:
+                            vals = f16_edge_values(L, rng)
+                        else:
+                            vals = edge_values(float(np.asarray(box, dtype=np.float64)[0]),
+                                               rng).astype(np.float32)
+                    pos = vals.reshape(-1, 1)
+                    pos_in = pos.copy()
+                    R = ref.MPIGridRedistributor(SingleComm(n), [n], box)
+                    p2 = pos.copy()
+                    with np.errstate(all="ignore"):
+                        idx = R.get_cell_indexes_from_position(p2, periodic=periodic)
+                        cell = R.get_cell_number_from_position(pos, periodic=periodic)
+                    key = f"c{ci}_{pname}_box{bk}" + ("" if periodic else "_nonperiodic")
+                    out[key + "_L"] = np.asarray(box)
+                    out[key + "_n"] = np.int64(n)
+                    out[key + "_pos_in"] = pos_in
+                    out[key + "_pos_out"] = pos
+                    out[key + "_idx"] = idx
+                    out[key + "_cell"] = cell
+    np.savez_compressed(os.path.join(OUT_DIR, "bin_dtypes.npz"), **out)
+    return len(out)
+
+
+DTYPE_CASES = [
+    # name, topology, box, pos dtype, position range (in box units)
+    ("p4_2d_i32pos_intbox", [2, 2], [100, 60], np.int32, (-1.5, 2.5)),
+    ("p8_f16pos", [2, 2, 2], [1.0, 1.0, 1.0], np.float16, (-0.5, 1.5)),
+    ("p2_i64pos_floatbox", [2, 1, 1], [2.5, 3.0, 1.5], np.int64, (-3.0, 4.0)),
+    ("p4_f16pos_f16box", [2, 2, 1], np.array([1.0, 2.0, 1.0], np.float16), np.float16,
+     (-0.3, 1.3)),
+    ("p6_321_i64pos_intbox", [3, 2, 1], [30, 20, 10], np.int64, (-2.0, 3.0)),
+]
+
+
+def _dtype_positions(rng, n, box, pdt, lo_hi):
+    b = np.asarray(box, dtype=np.float64)
+    p = rng.uniform(lo_hi[0], lo_hi[1], (n, len(b))) * b
+    if np.issubdtype(pdt, np.integer):
+        p = np.floor(p * (1 if b.min() >= 10 else 4))   # integer grid positions
+    return p.astype(pdt)
+
+
+def make_dtypes(ref, rng):
+    """Per-rank redistribution (and one halo case) of int32 / int64 / float16
+    positions through the reference: the in-place wrap's cast back to the
+    column (redist.py:68) and the binning of the stored values (:69)."""
+    n_files = make_bin_dtypes(ref, rng) and 1
+    for name, topo, box, pdt, lo_hi in DTYPE_CASES:
+        size = int(np.prod(topo))
+        pos_in, data_in = [], []
+        gid = 0
+        for r in range(size):
+            n = int(rng.integers(50, 400))
+            pos_in.append(_dtype_positions(rng, n, box, pdt, lo_hi))
+            data_in.append(np.arange(gid, gid + n, dtype=np.int64))
+            gid += n
+        pos_work = [p.copy() for p in pos_in]
+        cell_pos = [p.copy() for p in pos_in]
+
+        def fn(comm, r):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            with np.errstate(all="ignore"):
+                cell = R.get_cell_number_from_position(cell_pos[r])
+                out = R.redistribute_by_position(data_in[r], pos_work[r])
+            return cell, out
+
+        res = run_ranks(size, fn)
+        f = {"topology": np.asarray(topo, dtype=np.int64), "box": np.asarray(box),
+             "size": np.int64(size), "periodic": np.bool_(True), "alias": np.bool_(False)}
+        for r in range(size):
+            f[f"r{r}_pos_in"] = pos_in[r]
+            f[f"r{r}_pos_out"] = pos_work[r]
+            f[f"r{r}_data"] = data_in[r]
+            f[f"r{r}_cell"] = res[r][0]
+            f[f"r{r}_out"] = res[r][1]
+        np.savez_compressed(os.path.join(OUT_DIR, f"redist_{name}.npz"), **f)
+        n_files += 1
+    # halo with int32 positions: the float64 comparisons of :271-276
+    topo, box, ol = [2, 2, 1], [100, 100, 10], [6.5, 12.0, 1.0]
+    size = 4
+    pos_in, data_in = [], []
+    for r in range(size):
+        n = int(rng.integers(60, 300))
+        pos_in.append(_dtype_positions(rng, n, box, np.int32, (-0.2, 1.2)))
+        data_in.append(rng.normal(size=(n, 2)))
+    pos_work = [p.copy() for p in pos_in]
+
+    def fnh(comm, r):
+        R = ref.MPIGridRedistributor(comm, topo, box)
+        with np.errstate(all="ignore"):
+            return R.redistribute_by_position(data_in[r], pos_work[r], overload_lengths=ol)
+
+    res = run_ranks(size, fnh)
+    f = {"topology": np.asarray(topo, dtype=np.int64), "box": np.asarray(box),
+         "size": np.int64(size), "overload": np.asarray(ol, dtype=np.float64)}
+    for r in range(size):
+        f[f"r{r}_pos_in"] = pos_in[r]
+        f[f"r{r}_pos_out"] = pos_work[r]
+        f[f"r{r}_data"] = data_in[r]
+        f[f"r{r}_out"] = res[r]
+    np.savez_compressed(os.path.join(OUT_DIR, "halo_p4_i32pos.npz"), **f)
+    return n_files + 1
+
+
 def main():
     ref = load_reference()
     only = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if only in ("all", "dtypes"):
+        d = make_dtypes(ref, np.random.default_rng(20261018))
+        print(f"position-dtype fixtures: {d}")
     if only in ("all", "redist"):
         rng = np.random.default_rng(20261015)
         a = make_bin_edges(ref, rng)

@@ -124,6 +124,82 @@ def test_scan_failure_is_loud():
     assert (counts.cpu().numpy() > 0).all()
 
 
+class _Hooks:
+    """Set test hooks for a block, back to the shipped defaults after it."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            _lib.test_hook(k, v)
+
+    def __exit__(self, *exc):
+        for k in self.kw:
+            _lib.test_hook(k, _lib.HOOK_DEFAULTS[k])
+
+
+# ~2000 x s_sleep(127) = several ms: far longer than the rest of the scan
+_LATE = 2000
+
+
+@pytest.mark.parametrize("bin_", [0, 5])
+def test_scan_race_cfg2_late_inclusive_word(bin_):
+    """The round-4 scan race, forced (scan_delay_bin): in the 8-bin config-2
+    scan (2^26 rows, 512-row tiles, 64 chunks per bin) the chunk that ends bin
+    b counts itself done several ms before it stores its inclusive word --
+    the order relaxed atomics on two words allow.  The last chunk polls the
+    bin-end words, so counts and the whole partition stay exact against the
+    C oracle (redist.py:195-198 counts).  With one look at those words
+    (scan_end_spins = 0: the pre-fix reader) the same interleaving shows up as
+    a failed scan: the test does produce the race."""
+    from oracle import c_oracle
+    n = 1 << 26
+    pos0, _ = mgr.synth_uniform(n, seed=20261015)
+    pos_h = pos0.cpu().numpy()
+    cell = c_oracle.bin_positions(pos_h.copy(), [2, 2, 2], [1.0] * 3)
+    exp, exp_off = c_oracle.partition(np.arange(n, dtype=np.int64), cell, 8)
+    ids = torch.arange(n, dtype=torch.int64, device="cuda").view(torch.uint8)
+    P = GridPartitioner([2, 2, 2], [1.0] * 3)
+    with _Hooks(scan_delay_bin=bin_, scan_delay_sleeps=_LATE):
+        out, counts = P.partition_device(ids, 8, pos0.clone())
+        torch.cuda.synchronize()
+        assert np.array_equal(counts.cpu().numpy(), np.diff(exp_off))
+        assert np.array_equal(out[: 8 * n].view(torch.int64).cpu().numpy(), exp)
+    with _Hooks(scan_delay_bin=bin_, scan_delay_sleeps=_LATE, scan_end_spins=0):
+        out, counts = P.partition_device(ids, 8, pos0.clone())
+        c = counts.cpu().numpy()
+    assert c[bin_] == -1 and c[bin_ + 1] == -1, c      # the late word was seen
+    out, counts = P.partition_device(ids, 8, pos0.clone())   # defaults again
+    assert np.array_equal(counts.cpu().numpy(), np.diff(exp_off))
+
+
+@pytest.mark.parametrize("bin_", [0, 300])
+def test_scan_race_fine_late_inclusive_word(bin_):
+    """The same forced race in the config-5 destination scan: 512 fine cells x
+    16384 ranked tiles (2^26 ids, 2 chunks per bin, 8192 counts per chunk):
+    counts and the stable sort exact against numpy's stable argsort."""
+    from mpi_grid_redistribute_amd.redistributor import _IdField, _sort_by_ids
+    n, nb = 1 << 26, 512
+    rng = np.random.default_rng(bin_)
+    ids_h = rng.integers(0, nb, n).astype(np.uint16)
+    ids = torch.from_numpy(ids_h.view(np.int16)).cuda()
+    rows = _IdField(torch.arange(n, dtype=torch.int32, device="cuda").view(torch.uint8))
+    rows.row_bytes = 4
+    order = np.argsort(ids_h, kind="stable").astype(np.int32)
+    cnt = np.bincount(ids_h, minlength=nb)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    with _Hooks(scan_delay_bin=bin_, scan_delay_sleeps=_LATE):
+        outs, counts = _sort_by_ids([rows], ids, n, nb, dev, check_ids=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(counts.cpu().numpy(), cnt)
+        assert np.array_equal(outs[0][: 4 * n].view(torch.int32).cpu().numpy(), order)
+    with _Hooks(scan_delay_bin=bin_, scan_delay_sleeps=_LATE, scan_end_spins=0):
+        _, counts = _sort_by_ids([rows], ids, n, nb, dev, check_ids=False)
+        c = counts.cpu().numpy()
+    assert c[bin_] == -1 and c[bin_ + 1] == -1
+
+
 def test_single_rank_scan_failure_raises():
     pos, rec = mgr.synth_uniform(1 << 20, seed=6)
     R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)

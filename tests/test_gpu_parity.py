@@ -37,8 +37,12 @@ def _gpu():
 
 
 # ------------------------------------------------------------ binning
-def test_bin_edges_golden_numpy():
-    f = G.load("bin_edges.npz")
+EDGE_FILES = ["bin_edges.npz", "bin_dtypes.npz"]   # f32/f64; int32/int64/f16 (+ narrow boxes)
+
+
+@pytest.mark.parametrize("edges", EDGE_FILES)
+def test_bin_edges_golden_numpy(edges):
+    f = G.load(edges)
     for key in G.bin_edge_keys(f):
         n = int(f[key + "_n"])
         periodic = not key.endswith("nonperiodic")
@@ -53,8 +57,9 @@ def test_bin_edges_golden_numpy():
         assert np.array_equal(cell, f[key + "_cell"]), key
 
 
-def test_bin_edges_golden_torch():
-    f = G.load("bin_edges.npz")
+@pytest.mark.parametrize("edges", EDGE_FILES)
+def test_bin_edges_golden_torch(edges):
+    f = G.load(edges)
     for key in G.bin_edge_keys(f):
         n = int(f[key + "_n"])
         periodic = not key.endswith("nonperiodic")
@@ -84,6 +89,80 @@ def test_bin_random_vs_c_oracle(dt, boxdt):
     assert G.same_bytes(got.cpu().numpy(), exp)
     assert np.array_equal(cell.cpu().numpy(), cell_exp)
     assert np.array_equal(idx.cpu().numpy(), idx_exp)
+
+
+@pytest.mark.parametrize("dt,boxdt", [(np.int32, np.int64), (np.int64, np.int64),
+                                      (np.int32, np.float64), (np.int64, np.float32),
+                                      (np.int32, np.int16), (np.float16, np.float64),
+                                      (np.float16, np.float32), (np.float16, np.float16),
+                                      (np.float16, np.int8), (np.float16, np.int64),
+                                      (np.float32, np.int16), (np.float32, np.float16)])
+def test_bin_position_dtypes_vs_c_oracle(dt, boxdt):
+    """int32 / int64 / float16 positions (and float32 against narrow boxes)
+    over 300k rows, every numpy promotion of :68-69 -- against the C
+    restatement (pinned by bin_dtypes.npz), through the GPU API and the
+    redistribution's own binning kernel (mgr_bin_count)."""
+    rng = np.random.default_rng(sum(map(ord, np.dtype(dt).str + np.dtype(boxdt).str)))
+    topo = [3, 5, 2]
+    box = np.array([14, 6, 100]).astype(boxdt) if np.dtype(boxdt).kind in "iu" else \
+        np.array([0.7, 6.5, 3.0]).astype(boxdt)
+    n = 300_000
+    b64 = box.astype(np.float64)
+    raw = rng.uniform(-3, 4, (n, 3)) * b64
+    raw[::13] = rng.uniform(0, 1, (len(raw[::13]), 3)) * b64
+    if np.dtype(dt).kind == "i":
+        raw = np.floor(raw * (8 if b64.min() < 10 else 1))
+        raw[::101] = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, (len(raw[::101]), 3))
+    with np.errstate(all="ignore"):
+        pos = raw.astype(dt)
+    exp = pos.copy()
+    cell_exp, idx_exp = c_oracle.bin_positions(exp, topo, box, want_idx=True)
+    R = MPIGridRedistributor(SizedComm(30), topo, box)
+    got = torch.from_numpy(pos.copy()).cuda()
+    idx = R.get_cell_indexes_from_position(got.clone())
+    cell = R.get_cell_number_from_position(got)
+    assert G.same_bytes(got.cpu().numpy(), exp), G.diff_report(got.cpu().numpy(), exp)
+    assert np.array_equal(cell.cpu().numpy(), cell_exp)
+    assert np.array_equal(idx.cpu().numpy(), idx_exp)
+    # the hot path's binning kernel on the same rows: one rank, 30 virtual cells
+    P = GridPartitioner(topo, box)
+    gp = torch.from_numpy(pos.copy()).cuda()
+    data = torch.arange(n, dtype=torch.int64, device="cuda")
+    out, off = P.partition_by_position(data, gp)
+    assert G.same_bytes(gp.cpu().numpy(), exp)
+    order = np.argsort(cell_exp, kind="stable")
+    assert np.array_equal(out.cpu().numpy(), order)
+    assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(cell_exp, minlength=30))
+
+
+@pytest.mark.parametrize("dt", [np.float16, np.int32])
+def test_fine_cells_position_dtypes(dt):
+    """redistribute_by_position(fine_cells=...) with float16 / int32 positions:
+    the fine ids come from the same bin pass (kSideFine of bin_coord_ext)."""
+    rng = np.random.default_rng(31)
+    size, topo, fine = 2, [2, 1, 1], [4, 2, 3]
+    box = [2.0, 1.0, 1.0] if dt == np.float16 else [64, 32, 48]
+    pos = [(rng.uniform(-0.2, 1.2, (3000 + 100 * r, 3)) * np.asarray(box, dtype=np.float64))
+           .astype(dt) for r in range(size)]
+    data = [np.arange(len(p), dtype=np.int64) + 100_000 * r for r, p in enumerate(pos)]
+    pos_o = [p.copy() for p in pos]
+    plain = ro.redistribute_by_position_all_ranks(topo, box, size, data, pos_o)
+    plain_pos = ro.redistribute_by_cell_number_all_ranks(
+        size, pos_o, [ro.cell_number_from_position(ro.Geometry(topo, box, size), p.copy())
+                      for p in pos_o])
+
+    def fn(comm, r):
+        R = MPIGridRedistributor(comm, topo, box)
+        return R.redistribute_by_position(data[r], pos[r], fine_cells=fine)
+
+    outs = run_ranks(size, fn)
+    nfine = int(np.prod(fine))
+    for r in range(size):
+        fid = ro.fine_cell_ids(topo, fine, box, plain_pos[r])
+        exp, exp_off = ro.fine_cell_sort(plain[r], fid, nfine)
+        assert G.same_bytes(pos[r], pos_o[r])
+        assert G.same_bytes(outs[r][0], exp), r
+        assert np.array_equal(outs[r][1], exp_off), r
 
 
 def test_cell_number_from_indexes():

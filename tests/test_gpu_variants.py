@@ -25,6 +25,8 @@ VARIANTS = [
     {"tile_rounds": 1},
     {"tile_rounds": 8},
     {"tile_rounds": 16},
+    {"tile_rounds": 32},   # 2048-row tiles: the coop pack's largest
+    {"tile_rounds": 64},   # 4096-row tiles: coop / image packs refuse -> generic pack
     {"bin_generic": 1},
     {"bin_generic": 1, "write_back": "all"},
     {"write_back": "all"},

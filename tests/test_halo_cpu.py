@@ -43,6 +43,11 @@ class GeoRank:
         return ro.cell_number_from_indexes(self._g, idx, periodic=periodic)
 
 
+_POS_NP = {_lib.MGR_F16: np.dtype(np.float16), _lib.MGR_F32: np.dtype(np.float32),
+           _lib.MGR_F64: np.dtype(np.float64), _lib.MGR_I32: np.dtype(np.int32),
+           _lib.MGR_I64: np.dtype(np.int64)}
+
+
 class CpuSelect:
     """NumPy stand-in for halo.DeviceSelect (mgr_halo_flags / mgr_msel_count
     / mgr_scan / mgr_msel_pack)."""
@@ -51,7 +56,7 @@ class CpuSelect:
         return torch.empty(max(int(nbytes), 1), dtype=torch.uint8)
 
     def flags(self, pos_flat, n, ncols, code, dim, hi, lo):
-        dt = np.float32 if code == _lib.MGR_F32 else np.float64
+        dt = _POS_NP[code]
         p = pos_flat.numpy().view(dt).reshape(n, ncols).astype(np.float64)
         f = np.zeros(n, dtype=np.uint16)
         for d in range(dim):
@@ -120,7 +125,7 @@ def run_rank(f, case, transport, r, spare=None, carry_pos=True):
     data, pos, periodic = local_inputs(f, case)
     R = GeoRank(f["topology"], f["box"], size, r)
     d, p = data[r], pos[r]
-    code = _lib.MGR_F32 if p.dtype == np.float32 else _lib.MGR_F64
+    code = {v: k for k, v in _POS_NP.items()}[p.dtype]
     rbd = d.dtype.itemsize * int(np.prod(d.shape[1:], dtype=np.int64))
     rbp = p.dtype.itemsize * p.shape[1]
     n = len(d)

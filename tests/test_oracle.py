@@ -13,9 +13,11 @@ from oracle import redist_oracle as ro
 from tests import golden_io as G
 
 
-@pytest.fixture(scope="module")
-def edges():
-    return G.load("bin_edges.npz")
+# bin_edges: float32/float64 positions; bin_dtypes: int32/int64/float16
+# positions (and float32 against narrow boxes) over every box dtype
+@pytest.fixture(scope="module", params=["bin_edges.npz", "bin_dtypes.npz"])
+def edges(request):
+    return G.load(request.param)
 
 
 def _box_for(f, key):
