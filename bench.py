@@ -105,6 +105,52 @@ def xgmi_report(traffic, exch, dist, world, chunks):
     return out
 
 
+RCCL_LOG_PREFIX = "/tmp/mgr_bench_rccl"
+
+
+def rccl_log_env(environ):
+    """N > 1: RCCL's connection lines ("Channel 00/0 : 0[0] -> 1[1] via
+    P2P/IPC") to a per-process file, so the record can name the transport
+    RCCL chose (init-time logging only; the caller's own NCCL_DEBUG wins)."""
+    if "NCCL_DEBUG" in environ:
+        return None
+    path = f"{RCCL_LOG_PREFIX}.{os.getpid()}.log"
+    environ["NCCL_DEBUG"] = "INFO"
+    environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,SHM,NET"
+    environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def rccl_transports(text):
+    """Transports named by RCCL's connection lines: 'P2P/IPC', 'SHM/direct',
+    'NET/Socket', ... (the first two fields after 'via')."""
+    import re
+    out = set()
+    for m in re.finditer(r" via ([A-Za-z0-9_]+)(/[A-Za-z0-9_]+)?", text):
+        out.add(m.group(1) + (m.group(2) or ""))
+    return sorted(out)
+
+
+def rccl_block(info, transports, world):
+    """The scaling record's RCCL facts: versions (built against / loaded),
+    the library path, ranks as RCCL counts them (must equal the world size)
+    and the transports its connections use (P2P/IPC = xGMI on one node)."""
+    return {"version_compiled": info["version_compiled"],
+            "version_runtime": info["version_runtime"], "library": info["library"],
+            "nranks": info["nranks"], "nranks_ok": info["nranks"] == world,
+            "transports": transports}
+
+
+def exchange_ab_block(pipelined_ms, chunks, one_message_ms, steps):
+    """The pipelined exchange (the product default at > 1 rank, chunks per
+    peer) against one message per peer, same inputs, same ranks: the second
+    timed in an untimed pass after the region."""
+    return {"pipelined_ms_per_step": pipelined_ms, "chunks": chunks,
+            "one_message_ms_per_step": one_message_ms, "one_message_steps": steps,
+            "pipelined_speedup": (one_message_ms / pipelined_ms) if pipelined_ms > 0 else None,
+            "in_timed_region": False}
+
+
 def _m(n):
     """Workload size label: 2^26 -> 64M, 125_000_000 -> 125M."""
     return f"{n >> 20}M" if n % (1 << 20) == 0 else f"{n / 1e6:g}M"
@@ -246,6 +292,7 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     multi = world > 1 or args.exchange
+    rccl_log = rccl_log_env(os.environ) if world > 1 else None
     if multi:
         import torch.distributed as dist
         if world == 1:   # --exchange without a launcher: a one-rank group
@@ -408,6 +455,35 @@ def main():
     xgmi = None
     if multi and "exchange" in kernels:
         xgmi = xgmi_report(R.last_traffic, kernels["exchange"], dist, world, chunks)
+    rccl, exchange_ab = None, None
+    if multi and world > 1:
+        # untimed: one message per peer (exchange_chunks = 1) on the same
+        # inputs, beside the pipelined steps of the timed region
+        R.exchange_chunks = 1
+        for _ in range(2):
+            step()
+        barrier()
+        k1 = min(args.steps, 10)
+        t1 = time.perf_counter()
+        for _ in range(k1):
+            step()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        R.exchange_chunks = args.chunks or None
+        exchange_ab = exchange_ab_block(elapsed / args.steps * 1e3, chunks,
+                                        float(t.item()) / k1 * 1e3, k1)
+        mine = []
+        if rccl_log:
+            try:
+                with open(rccl_log) as f:
+                    mine = rccl_transports(f.read())
+                os.remove(rccl_log)
+            except OSError:
+                mine = []
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        rccl = rccl_block(comm.rccl_info(), sorted({x for e in every for x in e}), world)
     # per-kernel algorithmic bytes per launch: per-row figure x the rows one
     # launch processes (n: every launch of these kernels covers this rank's
     # rows -- received rows at N > 1 are ~n for the uniform inputs), or the
@@ -452,6 +528,8 @@ def main():
             "roofline": roofline,
             "kernels": kernels,
             "xgmi": xgmi,
+            "rccl": rccl,
+            "exchange_ab": exchange_ab,
             "count_skew": skew,
             "cpu_baseline": cpu,
             "cpu_baseline_cfg1": cpu_1,

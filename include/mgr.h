@@ -78,9 +78,8 @@ const char* mgr_version(void);
  * float32, with a float64 / int32 / int64 box in float64 (S9, S11a); integer
  * positions with an integer box wrap in integer arithmetic.  Integer box
  * lengths are passed as doubles and must be integral with |L| < 2^53.
- * nbins = number of
- * destinations = comm size (redist.py:42, :196); cells >= nbins are invalid
- * (redist.py:43-44 asserts prod(topology) <= size).                        */
+ * nbins = number of destinations = comm size (redist.py:42, :196); cells >=
+ * nbins are invalid (redist.py:43-44 asserts prod(topology) <= size).      */
 int mgr_plan_create(int dim, const int64_t* grid_topology, const double* box_length,
                     int box_dtype, int nbins, mgr_plan** out);
 /* Fine-cell plan (BASELINE config 5): the destination-side
@@ -226,7 +225,9 @@ int mgr_tile_offsets(const void* workspace, int64_t n, int nbins, int tile_rows,
  *                of its id inside its tile (ranks, uint16 [n]), every tile's
  *                start of each id inside the tile (tile_starts, uint16
  *                [ceil(n / tile_rows)][nbins]), and the tile histogram in the
- *                workspace for mgr_scan (tile_rows: a multiple of 256, <= 4096).
+ *                workspace for mgr_scan (nbins <= 2048; tile_rows =
+ *                mgr_ranked_tile_rows(...), i.e. 2048 or 4096; MGR_EINVAL
+ *                otherwise).
  * mgr_pack_ranked: the stable partition of n rows of row_bytes by those ids
  *                (after mgr_scan), each row placed at tile_start + rank --
  *                no ranking in the pack.  Rows of 4-byte multiples <= 64 B,
@@ -322,6 +323,16 @@ int mgr_comm_create(const void* id, int nranks, int rank, mgr_comm** out);
 int mgr_comm_destroy(mgr_comm* comm);
 int mgr_comm_rank(const mgr_comm* comm);
 int mgr_comm_size(const mgr_comm* comm);
+/* Ranks in the communicator as RCCL itself counts them (ncclCommCount), < 0
+ * on error: the scaling record checks it against the world size.          */
+int mgr_comm_count(const mgr_comm* comm);
+/* RCCL versions (major*10000 + minor*100 + patch): the headers libmgr.so was
+ * built with, and the library loaded in this process (ncclGetVersion; in a
+ * torch process, torch's bundled RCCL).  Host only.  mgr_comm_create refuses
+ * a runtime of another major version or older than 2.18 (MGR_ERCCL, both
+ * versions in the message): the RCCL calls used keep their ABI within that
+ * range.                                                                   */
+int mgr_rccl_version(int* compiled, int* runtime);
 
 /* All-to-all of one int64 per peer (the count row): recv[s] = send_of_s[me]. */
 int mgr_exchange_counts(mgr_comm* comm, const int64_t* send_counts, int64_t* recv_counts,

@@ -70,6 +70,8 @@ SIGNATURES = {
     "mgr_comm_destroy": (_I, [_P]),
     "mgr_comm_rank": (_I, [_P]),
     "mgr_comm_size": (_I, [_P]),
+    "mgr_comm_count": (_I, [_P]),
+    "mgr_rccl_version": (_I, [ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "mgr_exchange_counts": (_I, [_P, _P, _P, _P]),
     "mgr_exchange_count_rows": (_I, [_P, _P, _P, _I, _P]),
     "mgr_exchange_rows": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
@@ -148,6 +150,13 @@ def check(rc, what=""):
 
 def call(name, *args):
     return check(getattr(load(), name)(*args), name)
+
+
+def rccl_version():
+    """(compiled, runtime) RCCL version codes (mgr_rccl_version)."""
+    c, r = ctypes.c_int(0), ctypes.c_int(0)
+    call("mgr_rccl_version", ctypes.byref(c), ctypes.byref(r))
+    return c.value, r.value
 
 
 def require_gpu():

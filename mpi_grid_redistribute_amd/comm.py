@@ -23,6 +23,7 @@ Implementations
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -185,6 +186,19 @@ class SelfComm(Transport):
         return  # the pack wrote the self segment into the output
 
 
+def loaded_rccl_path():
+    """Path of the librccl mapped into this process (/proc/self/maps), or None."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if len(line.split()) >= 6 else ""
+                if os.path.basename(p).startswith("librccl.so"):
+                    return p
+    except OSError:
+        pass
+    return None
+
+
 class RcclComm(Transport):
     """Native RCCL communicator (libmgr.so ``mgr_comm_*``), one process per GPU.
 
@@ -219,6 +233,19 @@ class RcclComm(Transport):
         obj = [cls.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
         return cls(obj[0], size, rank)
+
+    def rccl_info(self):
+        """What RCCL runs this communicator: the version codes libmgr.so was
+        built with and the library loaded in this process (in a torch process
+        torch's bundled RCCL; mgr_comm_create refused an incompatible one),
+        that library's path, and the ranks RCCL itself counts (ncclCommCount)
+        -- the first things to check on a scaling record."""
+        compiled, runtime = _lib.rccl_version()
+        count = _lib.load().mgr_comm_count(self._h)
+        if count < 0:
+            _lib.check(count, "mgr_comm_count")
+        return {"version_compiled": compiled, "version_runtime": runtime,
+                "nranks": int(count), "library": loaded_rccl_path()}
 
     def close(self):
         if getattr(self, "_h", None):

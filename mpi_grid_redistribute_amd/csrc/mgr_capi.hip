@@ -485,9 +485,12 @@ int mgr_rank_ids(const uint16_t* ids, int64_t n, int nbins, int tile_rows, uint1
                  uint16_t* tile_starts, uint32_t* bad_ids, void* workspace, void* stream) {
     int rc = check_tile(tile_rows);
     if (rc) return rc;
-    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
-    if (tile_rows % (64 * mgr::kWaves) || tile_rows > 4096)
-        return fail(MGR_EINVAL, "tile_rows %d: a multiple of 256 <= 4096", tile_rows);
+    // the ranked tiles only (mgr_ranked_tile_rows: 2048 or 4096 rows, <= 2048
+    // ids: the per-wave LDS peer words); anything else is refused here, not
+    // by the launch
+    if (nbins < 1 || nbins > 2048) return fail(MGR_EINVAL, "nbins %d not in [1, 2048]", nbins);
+    if (tile_rows != 2048 && tile_rows != 4096)
+        return fail(MGR_EINVAL, "tile_rows %d: 2048 or 4096 (mgr_ranked_tile_rows)", tile_rows);
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (n > 0 && (!ids || !ranks || !tile_starts || !workspace)) return fail(MGR_EINVAL, "null argument");
     const mgr::Workspace ws = mgr::carve(workspace, n, nbins, tile_rows);
@@ -682,9 +685,41 @@ int mgr_comm_unique_id(void* out_id) {
     return MGR_OK;
 }
 
+int mgr_rccl_version(int* compiled, int* runtime) {
+    if (compiled) *compiled = NCCL_VERSION_CODE;
+    if (runtime) {
+        int v = 0;
+        NCCL_OK(ncclGetVersion(&v));
+        *runtime = v;
+    }
+    return MGR_OK;
+}
+
+// The RCCL calls this library makes (ncclGetUniqueId, ncclCommInitRank,
+// ncclSend / ncclRecv, ncclGroupStart / End, ncclAllReduce, ncclCommCount,
+// ncclCommDestroy) keep their signatures and enum values throughout RCCL 2.x
+// from 2.18 on; torch bundles its own RCCL (2.26 in this image) which a torch
+// process has already loaded when libmgr.so binds, while the headers are
+// ROCm's (2.27).  So the runtime must have the compiled major version and be
+// at least kMinRccl -- anything else is refused with the two versions named,
+// never run on an unmatched ABI.
+static constexpr int kMinRccl = 21800;
+static int rccl_check() {
+    int rt = 0;
+    NCCL_OK(ncclGetVersion(&rt));
+    if (rt / 10000 != NCCL_VERSION_CODE / 10000 || rt < kMinRccl)
+        return fail(MGR_ERCCL, "RCCL runtime %d.%d.%d is not compatible with the %d.%d.%d headers "
+                    "libmgr.so was built with (needs %d.x >= %d.%d)", rt / 10000, rt / 100 % 100,
+                    rt % 100, NCCL_MAJOR, NCCL_MINOR, NCCL_PATCH, NCCL_MAJOR, kMinRccl / 10000,
+                    kMinRccl / 100 % 100);
+    return MGR_OK;
+}
+
 int mgr_comm_create(const void* id, int nranks, int rank, mgr_comm** out) {
     if (!id || !out) return fail(MGR_EINVAL, "null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(MGR_EINVAL, "rank %d of %d", rank, nranks);
+    int rc = rccl_check();
+    if (rc) return rc;
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof uid);
     ncclComm_t c;
@@ -707,6 +742,13 @@ int mgr_comm_destroy(mgr_comm* comm) {
 
 int mgr_comm_rank(const mgr_comm* comm) { return comm ? comm->rank : -1; }
 int mgr_comm_size(const mgr_comm* comm) { return comm ? comm->size : -1; }
+
+int mgr_comm_count(const mgr_comm* comm) {
+    if (!comm) return fail(MGR_EINVAL, "null comm");
+    int c = 0;
+    NCCL_OK(ncclCommCount(comm->nccl, &c));
+    return c;
+}
 
 // An RCCL group that always closes: the first failing call inside it is
 // remembered and ncclGroupEnd still runs, so a failure never leaves the

@@ -140,3 +140,61 @@ def test_msel_validation(lib):
     assert lib.mgr_msel_pack(None, 8, 5, p, 2, bits, 4096, p, p, None) < 0  # null source
     assert b"null" in lib.mgr_last_error()
     assert lib.mgr_msel_pack(None, 8, 0, None, 2, bits, 4096, None, None, None) == 0  # empty
+
+
+def test_rank_ids_contract(lib):
+    """mgr_rank_ids takes the ranked tiles only (mgr_ranked_tile_rows: 2048 or
+    4096 rows, <= 2048 ids): other shapes are refused before any launch."""
+    buf = ctypes.create_string_buffer(256)
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    for tr in (256, 512, 1024, 3072):
+        assert lib.mgr_rank_ids(p, 5, 512, tr, p, p, None, p, None) == -1, tr
+        assert b"tile_rows" in lib.mgr_last_error()
+    assert lib.mgr_rank_ids(p, 5, 2049, 4096, p, p, None, p, None) == -1
+    assert b"nbins" in lib.mgr_last_error()
+    assert lib.mgr_rank_ids(p, 0, 512, 4096, p, p, None, p, None) == 0   # empty: no launch
+
+
+def test_position_and_box_dtypes(lib):
+    """Every box dtype code makes a plan; positions take float16/32/64 and
+    int32/64 only; an integer box must hold integers below 2^53."""
+    import numpy as np
+    from mpi_grid_redistribute_amd import _lib
+    topo = np.array([2], dtype=np.int64)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    h = ctypes.c_void_p()
+    for code in range(1, 12):
+        assert lib.mgr_plan_create(1, vp(topo), vp(np.array([4.0])), code, 2, ctypes.byref(h)) == 0
+        buf = ctypes.create_string_buffer(64)
+        p = ctypes.cast(buf, ctypes.c_void_p)
+        for pc in (_lib.MGR_I8, _lib.MGR_U16, 0, 12):
+            assert lib.mgr_bin_count(h, p, pc, 4, 1, 1, p, 64, p, None) == -1
+            assert b"positions must be" in lib.mgr_last_error()
+        assert lib.mgr_bin_count(h, p, _lib.MGR_F16, 0, 1, 1, p, 64, p, None) == 0   # n = 0
+        assert lib.mgr_plan_destroy(h) == 0
+    assert lib.mgr_plan_create(1, vp(topo), vp(np.array([4.0])), 12, 2, ctypes.byref(h)) < 0
+    assert lib.mgr_plan_create(1, vp(topo), vp(np.array([2.5])), _lib.MGR_I64, 2,
+                               ctypes.byref(h)) < 0
+    assert b"integer box_length" in lib.mgr_last_error()
+
+
+def test_box_dtype_codes():
+    import numpy as np
+    from mpi_grid_redistribute_amd import _lib
+    from mpi_grid_redistribute_amd._arrays import box_dtype_code, pos_code
+    exp = {np.float16: _lib.MGR_F16, np.float32: _lib.MGR_F32, np.float64: _lib.MGR_F64,
+           np.int8: _lib.MGR_I8, np.int16: _lib.MGR_I16, np.int32: _lib.MGR_I32,
+           np.int64: _lib.MGR_I64, np.uint8: _lib.MGR_U8, np.bool_: _lib.MGR_U8,
+           np.uint16: _lib.MGR_U16, np.uint32: _lib.MGR_U32, np.uint64: _lib.MGR_U64}
+    for dt, code in exp.items():
+        assert box_dtype_code(np.ones(3, dt)) == code, dt
+    assert box_dtype_code(np.array([1, 2])) == _lib.MGR_I64          # python ints (S11a)
+    with pytest.raises(TypeError):
+        box_dtype_code(np.ones(2, np.complex128))
+    with pytest.raises(NotImplementedError):
+        box_dtype_code(np.array([2 ** 60]))
+    for dt in (np.float16, np.float32, np.float64, np.int32, np.int64):
+        assert _lib.POS_ITEMSIZE[pos_code(dt)] == np.dtype(dt).itemsize
+    for dt in (np.int16, np.uint32, np.bool_):
+        with pytest.raises(TypeError):
+            pos_code(dt)

@@ -428,3 +428,49 @@ def test_bench_halo_pack_bytes_by_world():
     assert bench.row_bytes_per_kernel(3, True, world=1)["pack"] == 65
     assert bench.row_bytes_per_kernel(3, True, world=2)["pack"] == 69
     assert bench.row_bytes_per_kernel(3, False)["pack"] == 65
+
+
+def test_bench_scaling_record_schema():
+    """The N > 1 record checks itself: RCCL versions, library, ranks as RCCL
+    counts them, transports from RCCL's connection lines, and the one-message
+    exchange timed beside the pipelined one."""
+    import bench
+    env = {}
+    path = bench.rccl_log_env(env)
+    assert env["NCCL_DEBUG"] == "INFO" and env["NCCL_DEBUG_FILE"] == path
+    assert bench.rccl_log_env({"NCCL_DEBUG": "WARN"}) is None      # the caller's setting wins
+    log = ("host:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC/read\n"
+           "host:1:2 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC\n"
+           "host:1:2 [0] NCCL INFO Channel 00/1 : 1[0] -> 0[0] [send] via NET/Socket/0\n"
+           "host:1:2 [0] NCCL INFO comm 0x1 rank 0 nRanks 2\n")
+    assert bench.rccl_transports(log) == ["NET/Socket", "P2P/IPC"]
+    info = {"version_compiled": 22707, "version_runtime": 22606, "nranks": 8,
+            "library": "/x/librccl.so"}
+    r = bench.rccl_block(info, ["P2P/IPC"], 8)
+    assert set(r) == {"version_compiled", "version_runtime", "library", "nranks", "nranks_ok",
+                      "transports"}
+    assert r["nranks_ok"] and not bench.rccl_block(info, [], 4)["nranks_ok"]
+    ab = bench.exchange_ab_block(2.0, 4, 3.0, 10)
+    assert set(ab) == {"pipelined_ms_per_step", "chunks", "one_message_ms_per_step",
+                       "one_message_steps", "pipelined_speedup", "in_timed_region"}
+    assert ab["pipelined_speedup"] == 1.5 and ab["in_timed_region"] is False
+
+
+def test_rccl_runtime_version_is_the_loaded_library():
+    """mgr_rccl_version reports the headers libmgr.so was built with and the
+    RCCL this process loaded (torch's bundled one once torch is imported);
+    mgr_comm_create accepts only a runtime of the same major version, >= 2.18."""
+    import ctypes
+    from mpi_grid_redistribute_amd import _lib
+    from mpi_grid_redistribute_amd.comm import loaded_rccl_path
+    compiled, runtime = _lib.rccl_version()
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "include", "mgr.h")).read()
+    assert "mgr_rccl_version" in hdr
+    assert compiled == 22707                      # /opt/rocm/include/rccl/rccl.h NCCL_VERSION_CODE
+    path = loaded_rccl_path()
+    assert path is not None
+    v = ctypes.c_int(0)
+    assert ctypes.CDLL(path).ncclGetVersion(ctypes.byref(v)) == 0
+    assert runtime == v.value
+    assert runtime // 10000 == compiled // 10000 and runtime >= 21800
