@@ -34,13 +34,29 @@ class ExchangeLayout:
     redirect_self: bool
 
 
+# count-message sentinels: a scan whose look-back gave up reports -1 counts
+# (mgr_kernels.hip scan_onepass_kernel); the pipelined exchange sends -2 when
+# a rank's per-chunk counts do not add up to its scanned totals
+SCAN_FAILED, CHUNKS_INCONSISTENT = -1, -2
+
+
 def check_counts(send_counts, recv_counts):
-    """A failed device scan reports -1 counts (mgr_kernels.hip scan_onepass_kernel);
-    a peer's failure arrives here as a -1 receive count, so every rank raises
-    together instead of one rank leaving the others inside the exchange."""
-    if (np.asarray(send_counts) < 0).any() or (np.asarray(recv_counts) < 0).any():
-        raise MgrError("device scan failed (a look-back timed out on this rank or a peer): "
-                       f"send counts {list(send_counts)}, receive counts {list(recv_counts)}")
+    """A failure on this rank or a peer arrives as a negative count, so every
+    rank raises together instead of one rank leaving the others inside the
+    exchange; the message names the cause (-1: a look-back timed out, -2:
+    chunk counts that do not add up to the totals -- a wrong bin total)."""
+    sc, rc = np.asarray(send_counts), np.asarray(recv_counts)
+    if (sc >= 0).all() and (rc >= 0).all():
+        return
+    causes = []
+    if (sc == SCAN_FAILED).any() or (rc == SCAN_FAILED).any():
+        causes.append("device scan failed (a look-back timed out on this rank or a peer)")
+    if (sc == CHUNKS_INCONSISTENT).any() or (rc == CHUNKS_INCONSISTENT).any():
+        causes.append("pipelined exchange: chunk counts do not add up to the scanned totals "
+                      "on this rank or a peer (inconsistent scan offsets)")
+    if not causes:
+        causes.append("negative counts")
+    raise MgrError("; ".join(causes) + f": send counts {list(sc)}, receive counts {list(rc)}")
 
 
 def count_skew(matrix):
@@ -137,12 +153,15 @@ _COMM_STREAMS = {}
 
 def _comm_stream(device):
     """The side stream the pipelined exchange posts its row messages on: one
-    per device for the process (not one per call)."""
+    per (device, compute stream) for the process, not one per call -- calls on
+    different compute streams (the Scratch sets of redistributor.py) get
+    different comm streams, so neither queues behind the other's messages."""
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
-    st = _COMM_STREAMS.get(idx)
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+    st = _COMM_STREAMS.get(key)
     if st is None:
-        st = _COMM_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        st = _COMM_STREAMS[key] = torch.cuda.Stream(device=idx)
     return st
 
 
@@ -163,9 +182,10 @@ def exchange_pipelined(transport, row_bytes, bin_counts, rank, device, chunk_off
     every field (the self rows straight into the output, as exchange()'s
     pack).  One count message per peer carries [total, chunk 0, ..., chunk
     k-1] (k + 1 int64 each way, one group, ONE host sync per call), so every
-    receive is posted with its exact size.  A rank whose chunk counts do not
-    add up to its totals (or whose scan failed) sends -1 totals: every rank
-    then raises at the same point, before any row message is posted.  Output
+    receive is posted with its exact size.  A rank whose scan failed sends
+    -1 totals, one whose chunk counts do not add up to its totals -2: every
+    rank then raises at the same point, before any row message is posted,
+    naming the cause (check_counts).  Output
     bytes and order are exactly exchange()'s (receives in source-rank order,
     S7)."""
     size = transport.size
@@ -176,7 +196,9 @@ def exchange_pipelined(transport, row_bytes, bin_counts, rank, device, chunk_off
     cs_d = off[1:] - off[:-1]                                  # [chunk][peer] rows sent
     ok = (cs_d.sum(dim=0) == counts).all()
     msg = torch.empty((size, k + 1), dtype=torch.int64, device=dev)
-    msg[:, 0] = torch.where(ok, counts, torch.full_like(counts, -1))
+    # a failed scan keeps its -1; otherwise inconsistent chunks send -2
+    bad = torch.where(counts < 0, counts, torch.full_like(counts, CHUNKS_INCONSISTENT))
+    msg[:, 0] = torch.where(ok, counts, bad)
     msg[:, 1:] = cs_d.t()
     sh, rh = transport.exchange_count_rows(msg)
     for p in range(size):   # [total, k chunk counts] each way per peer

@@ -352,9 +352,10 @@ def test_rccl_schedule_order_and_self_copy():
 
 
 def _gloo_pipelined_bad_worker(rank, size, port, bad_rank):
-    """One rank's chunk offsets do not add up to its counts: it sends -1
+    """One rank's chunk offsets do not add up to its counts: it sends -2
     totals in the one count message, so EVERY rank raises there (none is left
-    waiting inside a row message)."""
+    waiting inside a row message), naming the inconsistent chunks -- not a
+    timed-out look-back (-1)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=size)
@@ -373,8 +374,9 @@ def _gloo_pipelined_bad_worker(rank, size, port, bad_rank):
             bad[3, 1] -= 1                     # and the totals no longer add up
             offs_fn = lambda: bad  # noqa: E731
         comm = TorchDistComm()
-        with pytest.raises(MgrError):
+        with pytest.raises(MgrError, match="chunk counts do not add up") as e:
             exchange_pipelined(comm, [rb], counts, rank, "cpu", offs_fn, pack_chunk, 3)
+        assert "look-back" not in str(e.value)
         comm.barrier()                          # every rank got here: nobody hangs
     finally:
         dist.destroy_process_group()
@@ -384,6 +386,20 @@ def _gloo_pipelined_bad_worker(rank, size, port, bad_rank):
 def test_gloo_pipelined_failure_agreed(size, bad_rank):
     mp.spawn(_gloo_pipelined_bad_worker, args=(size, _free_port(), bad_rank), nprocs=size,
              join=True)
+
+
+def test_check_counts_names_the_cause():
+    from mpi_grid_redistribute_amd._lib import MgrError
+    from mpi_grid_redistribute_amd.exchange import check_counts
+    check_counts([1, 2], [0, 3])
+    with pytest.raises(MgrError, match="look-back timed out") as e:
+        check_counts([-1, -1], [2, 3])
+    assert "chunk counts" not in str(e.value)
+    with pytest.raises(MgrError, match="chunk counts do not add up") as e:
+        check_counts([4, 5], [2, -2])
+    assert "look-back" not in str(e.value)
+    with pytest.raises(MgrError, match="look-back.*; pipelined"):
+        check_counts([-1, 5], [-2, 3])
 
 
 def test_count_skew_hand_built():
