@@ -4,6 +4,8 @@
 // and tile-size policy.  Helpers: mgr_device.h.
 #include "mgr_device.h"
 
+#include <algorithm>
+
 namespace mgr {
 
 
@@ -1107,6 +1109,263 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     }
 #undef MGR_PR
 #undef MGR_PRT
+    prof_end(s, K_PACK_FINE);
+    return e;
+}
+
+// ============================================================== sweep sort
+// The destination-side stable sort by fine cell in THREE light launches --
+// count_ranges (a 2-byte read per row), a scan of nbins x R counts, and
+// pack_sweep -- instead of rank_ids + a scan of nbins x T counts +
+// pack_ranked.  The tiles are dealt in R contiguous ranges, one per
+// workgroup of a persistent grid (R <= the CU count), and a workgroup walks
+// its range in order, so every bin's running output offset inside the range
+// lives in a register: the scan only needs each range's per-bin counts
+// (count_ranges), not per-tile ones, and no per-row rank, tile start or
+// per-tile offset ever leaves the chip.  pack_sweep ranks a tile's rows
+// itself (ballot match, per-wave counts in LDS), places them in the LDS image
+// and streams the image out as pack_ranked does.
+//
+// Why not a decoupled look-back across tiles: with one resident workgroup
+// per CU (the image fills the LDS) the workgroups run in lockstep, so a
+// tile's look-back finds its predecessors' aggregates but hardly ever an
+// inclusive prefix -- it would sum up to one word per concurrent workgroup
+// and bin, ~30 x 2 KB per 147 KB tile.  Owning a range removes the chain.
+constexpr int kSweepTR = 4096;   // sweep tiles (the ranked tiles' size)
+
+// Per-range counts: counts[b * R + r] = rows of id b in rows [r * range_rows,
+// (r + 1) * range_rows); ids >= nbins are clamped and reported through *bad
+// (as mgr_count_ids).  One 1024-thread workgroup per range, 8 ids per load.
+__global__ __launch_bounds__(1024) void count_ranges_kernel(const uint16_t* __restrict__ ids,
+                                                            int64_t n, int nbins, int64_t range_rows,
+                                                            int64_t R, int32_t* __restrict__ counts,
+                                                            uint64_t* __restrict__ scan_flags,
+                                                            uint32_t* __restrict__ bad) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    int32_t* hist = (int32_t*)smem;
+    clear_scan_flags(scan_flags);
+    const int64_t r = blockIdx.x;
+    for (int b = threadIdx.x; b < nbins; b += 1024) hist[b] = 0;
+    __syncthreads();
+    const int64_t row0 = r * range_rows;
+    const int64_t rows = min(range_rows, n - row0);
+    const uint16_t* p = ids + row0;
+    const bool vec = ((uintptr_t)p & 15) == 0;
+    bool oob = false;
+    auto add = [&](unsigned v) {
+        if (v >= (unsigned)nbins) { v = nbins - 1; oob = true; }
+        atomicAdd(&hist[v], 1);
+    };
+    for (int64_t i = 8 * (int64_t)threadIdx.x; i < rows; i += 8 * 1024) {
+        if (vec && i + 8 <= rows) {
+            const uint4 q = *(const uint4*)(p + i);
+            add(q.x & 0xffffu); add(q.x >> 16); add(q.y & 0xffffu); add(q.y >> 16);
+            add(q.z & 0xffffu); add(q.z >> 16); add(q.w & 0xffffu); add(q.w >> 16);
+        } else {
+            for (int64_t j = i; j < min(i + 8, rows); ++j) add(p[j]);
+        }
+    }
+    if (__any(oob) && lane_id() == 0 && bad) atomicOr(bad, 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbins; b += 1024) counts[(int64_t)b * R + r] = hist[b];
+}
+
+// The stable sort of one field by the ids, range r per workgroup (see above).
+// offsets[b * R + r] (mgr_scan over count_ranges' counts) = the first output
+// row of bin b's rows of range r.  LDS: the tile image [TR * RB], then a
+// table region -- per-wave bin counts u16 [NW][nb] while ranking, the image
+// rows' bins u16 [TR] and per-bin output addresses u64 [nb] while storing --
+// and, while the image is empty, the bins' tile starts inside it.
+template <int RB, int TR>
+__global__ __launch_bounds__(1024) void pack_sweep_kernel(
+    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids, int nb,
+    const int64_t* __restrict__ offsets, int64_t R, int64_t range_rows, int tab_bytes,
+    uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
+    static_assert(RB % 4 == 0 && RB <= 64, "sweep row size");
+    constexpr int NW = kFineWaves, RPW = TR / 64 / NW, NDW = RB / 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t* img = (uint32_t*)smem;
+    uint8_t* tabp = smem + align16(TR * RB);
+    uint16_t* tab = (uint16_t*)tabp;                                   // ranking: [NW][nb]
+    uint16_t* ibin = (uint16_t*)tabp;                                  // storing: [TR]
+    unsigned long long* gaddr = (unsigned long long*)(tabp + align16(TR * 2));   // [nb]
+    int* wsum = (int*)smem;                                            // in the empty image
+    uint32_t* tstart = (uint32_t*)(smem + 64);
+    if (scan_failed(scan_err)) return;
+    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const int64_t r = blockIdx.x;
+    const int64_t tpr = range_rows / TR;                               // tiles per range
+    const int64_t T = (n + TR - 1) / TR;
+    const int64_t t0 = r * tpr, t1 = min(T, t0 + tpr);
+    if (t0 >= t1) return;
+    const bool binner = tid < nb;                                      // thread b owns bin b
+    long long run = binner ? offsets[(int64_t)tid * R + r] : 0;        // bin's next output row
+    struct Set {
+        uint32_t v[RPW][NDW];
+        unsigned b[RPW];
+    };
+    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        t = min(t, t1 - 1);
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
+            S.b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));     // >= nb: clamped (count_ranges reports)
+            load_row_dw<NDW>(src + row * RB, S.v[q]);
+        }
+    };
+    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+        const int tr = (int)min((int64_t)TR, n - t * TR);
+        {   // zero the per-wave counts (16-byte stores)
+            typedef unsigned int z4_t __attribute__((ext_vector_type(4)));
+            for (int i = tid; i < tab_bytes / 16; i += 1024) ((z4_t*)tabp)[i] = z4_t{0u, 0u, 0u, 0u};
+        }
+        __syncthreads();
+        // rank: wave w holds rows [w * RPW * 64, (w + 1) * RPW * 64) of the
+        // tile in round order, so (wave, round, lane) is the row order and a
+        // ballot rank plus the wave's running count of the bin is stable
+        unsigned rk[RPW];
+        uint16_t* tw = tab + w * nb;
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const bool valid = (w * RPW + q) * 64 + lane < tr;
+            const unsigned long long peers = match_bin_t<9>(S.b[q], valid, 9);
+            const int rr = rank_in(peers);
+            const unsigned before = valid ? tw[S.b[q]] : 0u;
+            wave_sync();
+            if (valid && rr == 0) tw[S.b[q]] = (uint16_t)(before + __popcll(peers));
+            wave_sync();
+            rk[q] = before + rr;
+        }
+        __syncthreads();
+        // per bin: the waves' counts -> each wave's base inside the bin (in
+        // place), the tile count; a block scan over the bins -> tile starts
+        int cnt = 0;
+        if (binner) {
+#pragma unroll
+            for (int v = 0; v < NW; ++v) {
+                const int c = tab[v * nb + tid];
+                tab[v * nb + tid] = (uint16_t)cnt;
+                cnt += c;
+            }
+        }
+        const int incl = wave_incl_dpp(cnt);
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        int wpre = 0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) wpre += v < w ? wsum[v] : 0;
+        const int ts = wpre + incl - cnt;
+        long long delta = 0;
+        if (binner) {
+            tstart[tid] = (uint32_t)ts;
+            delta = run - ts;          // image row i of bin b -> output row i + delta
+            run += cnt;
+        }
+        __syncthreads();
+        int slot[RPW];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q)
+            slot[q] = (int)(tstart[S.b[q]] + tab[w * nb + S.b[q]] + rk[q]);
+        __syncthreads();   // the image and the table region are rewritten below
+        if (binner) gaddr[tid] = (unsigned long long)(dst + delta * (long long)RB);
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            if ((w * RPW + q) * 64 + lane < tr) {
+#pragma unroll
+                for (int i = 0; i < NDW; ++i) img[slot[q] * NDW + i] = S.v[q][i];
+                ibin[slot[q]] = (uint16_t)S.b[q];
+            }
+        }
+        __syncthreads();
+        const int nbytes = tr * RB;
+        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
+            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
+            const int bf = ibin[x / RB];
+            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
+                gstore<u32x4_a4>(gaddr[bf] + x, q);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
+                }
+            }
+        }
+        __syncthreads();   // the image and the table region are reused by the next tile
+    };
+    Set A, B;
+    int64_t t = t0;
+    load(A, t);
+    for (;;) {
+        load(B, t + 1);
+        process(A, t);
+        if (++t >= t1) break;
+        load(A, t + 1);
+        process(B, t);
+        if (++t >= t1) break;
+    }
+}
+
+// LDS of pack_sweep: the image and the table region (ranking counts, or the
+// image rows' bins and the per-bin output addresses).
+static int sweep_tab_bytes(int tile_rows, int nbins) {
+    return align16(std::max(kFineWaves * nbins * 2, align16(tile_rows * 2) + nbins * 8));
+}
+static int sweep_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
+    return align16(tile_rows * (int)row_bytes) + sweep_tab_bytes(tile_rows, nbins);
+}
+
+// Rows per range of the sweep sort for n rows of row_bytes (the widest field)
+// and nbins ids: a whole number of kSweepTR-row tiles, the ranges as many as
+// the CUs (one persistent workgroup each); 0 when the sweep does not take
+// these rows (nbins > 512: 9-bit ballot ranks; the image + table over 160 KiB).
+int64_t sweep_range_rows(int64_t n, int64_t row_bytes, int nbins) {
+    if (row_bytes < 1 || row_bytes % 4 || row_bytes > 64 || nbins < 1 || nbins > 512) return 0;
+    if (sweep_lds_bytes(kSweepTR, row_bytes, nbins) > 160 * 1024) return 0;
+    const int64_t T = std::max<int64_t>(1, (n + kSweepTR - 1) / kSweepTR);
+    const int64_t R = std::min<int64_t>(T, device_cus());
+    return (T + R - 1) / R * kSweepTR;
+}
+
+hipError_t launch_count_ranges(const uint16_t* ids, int64_t n, int nbins, int64_t range_rows,
+                               const Workspace& ws, uint32_t* bad, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    prof_begin(s, K_COUNT_IDS);
+    const int lds = align16(nbins * 4);
+    ensure_lds(count_ranges_kernel, lds);
+    hipLaunchKernelGGL(count_ranges_kernel, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s, ids,
+                       n, nbins, range_rows, ws.T, ws.counts, ws.flags, bad);
+    prof_end(s, K_COUNT_IDS);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_sweep(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
+                             int nbins, int64_t range_rows, const Workspace& ws, void* dst,
+                             hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (row_bytes % 4 || row_bytes > 64 || nbins > 512 || range_rows % kSweepTR ||
+        ((uintptr_t)src & 3) || ((uintptr_t)dst & 3))
+        return hipErrorNotSupported;
+    const int lds = sweep_lds_bytes(kSweepTR, row_bytes, nbins);
+    if (lds > 160 * 1024) return hipErrorNotSupported;
+    const int tab = sweep_tab_bytes(kSweepTR, nbins);
+    prof_begin(s, K_PACK_FINE);
+    hipError_t e = hipErrorNotSupported;
+#define MGR_PS(RB_)                                                                           \
+    case RB_: {                                                                               \
+        auto k = pack_sweep_kernel<RB_, kSweepTR>;                                            \
+        ensure_lds(k, lds);                                                                   \
+        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,               \
+                           (const uint8_t*)src, n, ids, nbins, ws.offsets, ws.T, range_rows,  \
+                           tab, (uint8_t*)dst, ws.scan_err);                                  \
+        e = hipGetLastError();                                                                \
+    } break;
+    switch ((int)row_bytes) {
+        MGR_PS(4) MGR_PS(8) MGR_PS(12) MGR_PS(16) MGR_PS(20) MGR_PS(24) MGR_PS(28) MGR_PS(32)
+        MGR_PS(36)
+        default: break;
+    }
+#undef MGR_PS
     prof_end(s, K_PACK_FINE);
     return e;
 }
