@@ -1172,25 +1172,33 @@ __global__ __launch_bounds__(1024) void count_ranges_kernel(const uint16_t* __re
 
 // The stable sort of one field by the ids, range r per workgroup (see above).
 // offsets[b * R + r] (mgr_scan over count_ranges' counts) = the first output
-// row of bin b's rows of range r.  LDS: the tile image [TR * RB], then a
-// table region -- per-wave bin counts u16 [NW][nb] while ranking, the image
-// rows' bins u16 [TR] and per-bin output addresses u64 [nb] while storing --
-// and, while the image is empty, the bins' tile starts inside it.
+// row of bin b's rows of range r.  LDS: the tile image [TR * RB] and, behind
+// it, the image rows' bins u16 [TR] and the per-bin output addresses u64
+// [nb].  While a tile is ranked the image is still empty and holds the
+// ranking state: per-wave peer words u64 [NW][nb] (rank_ids' OR words: 3 LDS
+// operations per 64-row round), per-wave bin counts u16 [NW][nb], the block
+// scan's wave sums and the bins' tile starts u32 [nb].
+// Registers: one tile's rows at a time (128 VGPRs at 16 waves per CU; two
+// tiles' rows spill) -- the next tile's ids are loaded before the ranking,
+// its rows as soon as this tile's rows are in the image, so they are in
+// flight during the image's store phase.
 template <int RB, int TR>
 __global__ __launch_bounds__(1024) void pack_sweep_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids, int nb,
-    const int64_t* __restrict__ offsets, int64_t R, int64_t range_rows, int tab_bytes,
+    const int64_t* __restrict__ offsets, int64_t R, int64_t range_rows,
     uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
     static_assert(RB % 4 == 0 && RB <= 64, "sweep row size");
     constexpr int NW = kFineWaves, RPW = TR / 64 / NW, NDW = RB / 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t* img = (uint32_t*)smem;
-    uint8_t* tabp = smem + align16(TR * RB);
-    uint16_t* tab = (uint16_t*)tabp;                                   // ranking: [NW][nb]
-    uint16_t* ibin = (uint16_t*)tabp;                                  // storing: [TR]
-    unsigned long long* gaddr = (unsigned long long*)(tabp + align16(TR * 2));   // [nb]
-    int* wsum = (int*)smem;                                            // in the empty image
-    uint32_t* tstart = (uint32_t*)(smem + 64);
+    uint16_t* ibin = (uint16_t*)(smem + align16(TR * RB));                       // [TR]
+    unsigned long long* gaddr = (unsigned long long*)(smem + align16(TR * RB) + align16(TR * 2));
+    // ranking state, inside the empty image
+    unsigned long long* mk = (unsigned long long*)smem;                          // [NW][nb]
+    uint16_t* cw = (uint16_t*)(smem + NW * nb * 8);                              // [NW][nb]
+    int* wsum = (int*)(smem + NW * nb * 8 + align16(NW * nb * 2));               // [NW]
+    uint32_t* tstart = (uint32_t*)((uint8_t*)wsum + 64);                         // [nb]
+    const int zero16 = (NW * nb * 8 + align16(NW * nb * 2)) / 16;
     if (scan_failed(scan_err)) return;
     const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const int64_t r = blockIdx.x;
@@ -1200,39 +1208,54 @@ __global__ __launch_bounds__(1024) void pack_sweep_kernel(
     if (t0 >= t1) return;
     const bool binner = tid < nb;                                      // thread b owns bin b
     long long run = binner ? offsets[(int64_t)tid * R + r] : 0;        // bin's next output row
-    struct Set {
-        uint32_t v[RPW][NDW];
-        unsigned b[RPW];
+    auto row_of = [&](int64_t t, int q) {
+        return min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
     };
-    auto load = [&](Set& S, int64_t t) __attribute__((always_inline)) {
-        t = min(t, t1 - 1);
+    uint32_t v[RPW][NDW];
+    unsigned bn[RPW], bnext[RPW];
+    auto load_ids = [&](unsigned (&b)[RPW], int64_t t) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const int64_t row = min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
-            S.b[q] = min((unsigned)ids[row], (unsigned)(nb - 1));     // >= nb: clamped (count_ranges reports)
-            load_row_dw<NDW>(src + row * RB, S.v[q]);
-        }
+        for (int q = 0; q < RPW; ++q)   // ids >= nb: clamped (count_ranges reports them)
+            b[q] = min((unsigned)ids[row_of(t, q)], (unsigned)(nb - 1));
     };
-    auto process = [&](Set& S, int64_t t) __attribute__((always_inline)) {
+    auto load_rows = [&](int64_t t) __attribute__((always_inline)) {
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) load_row_dw<NDW>(src + row_of(t, q) * RB, v[q]);
+    };
+    int64_t t = t0;
+    load_ids(bn, t);
+    load_rows(t);
+    for (;;) {
+        const int64_t tn = t + 1 < t1 ? t + 1 : t;      // next tile (reloads the last: unused)
+        load_ids(bnext, tn);
         const int tr = (int)min((int64_t)TR, n - t * TR);
-        {   // zero the per-wave counts (16-byte stores)
+        {   // zero the peer words and counts (16-byte stores)
             typedef unsigned int z4_t __attribute__((ext_vector_type(4)));
-            for (int i = tid; i < tab_bytes / 16; i += 1024) ((z4_t*)tabp)[i] = z4_t{0u, 0u, 0u, 0u};
+            for (int i = tid; i < zero16; i += 1024) ((z4_t*)smem)[i] = z4_t{0u, 0u, 0u, 0u};
         }
         __syncthreads();
         // rank: wave w holds rows [w * RPW * 64, (w + 1) * RPW * 64) of the
-        // tile in round order, so (wave, round, lane) is the row order and a
-        // ballot rank plus the wave's running count of the bin is stable
-        unsigned rk[RPW];
-        uint16_t* tw = tab + w * nb;
+        // tile in round order, so (wave, round, lane) is the row order; a
+        // round's peers by OR words (OR commutes: order-free), the wave's
+        // running count of the bin before them
+        int rk[RPW];
+        unsigned long long* mw = mk + w * nb;
+        uint16_t* ww = cw + w * nb;
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
             const bool valid = (w * RPW + q) * 64 + lane < tr;
-            const unsigned long long peers = match_bin_t<9>(S.b[q], valid, 9);
-            const int rr = rank_in(peers);
-            const unsigned before = valid ? tw[S.b[q]] : 0u;
+            const unsigned b = bn[q];
+            if (valid) __hip_atomic_fetch_or(&mw[b], 1ull << lane, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_WAVEFRONT);
             wave_sync();
-            if (valid && rr == 0) tw[S.b[q]] = (uint16_t)(before + __popcll(peers));
+            const unsigned long long peers = valid ? mw[b] : 0ull;
+            const int rr = rank_in(peers);
+            const int before = valid ? (int)ww[b] : 0;
+            wave_sync();
+            if (valid && rr == 0) {
+                ww[b] = (uint16_t)(before + __popcll(peers));
+                mw[b] = 0ull;
+            }
             wave_sync();
             rk[q] = before + rr;
         }
@@ -1242,9 +1265,9 @@ __global__ __launch_bounds__(1024) void pack_sweep_kernel(
         int cnt = 0;
         if (binner) {
 #pragma unroll
-            for (int v = 0; v < NW; ++v) {
-                const int c = tab[v * nb + tid];
-                tab[v * nb + tid] = (uint16_t)cnt;
+            for (int u = 0; u < NW; ++u) {
+                const int c = cw[u * nb + tid];
+                cw[u * nb + tid] = (uint16_t)cnt;
                 cnt += c;
             }
         }
@@ -1253,29 +1276,27 @@ __global__ __launch_bounds__(1024) void pack_sweep_kernel(
         __syncthreads();
         int wpre = 0;
 #pragma unroll
-        for (int v = 0; v < NW; ++v) wpre += v < w ? wsum[v] : 0;
+        for (int u = 0; u < NW; ++u) wpre += u < w ? wsum[u] : 0;
         const int ts = wpre + incl - cnt;
-        long long delta = 0;
         if (binner) {
             tstart[tid] = (uint32_t)ts;
-            delta = run - ts;          // image row i of bin b -> output row i + delta
+            // image row i of bin b -> output row i + run - ts
+            gaddr[tid] = (unsigned long long)(dst + (run - ts) * (long long)RB);
             run += cnt;
         }
         __syncthreads();
-        int slot[RPW];
 #pragma unroll
-        for (int q = 0; q < RPW; ++q)
-            slot[q] = (int)(tstart[S.b[q]] + tab[w * nb + S.b[q]] + rk[q]);
-        __syncthreads();   // the image and the table region are rewritten below
-        if (binner) gaddr[tid] = (unsigned long long)(dst + delta * (long long)RB);
+        for (int q = 0; q < RPW; ++q) rk[q] += (int)(tstart[bn[q]] + cw[w * nb + bn[q]]);
+        __syncthreads();   // the ranking state is overwritten by the image below
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
             if ((w * RPW + q) * 64 + lane < tr) {
 #pragma unroll
-                for (int i = 0; i < NDW; ++i) img[slot[q] * NDW + i] = S.v[q][i];
-                ibin[slot[q]] = (uint16_t)S.b[q];
+                for (int i = 0; i < NDW; ++i) img[rk[q] * NDW + i] = v[q][i];
+                ibin[rk[q]] = (uint16_t)bn[q];
             }
         }
+        if (t + 1 < t1) load_rows(tn);   // in flight during the store phase
         __syncthreads();
         const int nbytes = tr * RB;
         for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
@@ -1291,28 +1312,19 @@ __global__ __launch_bounds__(1024) void pack_sweep_kernel(
                 }
             }
         }
-        __syncthreads();   // the image and the table region are reused by the next tile
-    };
-    Set A, B;
-    int64_t t = t0;
-    load(A, t);
-    for (;;) {
-        load(B, t + 1);
-        process(A, t);
         if (++t >= t1) break;
-        load(A, t + 1);
-        process(B, t);
-        if (++t >= t1) break;
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) bn[q] = bnext[q];
+        __syncthreads();   // the image, ibin and gaddr are reused by the next tile
     }
 }
 
-// LDS of pack_sweep: the image and the table region (ranking counts, or the
-// image rows' bins and the per-bin output addresses).
-static int sweep_tab_bytes(int tile_rows, int nbins) {
-    return align16(std::max(kFineWaves * nbins * 2, align16(tile_rows * 2) + nbins * 8));
-}
+// LDS of pack_sweep: the image (which holds the ranking state while empty),
+// the image rows' bins and the per-bin output addresses.
 static int sweep_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
-    return align16(tile_rows * (int)row_bytes) + sweep_tab_bytes(tile_rows, nbins);
+    const int state = kFineWaves * nbins * 8 + align16(kFineWaves * nbins * 2) + 64 + nbins * 4;
+    const int img = std::max(align16(tile_rows * (int)row_bytes), align16(state));
+    return img + align16(tile_rows * 2) + nbins * 8;
 }
 
 // Rows per range of the sweep sort for n rows of row_bytes (the widest field)
@@ -1348,7 +1360,6 @@ hipError_t launch_pack_sweep(const void* src, int64_t row_bytes, int64_t n, cons
         return hipErrorNotSupported;
     const int lds = sweep_lds_bytes(kSweepTR, row_bytes, nbins);
     if (lds > 160 * 1024) return hipErrorNotSupported;
-    const int tab = sweep_tab_bytes(kSweepTR, nbins);
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
 #define MGR_PS(RB_)                                                                           \
@@ -1357,7 +1368,7 @@ hipError_t launch_pack_sweep(const void* src, int64_t row_bytes, int64_t n, cons
         ensure_lds(k, lds);                                                                   \
         hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,               \
                            (const uint8_t*)src, n, ids, nbins, ws.offsets, ws.T, range_rows,  \
-                           tab, (uint8_t*)dst, ws.scan_err);                                  \
+                           (uint8_t*)dst, ws.scan_err);                                       \
         e = hipGetLastError();                                                                \
     } break;
     switch ((int)row_bytes) {
