@@ -49,21 +49,15 @@ N_CFG5_PER_GPU = 512_000_000 // 8    # config 5: 512M over 8 GPUs
 
 # Algorithmic bytes per row of one launch (DESIGN.md §4 Measurement): what
 # the kernel must read and write at least, per row it processes.
-def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1,
-                         fine_sweep=True):
+def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1):
     if cfg == 5:
-        src = {
+        ts = 2.0 * fine_bins / fine_tile_rows        # u16 tile starts per row
+        return {
             "bin_fine": 36 + 1 + 2,          # read the 36-B record (staged slab), dest, fine id
             "pack": 1 + 36 + 2 + 36 + 2,     # dest, record + fine id in, record + fine id out
+            "count_ids": 2 + 2 + ts,         # mgr_rank_ids: ids in, ranks + tile starts out
+            "pack_fine": 2 + 2 + ts + 36 + 36,   # mgr_pack_ranked: ids, ranks, starts, record
         }
-        if fine_sweep:   # the destination sort as a sweep (mgr_sweep_count, mgr_pack_sweep)
-            return {**src,
-                    "count_ids": 2,                  # count_ranges: the ids
-                    "pack_fine": 2 + 36 + 36}        # pack_sweep: ids, record in, record out
-        ts = 2.0 * fine_bins / fine_tile_rows        # u16 tile starts per row
-        return {**src,
-                "count_ids": 2 + 2 + ts,             # mgr_rank_ids: ids in, ranks + tile starts out
-                "pack_fine": 2 + 2 + ts + 36 + 36}   # mgr_pack_ranked: ids, ranks, starts, record
     if halo:
         # one rank keeps its rows in order: the selections read the binning's
         # flags in place, no flag field travels with the pack
@@ -495,9 +489,7 @@ def main():
     # rows -- received rows at N > 1 are ~n for the uniform inputs), or the
     # host-counted bytes of the halo's selections
     fine_tr = int(_lib.load().mgr_ranked_tile_rows(36, 512)) if cfg == 5 else 2048
-    sweep = cfg == 5 and int(_lib.load().mgr_sweep_range_rows(n, 36, 512)) > 0
-    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world,
-                                     fine_sweep=sweep).items():
+    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world).items():
         if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
             kernels[k]["alg_bytes_per_launch"] = b * n
     for k, e in kernels.items():

@@ -244,30 +244,6 @@ int mgr_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_
                     const uint16_t* ranks, const uint16_t* tile_starts, int nbins, int tile_rows,
                     const void* workspace, void* dst, void* stream);
 
-/* The destination-side fine sort as a sweep (the product path where it
- * applies; config 5): the tiles are dealt in contiguous ranges, one per
- * resident workgroup, so a range's per-bin output offsets are all the scan
- * needs and the pack ranks each tile itself -- no per-row ranks or per-tile
- * starts in memory.
- * mgr_sweep_range_rows : rows per range for n rows of row_bytes (the widest
- *                field) and nbins ids; 0 when the sweep does not take them
- *                (nbins > 512, rows not 4-byte multiples, the tile image +
- *                tables over the LDS) -- then use mgr_rank_ids/mgr_pack_ranked.
- * mgr_sweep_workspace_bytes : its workspace (nbins x ranges counts).
- * mgr_sweep_count : per-range counts of the ids and their scan; bin_counts
- *                (int64 [nbins], device) = the sorted segments' sizes; ids >=
- *                nbins are clamped and flag *bad_ids (as mgr_count_ids).
- * mgr_pack_sweep : the stable sort of one field of n rows by the ids (after
- *                mgr_sweep_count on the same workspace), dst = rows of id 0,
- *                then id 1, ..., original order kept within an id.         */
-#define MGR_MAX_SWEEP_RANGES 4096
-int64_t mgr_sweep_range_rows(int64_t n, int64_t row_bytes, int nbins);
-int64_t mgr_sweep_workspace_bytes(int64_t n, int nbins, int64_t range_rows);
-int mgr_sweep_count(const uint16_t* ids, int64_t n, int nbins, int64_t range_rows,
-                    uint32_t* bad_ids, int64_t* bin_counts, void* workspace, void* stream);
-int mgr_pack_sweep(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids, int nbins,
-                   int64_t range_rows, const void* workspace, void* dst, void* stream);
-
 /* One call = bin_count + scan + pack of one field: the 1-GPU local stage
  * (bin + scan + stable pack, BASELINE config 2).  bin_offsets: int64
  * [nbins+1] device.                                                       */

@@ -46,10 +46,6 @@ SIGNATURES = {
     "mgr_count_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P, _P]),
     "mgr_rank_ids": (_I, [_P, _I64, _I, _I, _P, _P, _P, _P, _P]),
     "mgr_pack_ranked": (_I, [_P, _I64, _I64, _P, _P, _P, _I, _I, _P, _P, _P]),
-    "mgr_sweep_range_rows": (_I64, [_I64, _I64, _I]),
-    "mgr_sweep_workspace_bytes": (_I64, [_I64, _I, _I64]),
-    "mgr_sweep_count": (_I, [_P, _I64, _I, _I64, _P, _P, _P, _P]),
-    "mgr_pack_sweep": (_I, [_P, _I64, _I64, _P, _I, _I64, _P, _P, _P]),
     "mgr_cell_ids": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P]),
     "mgr_bin_ids": (_I, [_P, _P, _I, _I64, _P, _I, _P, _P]),
     "mgr_cell_number_from_indexes": (_I, [_P, _P, _I64, _I, _P, _P]),

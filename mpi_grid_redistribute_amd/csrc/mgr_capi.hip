@@ -519,59 +519,6 @@ int mgr_pack_ranked(const void* src, int64_t row_bytes, int64_t n, const uint16_
     return MGR_OK;
 }
 
-int64_t mgr_sweep_range_rows(int64_t n, int64_t row_bytes, int nbins) {
-    if (n < 0) return 0;
-    return mgr::sweep_range_rows(n, row_bytes, nbins);
-}
-
-int64_t mgr_sweep_workspace_bytes(int64_t n, int nbins, int64_t range_rows) {
-    if (n < 0 || nbins < 1 || nbins > MGR_MAX_BINS || range_rows < 64) return -1;
-    return mgr::workspace_bytes(n, nbins, range_rows);
-}
-
-static int check_sweep(int64_t n, int nbins, int64_t range_rows) {
-    if (n < 0) return fail(MGR_EINVAL, "n < 0");
-    if (nbins < 1 || nbins > 512) return fail(MGR_EINVAL, "nbins %d not in [1, 512]", nbins);
-    if (range_rows < 4096 || range_rows % 4096)
-        return fail(MGR_EINVAL, "range_rows %lld: a multiple of 4096 (mgr_sweep_range_rows)",
-                    (long long)range_rows);
-    if (mgr::num_tiles(n, range_rows) > MGR_MAX_SWEEP_RANGES)
-        return fail(MGR_EINVAL, "%lld ranges of %lld rows: at most %d (mgr_sweep_range_rows)",
-                    (long long)mgr::num_tiles(n, range_rows), (long long)range_rows,
-                    MGR_MAX_SWEEP_RANGES);
-    return MGR_OK;
-}
-
-int mgr_sweep_count(const uint16_t* ids, int64_t n, int nbins, int64_t range_rows,
-                    uint32_t* bad_ids, int64_t* bin_counts, void* workspace, void* stream) {
-    int rc = check_sweep(n, nbins, range_rows);
-    if (rc) return rc;
-    if (n > 0 && (!ids || !workspace)) return fail(MGR_EINVAL, "null argument");
-    if (!workspace) return MGR_OK;
-    const mgr::Workspace ws = mgr::carve(workspace, n, nbins, range_rows);
-    HIP_OK(mgr::launch_count_ranges(ids, n, nbins, range_rows, ws, bad_ids, (hipStream_t)stream));
-    HIP_OK(mgr::launch_scan(n, nbins, 0, ws, bin_counts, (hipStream_t)stream));
-    return MGR_OK;
-}
-
-int mgr_pack_sweep(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids, int nbins,
-                   int64_t range_rows, const void* workspace, void* dst, void* stream) {
-    int rc = check_sweep(n, nbins, range_rows);
-    if (rc) return rc;
-    if (row_bytes < 1) return fail(MGR_EINVAL, "row_bytes %lld", (long long)row_bytes);
-    if (n > 0 && (!src || !ids || !workspace || !dst)) return fail(MGR_EINVAL, "null argument");
-    if (n == 0) return MGR_OK;
-    const mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, range_rows);
-    const hipError_t e = mgr::launch_pack_sweep(src, row_bytes, n, ids, nbins, range_rows, ws, dst,
-                                                (hipStream_t)stream);
-    if (e == hipErrorNotSupported)
-        return fail(MGR_EUNSUPPORTED, "sweep pack: rows of %lld bytes, %d ids (needs 4-byte "
-                    "multiples whose 4096-row image + tables fit the LDS, <= 512 ids, 4-byte "
-                    "aligned buffers)", (long long)row_bytes, nbins);
-    HIP_OK(e);
-    return MGR_OK;
-}
-
 int mgr_cell_ids(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int64_t row_stride,
                  int periodic, int64_t* cell_out, int64_t* idx_out, void* stream) {
     int rc = check_pos(plan, pos, pos_dtype, n, row_stride);

@@ -89,9 +89,9 @@ struct Workspace {
     int64_t T;
     int64_t t0 = 0, tn = 0;    // the tiles [t0, t0 + tn) one pack launch covers (all: 0, T)
 };
-int64_t num_tiles(int64_t n, int64_t tile_rows);
-int64_t workspace_bytes(int64_t n, int nbins, int64_t tile_rows);
-Workspace carve(void* base, int64_t n, int nbins, int64_t tile_rows);
+int64_t num_tiles(int64_t n, int tile_rows);
+int64_t workspace_bytes(int64_t n, int nbins, int tile_rows);
+Workspace carve(void* base, int64_t n, int nbins, int tile_rows);
 int dest_bytes(int nbins);
 int nbits_for(int nbins);
 
@@ -141,12 +141,6 @@ int pack_tile_rows(int64_t row_bytes, int nbins);
 hipError_t launch_tile_offsets(const Workspace& ws, int nbins, const int64_t* tiles, int ntiles,
                                int64_t* out, hipStream_t s);
 int ranked_tile_rows(int64_t row_bytes, int nbins);
-int64_t sweep_range_rows(int64_t n, int64_t row_bytes, int nbins);
-hipError_t launch_count_ranges(const uint16_t* ids, int64_t n, int nbins, int64_t range_rows,
-                               const Workspace& ws, uint32_t* bad, hipStream_t s);
-hipError_t launch_pack_sweep(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
-                             int nbins, int64_t range_rows, const Workspace& ws, void* dst,
-                             hipStream_t s);
 hipError_t launch_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
 

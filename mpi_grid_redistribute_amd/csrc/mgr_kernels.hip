@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kBlock) void synth_uniform_kernel(uint64_t seed, in
 
 // ============================================================ launchers
 // ============================================================ launchers
-int64_t num_tiles(int64_t n, int64_t tile_rows) { return (n + tile_rows - 1) / tile_rows; }
+int64_t num_tiles(int64_t n, int tile_rows) { return (n + tile_rows - 1) / tile_rows; }
 
 int dest_bytes(int nbins) { return nbins <= 256 ? 1 : (nbins <= 65536 ? 2 : 4); }
 
@@ -466,14 +466,14 @@ int nbits_for(int nbins) {
 
 static int64_t a256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-int64_t workspace_bytes(int64_t n, int nbins, int64_t tile_rows) {
+int64_t workspace_bytes(int64_t n, int nbins, int tile_rows) {
     const int64_t T = num_tiles(n, tile_rows);
     const int64_t M = (int64_t)nbins * (T > 0 ? T : 1);
     return a256(M * 4) + a256(M * 8) + a256((nbins + 1) * 8) +
            a256((kScanFlags + kScanCtlWords) * 8);
 }
 
-Workspace carve(void* base, int64_t n, int nbins, int64_t tile_rows) {
+Workspace carve(void* base, int64_t n, int nbins, int tile_rows) {
     Workspace ws;
     ws.T = num_tiles(n, tile_rows);
     ws.t0 = 0;

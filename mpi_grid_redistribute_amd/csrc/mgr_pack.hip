@@ -4,8 +4,6 @@
 // and tile-size policy.  Helpers: mgr_device.h.
 #include "mgr_device.h"
 
-#include <algorithm>
-
 namespace mgr {
 
 
@@ -1109,274 +1107,6 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     }
 #undef MGR_PR
 #undef MGR_PRT
-    prof_end(s, K_PACK_FINE);
-    return e;
-}
-
-// ============================================================== sweep sort
-// The destination-side stable sort by fine cell in THREE light launches --
-// count_ranges (a 2-byte read per row), a scan of nbins x R counts, and
-// pack_sweep -- instead of rank_ids + a scan of nbins x T counts +
-// pack_ranked.  The tiles are dealt in R contiguous ranges, one per
-// workgroup of a persistent grid (R <= the CU count), and a workgroup walks
-// its range in order, so every bin's running output offset inside the range
-// lives in a register: the scan only needs each range's per-bin counts
-// (count_ranges), not per-tile ones, and no per-row rank, tile start or
-// per-tile offset ever leaves the chip.  pack_sweep ranks a tile's rows
-// itself (ballot match, per-wave counts in LDS), places them in the LDS image
-// and streams the image out as pack_ranked does.
-//
-// Why not a decoupled look-back across tiles: with one resident workgroup
-// per CU (the image fills the LDS) the workgroups run in lockstep, so a
-// tile's look-back finds its predecessors' aggregates but hardly ever an
-// inclusive prefix -- it would sum up to one word per concurrent workgroup
-// and bin, ~30 x 2 KB per 147 KB tile.  Owning a range removes the chain.
-constexpr int kSweepTR = 4096;   // sweep tiles (the ranked tiles' size)
-
-// Per-range counts: counts[b * R + r] = rows of id b in rows [r * range_rows,
-// (r + 1) * range_rows); ids >= nbins are clamped and reported through *bad
-// (as mgr_count_ids).  One 1024-thread workgroup per range, 8 ids per load.
-__global__ __launch_bounds__(1024) void count_ranges_kernel(const uint16_t* __restrict__ ids,
-                                                            int64_t n, int nbins, int64_t range_rows,
-                                                            int64_t R, int32_t* __restrict__ counts,
-                                                            uint64_t* __restrict__ scan_flags,
-                                                            uint32_t* __restrict__ bad) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int32_t* hist = (int32_t*)smem;
-    clear_scan_flags(scan_flags);
-    const int64_t r = blockIdx.x;
-    for (int b = threadIdx.x; b < nbins; b += 1024) hist[b] = 0;
-    __syncthreads();
-    const int64_t row0 = r * range_rows;
-    const int64_t rows = min(range_rows, n - row0);
-    const uint16_t* p = ids + row0;
-    const bool vec = ((uintptr_t)p & 15) == 0;
-    bool oob = false;
-    auto add = [&](unsigned v) {
-        if (v >= (unsigned)nbins) { v = nbins - 1; oob = true; }
-        atomicAdd(&hist[v], 1);
-    };
-    for (int64_t i = 8 * (int64_t)threadIdx.x; i < rows; i += 8 * 1024) {
-        if (vec && i + 8 <= rows) {
-            const uint4 q = *(const uint4*)(p + i);
-            add(q.x & 0xffffu); add(q.x >> 16); add(q.y & 0xffffu); add(q.y >> 16);
-            add(q.z & 0xffffu); add(q.z >> 16); add(q.w & 0xffffu); add(q.w >> 16);
-        } else {
-            for (int64_t j = i; j < min(i + 8, rows); ++j) add(p[j]);
-        }
-    }
-    if (__any(oob) && lane_id() == 0 && bad) atomicOr(bad, 1u);
-    __syncthreads();
-    for (int b = threadIdx.x; b < nbins; b += 1024) counts[(int64_t)b * R + r] = hist[b];
-}
-
-// The stable sort of one field by the ids, range r per workgroup (see above).
-// offsets[b * R + r] (mgr_scan over count_ranges' counts) = the first output
-// row of bin b's rows of range r.  LDS: the tile image [TR * RB] and, behind
-// it, the image rows' bins u16 [TR] and the per-bin output addresses u64
-// [nb].  While a tile is ranked the image is still empty and holds the
-// ranking state: per-wave peer words u64 [NW][nb] (rank_ids' OR words: 3 LDS
-// operations per 64-row round), per-wave bin counts u16 [NW][nb], the block
-// scan's wave sums and the bins' tile starts u32 [nb].
-// Registers: one tile's rows at a time (128 VGPRs at 16 waves per CU; two
-// tiles' rows spill) -- the next tile's ids are loaded before the ranking,
-// its rows as soon as this tile's rows are in the image, so they are in
-// flight during the image's store phase.
-template <int RB, int TR>
-__global__ __launch_bounds__(1024) void pack_sweep_kernel(
-    const uint8_t* __restrict__ src, int64_t n, const uint16_t* __restrict__ ids, int nb,
-    const int64_t* __restrict__ offsets, int64_t R, int64_t range_rows,
-    uint8_t* __restrict__ dst, const uint32_t* __restrict__ scan_err) {
-    static_assert(RB % 4 == 0 && RB <= 64, "sweep row size");
-    constexpr int NW = kFineWaves, RPW = TR / 64 / NW, NDW = RB / 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t* img = (uint32_t*)smem;
-    uint16_t* ibin = (uint16_t*)(smem + align16(TR * RB));                       // [TR]
-    unsigned long long* gaddr = (unsigned long long*)(smem + align16(TR * RB) + align16(TR * 2));
-    // ranking state, inside the empty image
-    unsigned long long* mk = (unsigned long long*)smem;                          // [NW][nb]
-    uint16_t* cw = (uint16_t*)(smem + NW * nb * 8);                              // [NW][nb]
-    int* wsum = (int*)(smem + NW * nb * 8 + align16(NW * nb * 2));               // [NW]
-    uint32_t* tstart = (uint32_t*)((uint8_t*)wsum + 64);                         // [nb]
-    const int zero16 = (NW * nb * 8 + align16(NW * nb * 2)) / 16;
-    if (scan_failed(scan_err)) return;
-    const int tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const int64_t r = blockIdx.x;
-    const int64_t tpr = range_rows / TR;                               // tiles per range
-    const int64_t T = (n + TR - 1) / TR;
-    const int64_t t0 = r * tpr, t1 = min(T, t0 + tpr);
-    if (t0 >= t1) return;
-    const bool binner = tid < nb;                                      // thread b owns bin b
-    long long run = binner ? offsets[(int64_t)tid * R + r] : 0;        // bin's next output row
-    auto row_of = [&](int64_t t, int q) {
-        return min(t * TR + (int64_t)(w * RPW + q) * 64 + lane, n - 1);
-    };
-    uint32_t v[RPW][NDW];
-    unsigned bn[RPW], bnext[RPW];
-    auto load_ids = [&](unsigned (&b)[RPW], int64_t t) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < RPW; ++q)   // ids >= nb: clamped (count_ranges reports them)
-            b[q] = min((unsigned)ids[row_of(t, q)], (unsigned)(nb - 1));
-    };
-    auto load_rows = [&](int64_t t) __attribute__((always_inline)) {
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) load_row_dw<NDW>(src + row_of(t, q) * RB, v[q]);
-    };
-    int64_t t = t0;
-    load_ids(bn, t);
-    load_rows(t);
-    for (;;) {
-        const int64_t tn = t + 1 < t1 ? t + 1 : t;      // next tile (reloads the last: unused)
-        load_ids(bnext, tn);
-        const int tr = (int)min((int64_t)TR, n - t * TR);
-        {   // zero the peer words and counts (16-byte stores)
-            typedef unsigned int z4_t __attribute__((ext_vector_type(4)));
-            for (int i = tid; i < zero16; i += 1024) ((z4_t*)smem)[i] = z4_t{0u, 0u, 0u, 0u};
-        }
-        __syncthreads();
-        // rank: wave w holds rows [w * RPW * 64, (w + 1) * RPW * 64) of the
-        // tile in round order, so (wave, round, lane) is the row order; a
-        // round's peers by OR words (OR commutes: order-free), the wave's
-        // running count of the bin before them
-        int rk[RPW];
-        unsigned long long* mw = mk + w * nb;
-        uint16_t* ww = cw + w * nb;
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            const bool valid = (w * RPW + q) * 64 + lane < tr;
-            const unsigned b = bn[q];
-            if (valid) __hip_atomic_fetch_or(&mw[b], 1ull << lane, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-            wave_sync();
-            const unsigned long long peers = valid ? mw[b] : 0ull;
-            const int rr = rank_in(peers);
-            const int before = valid ? (int)ww[b] : 0;
-            wave_sync();
-            if (valid && rr == 0) {
-                ww[b] = (uint16_t)(before + __popcll(peers));
-                mw[b] = 0ull;
-            }
-            wave_sync();
-            rk[q] = before + rr;
-        }
-        __syncthreads();
-        // per bin: the waves' counts -> each wave's base inside the bin (in
-        // place), the tile count; a block scan over the bins -> tile starts
-        int cnt = 0;
-        if (binner) {
-#pragma unroll
-            for (int u = 0; u < NW; ++u) {
-                const int c = cw[u * nb + tid];
-                cw[u * nb + tid] = (uint16_t)cnt;
-                cnt += c;
-            }
-        }
-        const int incl = wave_incl_dpp(cnt);
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        int wpre = 0;
-#pragma unroll
-        for (int u = 0; u < NW; ++u) wpre += u < w ? wsum[u] : 0;
-        const int ts = wpre + incl - cnt;
-        if (binner) {
-            tstart[tid] = (uint32_t)ts;
-            // image row i of bin b -> output row i + run - ts
-            gaddr[tid] = (unsigned long long)(dst + (run - ts) * (long long)RB);
-            run += cnt;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) rk[q] += (int)(tstart[bn[q]] + cw[w * nb + bn[q]]);
-        __syncthreads();   // the ranking state is overwritten by the image below
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-            if ((w * RPW + q) * 64 + lane < tr) {
-#pragma unroll
-                for (int i = 0; i < NDW; ++i) img[rk[q] * NDW + i] = v[q][i];
-                ibin[rk[q]] = (uint16_t)bn[q];
-            }
-        }
-        if (t + 1 < t1) load_rows(tn);   // in flight during the store phase
-        __syncthreads();
-        const int nbytes = tr * RB;
-        for (int x = 16 * tid; x < nbytes; x += 16 * 1024) {
-            const u32x4_t q = *(const u32x4_t*)((const uint8_t*)img + x);
-            const int bf = ibin[x / RB];
-            if (x + 16 <= nbytes && ibin[(x + 15) / RB] == bf) {
-                gstore<u32x4_a4>(gaddr[bf] + x, q);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    if (xd < nbytes) gstore<uint32_t>(gaddr[ibin[xd / RB]] + xd, q[d]);
-                }
-            }
-        }
-        if (++t >= t1) break;
-#pragma unroll
-        for (int q = 0; q < RPW; ++q) bn[q] = bnext[q];
-        __syncthreads();   // the image, ibin and gaddr are reused by the next tile
-    }
-}
-
-// LDS of pack_sweep: the image (which holds the ranking state while empty),
-// the image rows' bins and the per-bin output addresses.
-static int sweep_lds_bytes(int tile_rows, int64_t row_bytes, int nbins) {
-    const int state = kFineWaves * nbins * 8 + align16(kFineWaves * nbins * 2) + 64 + nbins * 4;
-    const int img = std::max(align16(tile_rows * (int)row_bytes), align16(state));
-    return img + align16(tile_rows * 2) + nbins * 8;
-}
-
-// Rows per range of the sweep sort for n rows of row_bytes (the widest field)
-// and nbins ids: a whole number of kSweepTR-row tiles, the ranges as many as
-// the CUs (one persistent workgroup each); 0 when the sweep does not take
-// these rows (nbins > 512: 9-bit ballot ranks; the image + table over 160 KiB).
-int64_t sweep_range_rows(int64_t n, int64_t row_bytes, int nbins) {
-    if (row_bytes < 1 || row_bytes % 4 || row_bytes > 64 || nbins < 1 || nbins > 512) return 0;
-    if (sweep_lds_bytes(kSweepTR, row_bytes, nbins) > 160 * 1024) return 0;
-    const int64_t T = std::max<int64_t>(1, (n + kSweepTR - 1) / kSweepTR);
-    const int64_t R = std::min<int64_t>(T, device_cus());
-    return (T + R - 1) / R * kSweepTR;
-}
-
-hipError_t launch_count_ranges(const uint16_t* ids, int64_t n, int nbins, int64_t range_rows,
-                               const Workspace& ws, uint32_t* bad, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    prof_begin(s, K_COUNT_IDS);
-    const int lds = align16(nbins * 4);
-    ensure_lds(count_ranges_kernel, lds);
-    hipLaunchKernelGGL(count_ranges_kernel, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s, ids,
-                       n, nbins, range_rows, ws.T, ws.counts, ws.flags, bad);
-    prof_end(s, K_COUNT_IDS);
-    return hipGetLastError();
-}
-
-hipError_t launch_pack_sweep(const void* src, int64_t row_bytes, int64_t n, const uint16_t* ids,
-                             int nbins, int64_t range_rows, const Workspace& ws, void* dst,
-                             hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    if (row_bytes % 4 || row_bytes > 64 || nbins > 512 || range_rows % kSweepTR ||
-        ((uintptr_t)src & 3) || ((uintptr_t)dst & 3))
-        return hipErrorNotSupported;
-    const int lds = sweep_lds_bytes(kSweepTR, row_bytes, nbins);
-    if (lds > 160 * 1024) return hipErrorNotSupported;
-    prof_begin(s, K_PACK_FINE);
-    hipError_t e = hipErrorNotSupported;
-#define MGR_PS(RB_)                                                                           \
-    case RB_: {                                                                               \
-        auto k = pack_sweep_kernel<RB_, kSweepTR>;                                            \
-        ensure_lds(k, lds);                                                                   \
-        hipLaunchKernelGGL(k, dim3((unsigned)ws.T), dim3(1024), (size_t)lds, s,               \
-                           (const uint8_t*)src, n, ids, nbins, ws.offsets, ws.T, range_rows,  \
-                           (uint8_t*)dst, ws.scan_err);                                       \
-        e = hipGetLastError();                                                                \
-    } break;
-    switch ((int)row_bytes) {
-        MGR_PS(4) MGR_PS(8) MGR_PS(12) MGR_PS(16) MGR_PS(20) MGR_PS(24) MGR_PS(28) MGR_PS(32)
-        MGR_PS(36)
-        default: break;
-    }
-#undef MGR_PS
     prof_end(s, K_PACK_FINE);
     return e;
 }

@@ -104,52 +104,30 @@ def _as_ids(fine_ids, n, dev, nbins):
     return t
 
 
-def _sort_by_ids(fields, ids, n, nb, dev, scratch=None, check_ids=True, path=None):
-    """Stable sort of every field by the uint16 ids (the fine cells): sweep
-    (mgr_sweep_count -> mgr_pack_sweep), rank (mgr_rank_ids) or count
-    (mgr_count_ids) -> scan -> pack.  Returns ([sorted flat fields], counts).
-    ``check_ids``: ids from the caller (not from this library's binning) --
-    an id >= nb is clamped by the kernels and turns the counts into -1 (the
-    failed-scan convention: host results raise).  ``path`` ("sweep",
-    "ranked", "count"; None = the first that takes the rows): the parity
-    tests and tools/cfg5_ab.py pin one."""
+def _sort_by_ids(fields, ids, n, nb, dev, scratch=None, check_ids=True):
+    """Stable sort of every field by the uint16 ids (the fine cells): rank
+    (mgr_rank_ids) or count (mgr_count_ids) -> scan -> pack.  Returns ([sorted
+    flat fields], counts).  ``check_ids``: ids from the caller (not from this
+    library's binning) -- an id >= nb is clamped by the kernels and turns the
+    counts into -1 (the failed-scan convention: host results raise)."""
     hint = max([f.row_bytes for f in fields] + [1])
     s = _lib.stream_handle()
-    lib = _lib.load()
     counts = torch.empty(nb, dtype=torch.int64, device=dev)
     bad = torch.zeros(1, dtype=torch.int32, device=dev) if check_ids else None
-    get = scratch.get if scratch is not None else (
-        lambda name, nbytes: torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev))
-    dword = all(f.row_bytes % 4 == 0 and f.row_bytes <= 64 and f.flat.data_ptr() % 4 == 0
-                for f in fields)
-    # <= 512 fine cells, 4-byte-multiple rows whose 4096-row image fits the
-    # LDS (<= 36 B): the sweep -- per-range counts, a small scan, and a pack
-    # that ranks each tile itself (mgr_pack_sweep)
-    rr = int(lib.mgr_sweep_range_rows(int(n), int(hint), int(nb))) if dword else 0
-    if n and rr > 0 and path in (None, "sweep"):
-        ws = get("ws_sweep", int(lib.mgr_sweep_workspace_bytes(int(n), int(nb), rr)))
-        _lib.call("mgr_sweep_count", _lib.ptr(ids), n, nb, rr, _lib.ptr(bad), _lib.ptr(counts),
-                  _lib.ptr(ws), s)
-        outs = []
-        for f in fields:
-            o = torch.empty(max(n * f.row_bytes, 1), dtype=torch.uint8, device=dev)
-            _lib.call("mgr_pack_sweep", _lib.ptr(f.flat), f.row_bytes, n, _lib.ptr(ids), nb, rr,
-                      _lib.ptr(ws), _lib.ptr(o), s)
-            outs.append(o)
-        if bad is not None:
-            counts.masked_fill_(bad.ne(0), -1)
-        return outs, counts
     # <= 1024 fine cells, 4-byte-multiple rows <= 64 B on 4-byte-aligned
     # storage: ranks computed once, the ranked pack only places rows
     # (mgr_rank_ids + mgr_pack_ranked), on its own tiles (mgr_ranked_tile_rows);
     # other rows: count + scan + the generic stable pack
-    rtr = int(lib.mgr_ranked_tile_rows(int(hint), int(nb)))
-    ranked = rtr > 0 and dword and path in (None, "ranked")
+    rtr = int(_lib.load().mgr_ranked_tile_rows(int(hint), int(nb)))
+    ranked = (rtr > 0 and all(f.row_bytes % 4 == 0 and f.row_bytes <= 64
+                              and f.flat.data_ptr() % 4 == 0 for f in fields))
     tile_rows, ws, dest = _scratch(n, nb, hint, dev, scratch, dest=not ranked,
                                    tag="_fine", tile_rows=rtr if ranked else None)
     outs = []
     if ranked:
         T = (n + tile_rows - 1) // tile_rows
+        get = scratch.get if scratch is not None else (
+            lambda name, nbytes: torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev))
         # tile slots (+ 16 B: the ranked pack reads u16 quads, the last one
         # a row past n when n is odd)
         ranks = get("ranks_fine", 2 * max(n, 1) + 16)

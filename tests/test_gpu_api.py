@@ -174,14 +174,11 @@ def test_scan_race_cfg2_late_inclusive_word(bin_):
     assert np.array_equal(counts.cpu().numpy(), np.diff(exp_off))
 
 
-@pytest.mark.parametrize("path", ["ranked", "sweep"])
-@pytest.mark.parametrize("bin_", [1, 300])   # (the sweep's bin 0 is chunk 0: no aggregate
-                                             # word, its successors wait for it -- no race)
-def test_scan_race_fine_late_inclusive_word(bin_, path):
-    """The same forced race in the config-5 destination scans: 512 fine cells
-    x 16384 ranked tiles (2^26 ids, 2 chunks per bin, 8192 counts per chunk),
-    and the sweep's 512 cells x ranges scan (one chunk per bin): counts and
-    the stable sort exact against numpy's stable argsort."""
+@pytest.mark.parametrize("bin_", [0, 300])
+def test_scan_race_fine_late_inclusive_word(bin_):
+    """The same forced race in the config-5 destination scan: 512 fine cells x
+    16384 ranked tiles (2^26 ids, 2 chunks per bin, 8192 counts per chunk):
+    counts and the stable sort exact against numpy's stable argsort."""
     from mpi_grid_redistribute_amd.redistributor import _IdField, _sort_by_ids
     n, nb = 1 << 26, 512
     rng = np.random.default_rng(bin_)
@@ -193,12 +190,12 @@ def test_scan_race_fine_late_inclusive_word(bin_, path):
     cnt = np.bincount(ids_h, minlength=nb)
     dev = torch.device("cuda", torch.cuda.current_device())
     with _Hooks(scan_delay_bin=bin_, scan_delay_sleeps=_LATE):
-        outs, counts = _sort_by_ids([rows], ids, n, nb, dev, check_ids=False, path=path)
+        outs, counts = _sort_by_ids([rows], ids, n, nb, dev, check_ids=False)
         torch.cuda.synchronize()
         assert np.array_equal(counts.cpu().numpy(), cnt)
         assert np.array_equal(outs[0][: 4 * n].view(torch.int32).cpu().numpy(), order)
     with _Hooks(scan_delay_bin=bin_, scan_delay_sleeps=_LATE, scan_end_spins=0):
-        _, counts = _sort_by_ids([rows], ids, n, nb, dev, check_ids=False, path=path)
+        _, counts = _sort_by_ids([rows], ids, n, nb, dev, check_ids=False)
         c = counts.cpu().numpy()
     assert c[bin_] == -1 and c[bin_ + 1] == -1
 

@@ -180,20 +180,9 @@ def test_partition_fine_ids_then_sort():
         assert torch.equal(a, b) and torch.equal(oa, ob)
 
 
-@pytest.fixture(params=["sweep", "ranked"])
-def sort_path(request, monkeypatch):
-    """Pin the destination sort's path (the product takes the sweep where it
-    applies, the ranked sort elsewhere): both must give the same bytes."""
-    import functools
-    from mpi_grid_redistribute_amd import redistributor as red
-    monkeypatch.setattr(red, "_sort_by_ids", functools.partial(red._sort_by_ids,
-                                                               path=request.param))
-    return request.param
-
-
 @pytest.mark.parametrize("rank_rows", [0, 2048, 4096])
 @pytest.mark.parametrize("row_bytes", [4, 12, 36, 40, 64])
-def test_ranked_sort_tile_sizes(rank_rows, row_bytes, sort_path):
+def test_ranked_sort_tile_sizes(rank_rows, row_bytes):
     """mgr_rank_ids + mgr_pack_ranked on both tile sizes (4096 where the LDS
     image fits, 2048 otherwise and on request), a ragged last tile, a hot
     cell and empty cells: the stable sort of the rows by their ids."""
@@ -247,7 +236,7 @@ def test_fine_ids_out_of_range(row_bytes):
 
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 63, 4095, 4097, 8193])
 @pytest.mark.parametrize("row_bytes", [4, 36])
-def test_ranked_sort_small_and_ragged(n, row_bytes, sort_path):
+def test_ranked_sort_small_and_ragged(n, row_bytes):
     """The ranked sort at tiny and tile-edge sizes (the unit-streamed pack
     reads the slots of row pairs: no read before row 0 or past row n - 1)."""
     rng = np.random.default_rng(n * 7 + row_bytes)
@@ -260,49 +249,3 @@ def test_ranked_sort_small_and_ragged(n, row_bytes, sort_path):
                                 fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
     assert np.array_equal(got.cpu().numpy(), exp)
     assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=512))
-
-
-@pytest.mark.parametrize("nb", [1, 7, 64, 120, 512])
-@pytest.mark.parametrize("row_bytes", [4, 8, 20, 24, 36])
-@pytest.mark.parametrize("n", [4096 * 513 + 17, 70_001])
-def test_sweep_sort_shapes(nb, row_bytes, n):
-    """mgr_sweep_count + mgr_pack_sweep: every row size it takes, 1..512 ids,
-    more tiles than CUs (several tiles per range, a short last range, a ragged
-    last tile) and fewer; a hot id and empty ids -- the stable argsort."""
-    from mpi_grid_redistribute_amd.redistributor import _IdField, _sort_by_ids
-    rng = np.random.default_rng(nb * 31 + row_bytes + n % 97)
-    ids = rng.integers(0, nb, n).astype(np.uint16)
-    ids[rng.random(n) < 0.25] = nb // 2
-    ids[(ids > nb // 3) & (ids < nb // 3 + 3)] = 0
-    data = rng.integers(0, 256, (n, row_bytes), dtype=np.uint8)
-    order = np.argsort(ids, kind="stable")
-    f = _IdField(torch.from_numpy(data).cuda().reshape(-1))
-    f.row_bytes = row_bytes
-    dev = torch.device("cuda", torch.cuda.current_device())
-    tid = torch.from_numpy(ids.view(np.int16)).cuda()
-    outs, counts = _sort_by_ids([f], tid, n, nb, dev, path="sweep")
-    assert np.array_equal(counts.cpu().numpy(), np.bincount(ids, minlength=nb))
-    got = outs[0][: n * row_bytes].cpu().numpy().reshape(n, row_bytes)
-    assert np.array_equal(got, data[order])
-
-
-def test_sweep_one_id_and_two_fields():
-    """Every row in one id (per-wave counts of 256, tile counts of 4096), and
-    two fields sorted by the same ids on one workspace."""
-    from mpi_grid_redistribute_amd.redistributor import _IdField, _sort_by_ids
-    n = 4096 * 300 + 5
-    ids = np.full(n, 511, dtype=np.uint16)
-    ids[::1000] = 3
-    a = np.arange(n, dtype=np.int32)
-    b = np.random.default_rng(1).integers(0, 256, (n, 12), dtype=np.uint8)
-    fa = _IdField(torch.from_numpy(a).cuda().view(torch.uint8))
-    fa.row_bytes = 4
-    fb = _IdField(torch.from_numpy(b).cuda().reshape(-1))
-    fb.row_bytes = 12
-    dev = torch.device("cuda", torch.cuda.current_device())
-    outs, counts = _sort_by_ids([fa, fb], torch.from_numpy(ids.view(np.int16)).cuda(), n, 512,
-                                dev, path="sweep")
-    order = np.argsort(ids, kind="stable")
-    assert np.array_equal(outs[0][: 4 * n].view(torch.int32).cpu().numpy(), order)
-    assert np.array_equal(outs[1][: 12 * n].cpu().numpy().reshape(n, 12), b[order])
-    assert counts[511].item() == n - len(ids[::1000])

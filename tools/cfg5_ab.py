@@ -54,10 +54,6 @@ def main():
         recv.reshape(-1), 36, rpos, fine_cells=[8, 8, 8])
     fids = fids.clone()
     flat = rec.reshape(-1)
-    from mpi_grid_redistribute_amd.redistributor import _IdField, _sort_by_ids
-    rows = _IdField(recv.reshape(-1))
-    rows.row_bytes = 36
-    dev = torch.device("cuda", torch.cuda.current_device())
     for _ in range(repeat):
         for v in variants:
             for k, x in v.items():
@@ -65,12 +61,7 @@ def main():
             res = {"variant": v,
                    "src_plain": timed(lambda: part.partition_device(flat, 36, pos)),
                    "src_fine": timed(lambda: part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])),
-                   "dst_sort": timed(lambda: R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=fids)),
-                   # the destination sort's two paths on the same ids
-                   "dst_sweep": timed(lambda: _sort_by_ids([rows], fids, N, 512, dev,
-                                                           check_ids=False, path="sweep")),
-                   "dst_ranked": timed(lambda: _sort_by_ids([rows], fids, N, 512, dev,
-                                                            check_ids=False, path="ranked"))}
+                   "dst_sort": timed(lambda: R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=fids))}
             print(json.dumps(res), flush=True)
             for k in v:
                 _lib.test_hook(k, _lib.HOOK_DEFAULTS[k])
