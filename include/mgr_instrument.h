@@ -23,15 +23,14 @@ extern "C" {
  * "rank_rows" (0 / 2048 / 4096 ranked fine-sort tiles), "bin_unstaged" (bin
  * kernel without LDS slab staging), "bin_generic" (bin kernel with run-time
  * geometry for simple plans), "pack_generic" (the wave-per-tile pack for <= 64
- * bins), "msel_lists" (the halo selections by the list kernel where the
- * stream kernel would run), "scan_delay_bin" / "scan_delay_sleeps" (the scan
- * chunk that ends that bin counts itself done, then sleeps that many
- * s_sleep(127) before storing its inclusive word: the visibility order
- * relaxed atomics on two words allow, forced) and "scan_end_spins" (polls of
- * the bin-end words by the scan's last chunk, -1 = scan_spins; 0 = one look,
- * which then reports the forced race as a failed scan).  Each call publishes
- * a new immutable snapshot of every hook (the library's launches read one
- * snapshot each); < 0 for an unknown key or an out-of-range value.         */
+ * bins), "scan_delay_bin" / "scan_delay_sleeps" (the scan chunk that ends
+ * that bin counts itself done, then sleeps that many s_sleep(127) before
+ * storing its inclusive word: the visibility order relaxed atomics on two
+ * words allow, forced) and "scan_end_spins" (polls of the bin-end words by
+ * the scan's last chunk, -1 = scan_spins; 0 = one look, which then reports
+ * the forced race as a failed scan).  Each call publishes a new immutable snapshot of every hook (the
+ * library's launches read one snapshot each); < 0 for an unknown key or an
+ * out-of-range value.                                                      */
 int mgr_test_hook(const char* key, int64_t value);
 
 /* ----------------------------------------------------------- profiling --

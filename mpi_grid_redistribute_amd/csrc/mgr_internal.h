@@ -161,7 +161,6 @@ struct Hooks {
     int bin_unstaged = 0;    // bin kernel without LDS slab staging (the wide / unaligned fallback)
     int bin_generic = 0;     // bin kernel with run-time geometry also for simple plans
     int pack_generic = 0;    // wave-per-tile pack_kernel also for <= 64 bins (the > 64-B row path)
-    int msel_lists = 0;      // halo selections by the list kernel also where the stream kernel runs
     // scan race test: the chunk that ends bin scan_delay_bin counts itself
     // done, then sleeps scan_delay_sleeps x s_sleep(127) before storing its
     // inclusive word;

@@ -53,7 +53,6 @@ int set_hook(const char* key, int64_t v) {
     else if (!strcmp(key, "bin_unstaged") && in(0, 1)) h->bin_unstaged = (int)v;
     else if (!strcmp(key, "bin_generic") && in(0, 1)) h->bin_generic = (int)v;
     else if (!strcmp(key, "pack_generic") && in(0, 1)) h->pack_generic = (int)v;
-    else if (!strcmp(key, "msel_lists") && in(0, 1)) h->msel_lists = (int)v;
     else if (!strcmp(key, "scan_delay_bin") && in(-1, MGR_MAX_BINS)) h->scan_delay_bin = (int)v;
     else if (!strcmp(key, "scan_delay_sleeps") && in(0, 1 << 16)) h->scan_delay_sleeps = (int)v;
     else if (!strcmp(key, "scan_end_spins") && in(-1, 1 << 30)) h->scan_end_spins = (int)v;

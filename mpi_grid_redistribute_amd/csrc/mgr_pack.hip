@@ -381,130 +381,6 @@ __global__ __launch_bounds__(256) void msel_pack_kernel(
     }
 }
 
-// Streaming multi-selection (round 5): one field whose rows are UPR units of
-// W bytes (UPR <= 4).  One wave per tile, its 64-row rounds in order, four
-// at a time: the rounds' flags arrive a group ahead; per round, NB ballots
-// (one per flag bit) give every set's members as a scalar AND of bit masks;
-// the units of the rows some set selects are loaded once, coalesced (lines
-// holding no selected row are never fetched); and for every set with a
-// member in the round, the members' units go to the set's next rows -- one
-// contiguous run, the rank of a member = the set's members below it
-// (popcount of the mask under its row).  No LDS lists, no gathers: the list
-// kernel's per-row chain (entry -> set -> slot -> address -> load -> store)
-// becomes per-set scalar masks and UPR store instructions per set and round.
-// Set k's next output row lives in lane k (readlane).
-struct SetDst {
-    uint8_t* d[kMaxSets];
-};
-constexpr int kStreamGroup = 4;   // rounds whose units are loaded together
-
-template <int W, int UPR, int NB>
-__global__ __launch_bounds__(256) void msel_stream_kernel(
-    const uint8_t* __restrict__ src, SetDst dsts, int nsets, SetMasks masks, int64_t n,
-    const uint16_t* __restrict__ flags, const int64_t* __restrict__ offsets,
-    const int64_t* __restrict__ set_starts, int64_t T, int tile_rows, long long cap,
-    const uint32_t* __restrict__ scan_err) {
-    using UT = typename Unit<W>::T;
-    using GU = __attribute__((address_space(1))) UT;
-    constexpr int RB = W * UPR, G = kStreamGroup;
-    const int w = threadIdx.x >> 6, lane = lane_id();
-    const int64_t tile = (int64_t)blockIdx.x * 4 + w;
-    if (tile >= T || scan_failed(scan_err)) return;
-    const int64_t row0 = tile * (int64_t)tile_rows;
-    const int rows = (int)min((int64_t)tile_rows, n - row0);
-    // lane k: set k's destination and next output row (set_starts == nullptr:
-    // the sets back to back from one base, placed on the device), its mask
-    const unsigned long long ldst = lane < nsets ? (unsigned long long)dsts.d[lane] : 0ull;
-    long long lat = lane < nsets ? offsets[(int64_t)lane * T + tile] -
-                                       (set_starts ? set_starts[lane] : 0) : 0;
-    const unsigned lmask = lane < nsets ? (unsigned)masks.m[lane] : 0u;
-    const int nbits = NB > 0 ? NB : mask_bits(masks, nsets);
-    const GU* sp = (const GU*)(src + row0 * RB);
-    const uint16_t* fp = flags + row0;
-    unsigned fcur[G], fnext[G];
-#pragma unroll
-    for (int q = 0; q < G; ++q) fcur[q] = 64 * q + lane < rows ? fp[64 * q + lane] : 0u;
-    for (int g0 = 0; g0 < rows; g0 += 64 * G) {
-#pragma unroll
-        for (int q = 0; q < G; ++q) {   // the next group's flags
-            const int r = g0 + 64 * (G + q) + lane;
-            fnext[q] = r < rows ? fp[r] : 0u;
-        }
-        // per round: one ballot per flag bit; a row no set can select has no bits
-        unsigned long long fb[G][NB > 0 ? NB : 16];
-        unsigned long long anyb[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-            anyb[q] = __ballot(fcur[q] != 0u);
-#pragma unroll
-            for (int i = 0; i < (NB > 0 ? NB : 16); ++i)
-                fb[q][i] = (NB > 0 || i < nbits) ? __ballot((fcur[q] >> i) & 1u) : 0ull;
-        }
-        // the units of the rows with a flag, every round of the group at once
-        UT v[G][UPR];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-#pragma unroll
-            for (int j = 0; j < UPR; ++j) {
-                const int u = 64 * j + lane, r = u / UPR;
-                if ((anyb[q] >> r) & 1ull) v[q][j] = sp[(int64_t)(g0 + 64 * q) * UPR + u];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-            if (!anyb[q]) continue;
-            for (int k = 0; k < nsets; ++k) {
-                const unsigned mk = (unsigned)__builtin_amdgcn_readlane((int)lmask, k);
-                unsigned long long m = anyb[q];
-#pragma unroll
-                for (int i = 0; i < (NB > 0 ? NB : 16); ++i)
-                    if (NB > 0 || i < nbits) m &= ((mk >> i) & 1u) ? fb[q][i] : ~0ull;
-                if (!m) continue;
-                const long long base = readlane64(lat, k);
-                GU* d = (GU*)readlane64(ldst, k);
-#pragma unroll
-                for (int j = 0; j < UPR; ++j) {
-                    const int u = 64 * j + lane, r = u / UPR, part = u - r * UPR;
-                    if ((m >> r) & 1ull) {
-                        const long long o = base + __popcll(m & ((1ull << r) - 1ull));
-                        if (o < cap && d) d[o * UPR + part] = v[q][j];
-                    }
-                }
-                if (lane == k) lat += __popcll(m);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < G; ++q) fcur[q] = fnext[q];
-    }
-}
-
-// The stream kernel for one field: W / UPR from the field's alignment and
-// size (UPR <= 4, W >= 2); hipErrorNotSupported otherwise (the list kernel).
-template <int NB>
-static hipError_t msel_stream_nb(const void* src, int64_t row_bytes, const SetDst& d, int nsets,
-                                 const SetMasks& sb, int64_t n, const uint16_t* flags,
-                                 int tile_rows, const Workspace& ws, long long cap, bool placed,
-                                 int wlog, hipStream_t s) {
-    const int W = 1 << wlog;
-    if (W < 2 || row_bytes % W || row_bytes / W > 4) return hipErrorNotSupported;
-    const int upr = (int)(row_bytes / W);
-    const dim3 grid((unsigned)((ws.T + 3) / 4));
-#define MGR_MS(W_, U_)                                                                        \
-    if (W == W_ && upr == U_) {                                                               \
-        hipLaunchKernelGGL((msel_stream_kernel<W_, U_, NB>), grid, dim3(256), 0, s,           \
-                           (const uint8_t*)src, d, nsets, sb, n, flags, ws.offsets,           \
-                           placed ? nullptr : ws.bin_starts, ws.T, tile_rows, cap,            \
-                           ws.scan_err);                                                      \
-        return hipGetLastError();                                                             \
-    }
-    MGR_MS(16, 1) MGR_MS(16, 2) MGR_MS(16, 3) MGR_MS(16, 4)
-    MGR_MS(8, 1) MGR_MS(8, 2) MGR_MS(8, 3) MGR_MS(8, 4)
-    MGR_MS(4, 1) MGR_MS(4, 2) MGR_MS(4, 3) MGR_MS(4, 4)
-    MGR_MS(2, 1) MGR_MS(2, 2) MGR_MS(2, 3) MGR_MS(2, 4)
-#undef MGR_MS
-    return hipErrorNotSupported;
-}
-
 hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t* row_bytes,
                             int64_t n, const uint16_t* flags, int nsets, const int* masks,
                             int tile_rows, const Workspace& ws, void* const* dsts, hipStream_t s,
@@ -512,44 +388,6 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
     if (n <= 0) return hipSuccess;
     if (nfields < 1 || nfields > kSelFields || nsets < 1 || nsets > kMaxSets)
         return hipErrorInvalidValue;
-    if (!hooks().msel_lists) {
-        // the stream kernel, one launch per field, when every field takes it
-        SetMasks sb{};
-        unsigned um = 0;
-        for (int k = 0; k < nsets; ++k) {
-            sb.m[k] = (uint16_t)masks[k];
-            um |= (unsigned)masks[k];
-        }
-        const int nb = flag_bits_class(um ? 32 - __builtin_clz(um) : 0);
-        bool ok = true;
-        int wl[kSelFields];
-        SetDst d[kSelFields];
-        for (int f = 0; f < nfields && ok; ++f) {
-            uintptr_t a = (uintptr_t)srcs[f] | (uintptr_t)row_bytes[f];
-            for (int k = 0; k < nsets; ++k) {
-                d[f].d[k] = cap_rows >= 0 ? (uint8_t*)dsts[f]
-                            : dsts[0 * nsets + k] ? (uint8_t*)dsts[f * nsets + k] : nullptr;
-                a |= (uintptr_t)d[f].d[k];
-            }
-            wl[f] = (a & 15) == 0 ? 4 : (a & 7) == 0 ? 3 : (a & 3) == 0 ? 2 : (a & 1) == 0 ? 1 : 0;
-            while (wl[f] > 1 && row_bytes[f] / (1 << wl[f]) < 1) --wl[f];
-            ok = wl[f] >= 1 && row_bytes[f] % (1 << wl[f]) == 0 && row_bytes[f] / (1 << wl[f]) <= 4;
-        }
-        if (ok) {
-            const long long cap = cap_rows >= 0 ? (long long)cap_rows : (long long)INT64_MAX;
-            prof_begin(s, K_HALO_PACK);
-            hipError_t e = hipSuccess;
-            for (int f = 0; f < nfields && e == hipSuccess; ++f) {
-#define MGR_NB(NB_) e = msel_stream_nb<NB_>(srcs[f], row_bytes[f], d[f], nsets, sb, n, flags, \
-                                            tile_rows, ws, cap, cap_rows >= 0, wl[f], s)
-                if (nb == 2) MGR_NB(2); else if (nb == 4) MGR_NB(4); else if (nb == 6) MGR_NB(6);
-                else if (nb == 8) MGR_NB(8); else MGR_NB(0);
-#undef MGR_NB
-            }
-            prof_end(s, K_HALO_PACK);
-            if (e != hipErrorNotSupported) return e;
-        }
-    }
     SetMasks sb{};
     for (int k = 0; k < nsets; ++k) sb.m[k] = (uint16_t)masks[k];
     SelFields fs{};

@@ -41,7 +41,6 @@ VARIANTS = [
     {"scan_max_chunks": 8, "scan_chunk": 256},
     {"pack_img_all": 1},
     {"pack_img_all": 1, "tile_rounds": 16},
-    {"msel_lists": 1},   # the halo selections' list kernel (the stream kernel is the default)
 ]
 
 
