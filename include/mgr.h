@@ -43,11 +43,10 @@ typedef enum {
     MGR_EUNSUPPORTED = -4 /* valid request this build does not implement   */
 } mgr_status;
 
-/* Element types.  Positions: MGR_F16, MGR_F32, MGR_F64, MGR_I32, MGR_I64
- * (the reference bins any numpy column, redist.py:68-69).  box_length: any
- * of these and the narrower integers below (numpy's promotion of
- * position % box and position / box depends on the box's dtype, S9/S11a).
- * rank ids: MGR_F32, MGR_F64, MGR_I32, MGR_I64.                           */
+/* Element types.  Positions and box_length: any of them (the reference
+ * bins any numeric numpy column, redist.py:68-69; numpy's promotion of
+ * position % box and position / box depends on both dtypes, S9/S11a).
+ * Rank ids: MGR_F32, MGR_F64, MGR_I32, MGR_I64.                           */
 typedef enum {
     MGR_F32 = 1,
     MGR_F64 = 2,
@@ -56,10 +55,11 @@ typedef enum {
     MGR_F16 = 5,
     MGR_I8 = 6,
     MGR_I16 = 7,
-    MGR_U8 = 8,   /* also numpy bool (same promotions against positions)  */
+    MGR_U8 = 8,
     MGR_U16 = 9,
     MGR_U32 = 10,
-    MGR_U64 = 11
+    MGR_U64 = 11,
+    MGR_B8 = 12   /* numpy bool, one byte                                   */
 } mgr_dtype;
 
 typedef struct mgr_plan mgr_plan; /* grid geometry of one rank            */
@@ -119,11 +119,11 @@ int mgr_dest_bytes(int nbins);
  *      wrap of every index and the row-major dot.
  * Bit-exact with numpy 2.2.6 (NaN/out-of-range bins
  * like x86's INT64_MIN).  pos: n rows, row r coordinate d at
- * pos[r*row_stride + d] (elements), dtype MGR_F16, MGR_F32, MGR_F64,
- * MGR_I32 or MGR_I64.  Integer and float16 positions follow numpy's
- * promotion (see mgr_plan_create): the wrap is computed in the promoted type
- * and cast back on the in-place write-back (float -> int by x86 truncation,
- * -> float16 rounded to nearest even), the bin reads the stored value back.
+ * pos[r*row_stride + d] (elements), any mgr_dtype.  Positions other than
+ * float32 / float64 follow numpy's promotion (see mgr_plan_create): the wrap
+ * is computed in the promoted type and cast back on the in-place write-back
+ * (float -> integer as numpy's x86 casts, -> float16 rounded to nearest even,
+ * -> bool != 0), the bin reads the stored value back.
  *
  * mgr_bin_count : writes dest[r] (mgr_dest_bytes(nbins) wide) and the per
  *                 tile histogram into the workspace; feeds mgr_scan.

@@ -16,14 +16,22 @@ import torch
 
 from . import _lib
 
-# position dtypes the binning kernels take (redist.py:68-69 bins any numpy
-# column; these are the ones with a kernel, everything else is refused)
+# position dtypes the binning kernels take: every float, integer and bool
+# dtype (redist.py:68-69 bins any numeric numpy column).  float128 (x87
+# extended precision) and complex are refused: the GPU has no extended float,
+# and numpy's remainder is undefined for complex (the reference raises too).
+_BOX_CODES = {"f2": _lib.MGR_F16, "f4": _lib.MGR_F32, "f8": _lib.MGR_F64, "i1": _lib.MGR_I8,
+              "i2": _lib.MGR_I16, "i4": _lib.MGR_I32, "i8": _lib.MGR_I64, "u1": _lib.MGR_U8,
+              "b1": _lib.MGR_B8, "u2": _lib.MGR_U16, "u4": _lib.MGR_U32, "u8": _lib.MGR_U64}
+_NP_POS_CODES = {np.dtype(k): v for k, v in _BOX_CODES.items()}
 _POS_CODES = {torch.float16: _lib.MGR_F16, torch.float32: _lib.MGR_F32,
-              torch.float64: _lib.MGR_F64, torch.int32: _lib.MGR_I32, torch.int64: _lib.MGR_I64}
-_NP_POS_CODES = {np.dtype(np.float16): _lib.MGR_F16, np.dtype(np.float32): _lib.MGR_F32,
-                 np.dtype(np.float64): _lib.MGR_F64, np.dtype(np.int32): _lib.MGR_I32,
-                 np.dtype(np.int64): _lib.MGR_I64}
-_POS_NAMES = "float16/float32/float64/int32/int64"
+              torch.float64: _lib.MGR_F64, torch.int8: _lib.MGR_I8, torch.int16: _lib.MGR_I16,
+              torch.int32: _lib.MGR_I32, torch.int64: _lib.MGR_I64, torch.uint8: _lib.MGR_U8,
+              torch.bool: _lib.MGR_B8}
+for _name, _code in (("uint16", _lib.MGR_U16), ("uint32", _lib.MGR_U32), ("uint64", _lib.MGR_U64)):
+    if hasattr(torch, _name):
+        _POS_CODES[getattr(torch, _name)] = _code
+_POS_NAMES = "float16/32/64, (u)int8-64, bool"
 _ID_CODES = {torch.int32: _lib.MGR_I32, torch.int64: _lib.MGR_I64, torch.float32: _lib.MGR_F32,
              torch.float64: _lib.MGR_F64}
 
@@ -175,11 +183,6 @@ def pos_code(dtype):
     if code is None:
         raise TypeError(f"position dtype {dtype} not supported ({_POS_NAMES})")
     return code
-
-
-_BOX_CODES = {"f2": _lib.MGR_F16, "f4": _lib.MGR_F32, "f8": _lib.MGR_F64, "i1": _lib.MGR_I8,
-              "i2": _lib.MGR_I16, "i4": _lib.MGR_I32, "i8": _lib.MGR_I64, "u1": _lib.MGR_U8,
-              "b1": _lib.MGR_U8, "u2": _lib.MGR_U16, "u4": _lib.MGR_U32, "u8": _lib.MGR_U64}
 
 
 def box_dtype_code(box: np.ndarray):

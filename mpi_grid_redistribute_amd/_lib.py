@@ -19,9 +19,10 @@ LIB_PATH = os.path.join(_HERE, "libmgr.so")
 
 MGR_OK = 0
 MGR_F32, MGR_F64, MGR_I32, MGR_I64 = 1, 2, 3, 4
-MGR_F16, MGR_I8, MGR_I16, MGR_U8, MGR_U16, MGR_U32, MGR_U64 = 5, 6, 7, 8, 9, 10, 11
+MGR_F16, MGR_I8, MGR_I16, MGR_U8, MGR_U16, MGR_U32, MGR_U64, MGR_B8 = 5, 6, 7, 8, 9, 10, 11, 12
 # element bytes of the position dtypes (mgr_bin_count & co.)
-POS_ITEMSIZE = {MGR_F16: 2, MGR_F32: 4, MGR_F64: 8, MGR_I32: 4, MGR_I64: 8}
+POS_ITEMSIZE = {MGR_F16: 2, MGR_F32: 4, MGR_F64: 8, MGR_I8: 1, MGR_I16: 2, MGR_I32: 4,
+                MGR_I64: 8, MGR_U8: 1, MGR_U16: 2, MGR_U32: 4, MGR_U64: 8, MGR_B8: 1}
 UNIQUE_ID_BYTES = 128
 
 _P = ctypes.c_void_p

@@ -358,8 +358,8 @@ static hipError_t bin_count_d(const Geom& g, void* pos, int64_t n, int64_t strid
     return bin_count_p<PosT, uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fo);
 }
 
-// int32 / int64 / float16 positions (bin_coord_ext): each lane reads its own
-// row (no slab staging: float16 rows need not be 4-byte multiples), run-time
+// integer / float16 / bool positions (bin_coord_ext): each lane reads its
+// own row (no slab staging: such rows need not be 4-byte multiples), run-time
 // dimensionality -- the general path of every plan.
 template <typename PosT, typename DestT>
 static hipError_t bin_count_ext(const Geom& g, void* pos, int64_t n, int64_t stride, int periodic,
@@ -391,6 +391,13 @@ hipError_t launch_bin_count(const Geom& g, void* pos, int pos_dtype, int64_t n, 
         case MGR_I32: e = bin_count_ext_d<int32_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
         case MGR_I64: e = bin_count_ext_d<int64_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
         case MGR_F16: e = bin_count_ext_d<f16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_I8: e = bin_count_ext_d<int8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_I16: e = bin_count_ext_d<int16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_U8: e = bin_count_ext_d<uint8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_U16: e = bin_count_ext_d<uint16_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_U32: e = bin_count_ext_d<uint32_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_U64: e = bin_count_ext_d<uint64_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
+        case MGR_B8: e = bin_count_ext_d<b8_t>(g, pos, n, stride, periodic, dest, tile_rows, ws, s, fg, hg, fine_out); break;
         default: e = hipErrorInvalidValue;
     }
     prof_end(s, kid);
@@ -609,6 +616,13 @@ hipError_t launch_cell_ids(const Geom& g, void* pos, int pos_dtype, int64_t n, i
         case MGR_I32: e = cell_ids_t<int32_t>(g, pos, n, stride, periodic, cell, idx, s); break;
         case MGR_I64: e = cell_ids_t<int64_t>(g, pos, n, stride, periodic, cell, idx, s); break;
         case MGR_F16: e = cell_ids_t<f16_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_I8: e = cell_ids_t<int8_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_I16: e = cell_ids_t<int16_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_U8: e = cell_ids_t<uint8_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_U16: e = cell_ids_t<uint16_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_U32: e = cell_ids_t<uint32_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_U64: e = cell_ids_t<uint64_t>(g, pos, n, stride, periodic, cell, idx, s); break;
+        case MGR_B8: e = cell_ids_t<b8_t>(g, pos, n, stride, periodic, cell, idx, s); break;
         default: e = hipErrorInvalidValue;
     }
     prof_end(s, K_CELL_IDS);

@@ -149,6 +149,7 @@ static bool dtype_kind(int t, Kind* out) {
         case MGR_U16: *out = {'u', 2}; return true;
         case MGR_U32: *out = {'u', 4}; return true;
         case MGR_U64: *out = {'u', 8}; return true;
+        case MGR_B8: *out = {'b', 1}; return true;
         default: return false;
     }
 }
@@ -161,6 +162,9 @@ static int dtype_of(Kind k) {
 static int promote(int a, int b) {
     Kind x, y;
     if (!dtype_kind(a, &x) || !dtype_kind(b, &y)) return 0;
+    if (x.k == 'b' && y.k == 'b') return MGR_I8;   // bool % bool: numpy's int8 loop
+    if (x.k == 'b') return b;                        // bool joins anything as that type
+    if (y.k == 'b') return a;
     if (x.k == 'f' || y.k == 'f') {
         // an integer joins a float as the smallest float holding it exactly
         // (8-bit -> float16, 16-bit -> float32, wider -> float64)
@@ -174,7 +178,8 @@ static int promote(int a, int b) {
     return MGR_F64;   // int64 with uint64
 }
 static bool is_pos_dtype(int t) {
-    return t == MGR_F16 || t == MGR_F32 || t == MGR_F64 || t == MGR_I32 || t == MGR_I64;
+    Kind k;
+    return dtype_kind(t, &k);   // every float, integer and bool dtype
 }
 
 // The per-call modes of a plan's geometry for positions of pos_dtype: the
@@ -327,7 +332,7 @@ static int check_tile(int tile_rows) {
 static int check_pos(const mgr_plan* plan, const void* pos, int dtype, int64_t n, int64_t stride) {
     if (!plan) return fail(MGR_EINVAL, "null plan");
     if (!is_pos_dtype(dtype))
-        return fail(MGR_EINVAL, "positions must be float16/32/64 or int32/64 (dtype %d)", dtype);
+        return fail(MGR_EINVAL, "positions must be a float, integer or bool dtype (dtype %d)", dtype);
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (n > 0 && !pos) return fail(MGR_EINVAL, "null positions");
     if (stride < plan->g.dim) return fail(MGR_EINVAL, "row_stride %lld < dim %d", (long long)stride, plan->g.dim);
@@ -664,7 +669,7 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
 int mgr_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t row_stride, int dim,
                    const double* hi, const double* lo, uint16_t* flags, void* stream) {
     if (!is_pos_dtype(pos_dtype))
-        return fail(MGR_EINVAL, "positions must be float16/32/64 or int32/64 (dtype %d)", pos_dtype);
+        return fail(MGR_EINVAL, "positions must be a float, integer or bool dtype (dtype %d)", pos_dtype);
     if (dim < 1 || dim > MGR_MAX_DIM) return fail(MGR_EINVAL, "dim %d", dim);
     if (n < 0) return fail(MGR_EINVAL, "n < 0");
     if (row_stride < dim) return fail(MGR_EINVAL, "row_stride %lld < dim %d", (long long)row_stride, dim);

@@ -199,22 +199,65 @@ __device__ __forceinline__ int trunc_i32(double v) {
     return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : INT_MIN;
 }
 
+// numpy bool positions (one byte, 0 / 1).
+struct b8_t {
+    uint8_t u;
+};
+
+// The positions' dtypes beyond float32 / float64: every integer width,
+// float16 and bool (bin_coord_ext).
 template <typename P>
-constexpr bool kExtPos = std::is_same<P, int32_t>::value || std::is_same<P, int64_t>::value ||
-                         std::is_same<P, f16_t>::value;
+constexpr bool kExtPos = std::is_integral<P>::value || std::is_same<P, f16_t>::value ||
+                         std::is_same<P, b8_t>::value;
 
 // A stored position as numpy promotes it against a float64 scalar (the
 // quotient of integer positions, the halo's float64 comparisons).
 template <typename PosT>
 __device__ __forceinline__ double pos_as_f64(PosT v) {
     if constexpr (std::is_same<PosT, f16_t>::value) return h2d(v.u);
+    else if constexpr (std::is_same<PosT, b8_t>::value) return v.u ? 1.0 : 0.0;
     else if constexpr (std::is_same<PosT, float>::value) return f32_to_f64_x86(v);
-    else return (double)v;   // int64: round to nearest, as numpy's cast
+    else return (double)v;   // 64-bit integers: round to nearest, as numpy's cast
+}
+
+// numpy's float -> integer casts on x86 (the in-place write-back of integer
+// positions wrapped in a float type; probed on numpy 2.2.6, pinned by
+// tests/golden/bin_dtypes.npz): <= 32-bit signed and <= 16-bit unsigned
+// types through a 32-bit cvttsd2si (NaN / out of range -> INT_MIN, then the
+// low bits), int64 through the 64-bit one; uint32 / uint64: values at or
+// above 2^(w-1) converted after subtracting it, the top bit flipped back;
+// bool: != 0.  A float32 / float16 wrap converts exactly to float64 first.
+template <typename P>
+__device__ __forceinline__ P pos_from_f64(double t) {
+    if constexpr (std::is_same<P, b8_t>::value) {
+        return b8_t{(uint8_t)(t != 0.0 ? 1 : 0)};
+    } else if constexpr (std::is_same<P, int64_t>::value) {
+        return (P)trunc_i64(t);
+    } else if constexpr (std::is_same<P, uint64_t>::value) {
+        return t >= 9223372036854775808.0
+                   ? (uint64_t)trunc_i64(t - 9223372036854775808.0) ^ 0x8000000000000000ull
+                   : (uint64_t)trunc_i64(t);
+    } else if constexpr (std::is_same<P, uint32_t>::value) {
+        return t >= 2147483648.0 ? (uint32_t)trunc_i32(t - 2147483648.0) ^ 0x80000000u
+                                 : (uint32_t)trunc_i32(t);
+    } else {
+        return (P)(unsigned)trunc_i32(t);
+    }
+}
+template <typename P>
+__device__ __forceinline__ P pos_from_int(long long t) {   // C truncation, as numpy's casts
+    if constexpr (std::is_same<P, b8_t>::value) return b8_t{(uint8_t)(t != 0 ? 1 : 0)};
+    else return (P)t;
+}
+template <typename P>
+__device__ __forceinline__ long long pos_int(P v) {   // unsigned 64-bit: the bits
+    if constexpr (std::is_same<P, b8_t>::value) return v.u ? 1 : 0;
+    else return (long long)v;
 }
 
 template <typename PosT>
 __device__ __forceinline__ bool same_bits(PosT a, PosT b) {
-    if constexpr (std::is_same<PosT, f16_t>::value) return a.u == b.u;
+    if constexpr (std::is_same<PosT, f16_t>::value || std::is_same<PosT, b8_t>::value) return a.u == b.u;
     else if constexpr (std::is_integral<PosT>::value) return a == b;
     else if constexpr (sizeof(PosT) == 8) return __double_as_longlong((double)a) == __double_as_longlong((double)b);
     else return __float_as_uint((float)a) == __float_as_uint((float)b);
@@ -266,26 +309,45 @@ __device__ __forceinline__ long long coord_index(long long k, long long kf, doub
     return k;
 }
 
-// One coordinate of an int32 / int64 / float16 position (kExtPos): numpy
+// One coordinate of an integer / float16 / bool position (kExtPos): numpy
 // 2.2.6's promotion of `position[:, d] % box[d]` (Geom::wmode) and of
 // `position[:, d] / box[d]` (Geom::dmode), mgr_capi.hip pos_modes:
-//   * integer positions, integer box: integer floor-mod at the promoted width
-//     (the `+ L` wraps like numpy's), stored back truncated to the column's
-//     width; the quotient is float64 (true division);
-//   * integer positions, float box: the wrap in float64, stored back by x86
-//     truncation (NaN / out of range -> INT_MIN), the quotient float64 from the
-//     stored integer;
+//   * integer positions, integer box: integer remainder at the promoted type
+//     (floor-mod for signed, plain for unsigned; the `+ L` wraps at its
+//     width), stored back truncated to the column's width; the quotient is
+//     float64 (true division);
+//   * integer / bool positions, float box: the wrap in the promoted float
+//     type (float64; float32 for <= 16-bit integers against a float32 box;
+//     float16 for 8-bit ones against a float16 box), stored back by numpy's
+//     x86 float -> int cast (pos_from_f64), the quotient from the stored
+//     value in the same float type;
 //   * float16 positions: the wrap in float64 / float32 rounded to float16 on
-//     the write-back (as S9 for float32), or -- box float16 / int8 / uint8 --
+//     the write-back (as S9 for float32), or -- box float16 / 8-bit integer --
 //     every operation in float32 rounded to float16 (numpy's half arithmetic);
 //     the quotient in float64, float32 or float16 alike, then * n in float64.
 // The general path only (no fast in-box variant): these dtypes are for
 // parity with the reference's inputs, not the bench's hot configurations.
-static __device__ __forceinline__ long long wrap_int(long long x, long long L, bool w32) {
-    const long long m = floormod_i64(x, L);   // numpy: x % 0 == 0
-    long long s = (long long)((unsigned long long)m + (unsigned long long)L);
-    if (w32) s = (long long)(int)(unsigned)s;
-    return floormod_i64(s, L);
+static __device__ __forceinline__ long long wrap_int(long long x, long long L, int wmode) {
+    const int bits = (wmode == MGR_I8 || wmode == MGR_U8) ? 8
+                   : (wmode == MGR_I16 || wmode == MGR_U16) ? 16
+                   : (wmode == MGR_I32 || wmode == MGR_U32) ? 32 : 64;
+    const bool sgn = wmode == MGR_I8 || wmode == MGR_I16 || wmode == MGR_I32 || wmode == MGR_I64;
+    auto norm = [&](unsigned long long v) -> unsigned long long {   // to the type's value
+        if (bits == 64) return v;
+        const unsigned long long m = (1ull << bits) - 1ull;
+        v &= m;
+        if (sgn && ((v >> (bits - 1)) & 1ull)) v |= ~m;
+        return v;
+    };
+    if (sgn) {
+        const long long m = floormod_i64(x, L);   // numpy: x % 0 == 0
+        const long long s = (long long)norm((unsigned long long)m + (unsigned long long)L);
+        return floormod_i64(s, L);
+    }
+    const unsigned long long ux = (unsigned long long)x, uL = (unsigned long long)L;
+    if (uL == 0ull) return 0;
+    const unsigned long long s = norm(ux % uL + uL);
+    return (long long)(s % uL);
 }
 static __device__ __forceinline__ uint16_t wrap_f16(uint16_t x, float L) {
     const float m = pymodf(h2f(x), L);
@@ -310,28 +372,27 @@ __device__ __forceinline__ long long bin_coord_ext(PosT* p, const Geom& g, int d
             else
                 s.u = wrap_f16(in.u, g.Lf[d]);
         } else {
-            if (g.wmode == MGR_F64) {
-                const double t = wrap_f64((double)in, g.L[d], g.twoL[d], g.fast[d]);
-                s = sizeof(PosT) == 4 ? (PosT)trunc_i32(t) : (PosT)trunc_i64(t);
-            } else {
-                s = (PosT)wrap_int((long long)in, g.Li[d], g.wmode == MGR_I32);
-            }
+            if (g.wmode == MGR_F64)
+                s = pos_from_f64<PosT>(wrap_f64(pos_as_f64(in), g.L[d], g.twoL[d], g.fast[d]));
+            else if (g.wmode == MGR_F32)   // <= 16-bit integers / bool: exact in float32
+                s = pos_from_f64<PosT>((double)wrap_f32((float)pos_as_f64(in), g.Lf[d],
+                                                        g.twoLf[d], g.fastf[d]));
+            else if (g.wmode == MGR_F16)   // 8-bit integers / bool: exact in float16
+                s = pos_from_f64<PosT>((double)h2f(wrap_f16(f2h((float)pos_as_f64(in)), g.Lf[d])));
+            else
+                s = pos_from_int<PosT>(wrap_int(pos_int(in), g.Li[d], g.wmode));
         }
         if (!same_bits(s, in)) { *p = s; *dirty = true; }
     }
     long long k, kf = 0;
     const double xs = pos_as_f64(s);
-    double q = 0.0;   // the quotient as the float64 the `* n` promotes it to
-    if constexpr (std::is_same<PosT, f16_t>::value) {
-        if (g.dmode == MGR_F64) {
-            q = xs / g.L[d];
-        } else {   // the quotient in float32, or float16
-            float qf = h2f(s.u) / g.Lf[d];
-            if (g.dmode == MGR_F16) qf = h2f(f2h(qf));
-            q = (double)qf;
-        }
-    } else {
-        q = xs / g.L[d];   // integer positions: true division in float64
+    double q;   // the quotient as the float64 the `* n` promotes it to
+    if (g.dmode == MGR_F64) {
+        q = xs / g.L[d];
+    } else {   // the quotient in float32, or float16 (the stored value is exact in either)
+        float qf = (float)xs / g.Lf[d];
+        if (g.dmode == MGR_F16) qf = h2f(f2h(qf));
+        q = (double)qf;
     }
     k = trunc_i64(q * g.nd[d]);
     if (SIDE == kSideFine) kf = trunc_i64(q * fg->nd[d]);

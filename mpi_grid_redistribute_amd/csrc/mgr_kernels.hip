@@ -267,8 +267,9 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
 // exchange_overload_by_position (redist.py:202-309) selects, per dimension
 // d, the rows with position[:, d] > limits[d,1] - ol[d] (sent to the right
 // neighbour, :271/:274) and position[:, d] < limits[d,0] + ol[d] (to the
-// left, :272/:275).  numpy compares the column (float16/32/64, int32/64)
-// against the float64 threshold in float64 (pos_as_f64), NaN selects nothing.
+// left, :272/:275).  numpy compares the column (any float, integer or bool
+// dtype) against the float64 threshold in float64 (pos_as_f64), NaN selects
+// nothing.
 struct HaloThr { double hi[MGR_MAX_DIM]; double lo[MGR_MAX_DIM]; };
 
 // flags[r] bit 2d: coordinate d > hi[d]; bit 2d+1: coordinate d < lo[d].
@@ -536,6 +537,13 @@ hipError_t launch_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t 
         case MGR_F64: halo_flags_t<double>(pos, n, stride, dim, t, flags, s); break;
         case MGR_I32: halo_flags_t<int32_t>(pos, n, stride, dim, t, flags, s); break;
         case MGR_I64: halo_flags_t<int64_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_I8: halo_flags_t<int8_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_I16: halo_flags_t<int16_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_U8: halo_flags_t<uint8_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_U16: halo_flags_t<uint16_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_U32: halo_flags_t<uint32_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_U64: halo_flags_t<uint64_t>(pos, n, stride, dim, t, flags, s); break;
+        case MGR_B8: halo_flags_t<b8_t>(pos, n, stride, dim, t, flags, s); break;
         default: halo_flags_t<f16_t>(pos, n, stride, dim, t, flags, s); break;
     }
     prof_end(s, K_HALO);

@@ -61,9 +61,10 @@ def _ptr(a):
 
 
 # oracle_bin_ext dtype codes (the O_* of mgr_oracle.c)
-_CODES = {np.dtype(np.float32): 1, np.dtype(np.float64): 2, np.dtype(np.int32): 3,
-          np.dtype(np.int64): 4, np.dtype(np.float16): 5}
-_EXT = {np.dtype(np.int32): 3, np.dtype(np.int64): 4, np.dtype(np.float16): 5}
+_CODES = {np.dtype(k): v for k, v in {"f4": 1, "f8": 2, "i4": 3, "i8": 4, "f2": 5, "i1": 6,
+                                       "i2": 7, "u1": 8, "u2": 9, "u4": 10, "u8": 11,
+                                       "b1": 12}.items()}
+_EXT = {k: v for k, v in _CODES.items() if v > 2}
 
 
 def bin_positions(position, grid_topology, box_length, periodic=True, compute_f32=None,

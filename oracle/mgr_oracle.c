@@ -131,7 +131,7 @@ void oracle_bin(void* pos, int pos_is_f32, int compute_f32, int64_t n, int64_t r
                           periodic, idx, 0);
 }
 
-/* ---- int32 / int64 / float16 positions (redist.py:68-69 on any numpy column).
+/* ---- integer / float16 / bool positions (redist.py:68-69 on any numpy column).
  * numpy 2.2.6 float16 conversions, restated from their documented behaviour:
  * round to nearest even with overflow to inf; NaN keeps sign and payload
  * (shifted), never quieted, forced nonzero; half arithmetic = the float32
@@ -205,13 +205,81 @@ uint16_t oracle_d2h(double x) { return d2h(x); }
 uint16_t oracle_f2h(float x) { return f2h(x); }
 double oracle_h2d(uint16_t h) { return h2d(h); }
 
-enum { O_F32 = 1, O_F64 = 2, O_I32 = 3, O_I64 = 4, O_F16 = 5 };
+enum { O_F32 = 1, O_F64 = 2, O_I32 = 3, O_I64 = 4, O_F16 = 5, O_I8 = 6, O_I16 = 7, O_U8 = 8,
+       O_U16 = 9, O_U32 = 10, O_U64 = 11, O_B8 = 12 };
 
-/* Bin n rows of int32 / int64 / float16 positions (pos_dtype O_*).  wmode:
- * numpy's type of position % box (O_F16/F32/F64/I32/I64), dmode: of
- * position / box (O_F16/F32/F64) -- the caller takes both from numpy itself
- * (c_oracle.bin_positions).  The wrap is stored back cast to the column's
- * type; binning reads the stored value (S2). */
+static int o_bits(int t) {
+    switch (t) {
+        case O_I8: case O_U8: case O_B8: return 8;
+        case O_I16: case O_U16: case O_F16: return 16;
+        case O_I32: case O_U32: case O_F32: return 32;
+        default: return 64;
+    }
+}
+static int o_signed(int t) { return t == O_I8 || t == O_I16 || t == O_I32 || t == O_I64; }
+
+/* an integer / bool column element, widened (unsigned 64-bit: its bits) */
+static int64_t o_load(const void* pos, int t, int64_t e) {
+    switch (t) {
+        case O_I8: return ((const int8_t*)pos)[e];
+        case O_I16: return ((const int16_t*)pos)[e];
+        case O_I32: return ((const int32_t*)pos)[e];
+        case O_I64: return ((const int64_t*)pos)[e];
+        case O_U8: return ((const uint8_t*)pos)[e];
+        case O_U16: return ((const uint16_t*)pos)[e];
+        case O_U32: return ((const uint32_t*)pos)[e];
+        case O_B8: return ((const uint8_t*)pos)[e] != 0;
+        default: return (int64_t)((const uint64_t*)pos)[e];
+    }
+}
+static void o_store(void* pos, int t, int64_t e, int64_t v) {   /* C truncation; bool != 0 */
+    switch (t) {
+        case O_I8: case O_U8: ((uint8_t*)pos)[e] = (uint8_t)v; break;
+        case O_B8: ((uint8_t*)pos)[e] = v != 0; break;
+        case O_I16: case O_U16: ((uint16_t*)pos)[e] = (uint16_t)v; break;
+        case O_I32: case O_U32: ((uint32_t*)pos)[e] = (uint32_t)v; break;
+        default: ((uint64_t*)pos)[e] = (uint64_t)v; break;
+    }
+}
+static double o_as_f64(int t, int64_t v) {
+    return t == O_U64 ? (double)(uint64_t)v : (double)v;
+}
+/* numpy's float -> integer cast on x86, written out (not left to the C
+ * compiler: out-of-range conversions are undefined in C): 32-bit cvttsd2si
+ * for <= 32-bit signed and <= 16-bit unsigned types, 64-bit for int64,
+ * uint32 / uint64 offset by 2^(w-1) at and above it; bool != 0. */
+static int64_t o_from_f64(int t, double x) {
+    if (t == O_B8) return x != 0.0;
+    if (t == O_I64) return trunc_i64(x);
+    if (t == O_U64)
+        return x >= 9223372036854775808.0
+                   ? (int64_t)((uint64_t)trunc_i64(x - 9223372036854775808.0) ^ 0x8000000000000000ull)
+                   : trunc_i64(x);
+    if (t == O_U32)
+        return x >= 2147483648.0 ? (int64_t)((uint32_t)trunc_i32(x - 2147483648.0) ^ 0x80000000u)
+                                 : (int64_t)(uint32_t)trunc_i32(x);
+    return trunc_i32(x);
+}
+/* numpy's integer remainder at type w (floor-mod signed, plain unsigned,
+ * x % 0 == 0), ((x % L) + L) % L with the + L wrapping at w's width */
+static int64_t o_wrap_int(int64_t x, int64_t L, int w) {
+    const int bits = o_bits(w), sgn = o_signed(w);
+    const uint64_t mask = bits == 64 ? ~0ull : (1ull << bits) - 1ull;
+    if (sgn) {
+        uint64_t s = (uint64_t)floormod_i64(x, L) + (uint64_t)L;
+        s &= mask;
+        if (bits < 64 && ((s >> (bits - 1)) & 1ull)) s |= ~mask;
+        return floormod_i64((int64_t)s, L);
+    }
+    const uint64_t ux = (uint64_t)x, uL = (uint64_t)L;
+    if (uL == 0) return 0;
+    return (int64_t)(((ux % uL + uL) & mask) % uL);
+}
+
+/* Bin n rows of integer / float16 / bool positions (pos_dtype O_*).  wmode:
+ * numpy's type of position % box, dmode: of position / box -- the caller
+ * takes both from numpy itself (c_oracle.bin_positions).  The wrap is stored
+ * back cast to the column's type; binning reads the stored value (S2). */
 void oracle_bin_ext(void* pos, int pos_dtype, int wmode, int dmode, int64_t n, int64_t row_stride,
                     int dim, const double* box, const int64_t* topo, int periodic, int64_t* cell,
                     int64_t* idx) {
@@ -239,33 +307,30 @@ void oracle_bin_ext(void* pos, int pos_dtype, int wmode, int dmode, int64_t n, i
                     }
                 }
                 xs = h2d(*p);
-                double q;
-                if (dmode == O_F64) q = xs / L;
-                else if (dmode == O_F32) q = (double)(h2f(*p) / Lf);
-                else q = (double)h2f(f2h(h2f(*p) / Lf));
-                const int64_t k = trunc_i64(q * (double)topo[d]);
-                if (idx) idx[r * dim + d] = k;
-                c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
-                continue;
-            }
-            int64_t x = pos_dtype == O_I32 ? (int64_t)((int32_t*)pos)[e] : ((int64_t*)pos)[e];
-            if (periodic) {
-                int64_t t;
-                if (wmode == O_F64) {
-                    const double w = pymod(pymod((double)x, L) + L, L);
-                    t = pos_dtype == O_I32 ? (int64_t)trunc_i32(w) : trunc_i64(w);
-                } else {   /* integer floor-mod at the promoted width; the + L wraps */
-                    const int64_t Li = (int64_t)L;
-                    uint64_t s = (uint64_t)floormod_i64(x, Li) + (uint64_t)Li;
-                    if (wmode == O_I32) s = (uint64_t)(int64_t)(int32_t)(uint32_t)s;
-                    t = floormod_i64((int64_t)s, Li);
+            } else {
+                if (periodic) {
+                    const int64_t x = o_load(pos, pos_dtype, e);
+                    int64_t t;
+                    if (wmode == O_F64) {
+                        t = o_from_f64(pos_dtype, pymod(pymod(o_as_f64(pos_dtype, x), L) + L, L));
+                    } else if (wmode == O_F32) {   /* <= 16-bit: exact in float32 */
+                        t = o_from_f64(pos_dtype, (double)pymodf(pymodf((float)x, Lf) + Lf, Lf));
+                    } else if (wmode == O_F16) {   /* 8-bit: exact in float16 */
+                        const uint16_t m = f2h(pymodf((float)x, Lf));
+                        const uint16_t y = f2h(h2f(m) + Lf);
+                        t = o_from_f64(pos_dtype, (double)h2f(f2h(pymodf(h2f(y), Lf))));
+                    } else {
+                        t = o_wrap_int(x, (int64_t)L, wmode);
+                    }
+                    o_store(pos, pos_dtype, e, t);
                 }
-                if (pos_dtype == O_I32) ((int32_t*)pos)[e] = (int32_t)(uint32_t)(uint64_t)t;
-                else ((int64_t*)pos)[e] = t;
-                x = pos_dtype == O_I32 ? (int64_t)((int32_t*)pos)[e] : ((int64_t*)pos)[e];
+                xs = o_as_f64(pos_dtype, o_load(pos, pos_dtype, e));
             }
-            xs = (double)x;
-            const int64_t k = trunc_i64(xs / L * (double)topo[d]);
+            double q;
+            if (dmode == O_F64) q = xs / L;
+            else if (dmode == O_F32) q = (double)((float)xs / Lf);
+            else q = (double)h2f(f2h((float)xs / Lf));
+            const int64_t k = trunc_i64(q * (double)topo[d]);
             if (idx) idx[r * dim + d] = k;
             c += offset[d] * floormod_i64(floormod_i64(k, topo[d]) + topo[d], topo[d]);
         }

@@ -409,11 +409,14 @@ BOX_KINDS = {  # how the caller spells box_length -> np.array(box_length) (redis
     "f32": lambda L: np.array([L], np.float32), "f16": lambda L: np.array([L], np.float16),
     "i8": lambda L: np.array([L], np.int8), "i16": lambda L: np.array([L], np.int16),
     "i32": lambda L: np.array([L], np.int32), "u32": lambda L: np.array([L], np.uint32),
-    "u64": lambda L: np.array([L], np.uint64),
+    "u64": lambda L: np.array([L], np.uint64), "u8": lambda L: np.array([L], np.uint8),
+    "b1": lambda L: np.array([bool(L)]),
 }
 
 
 def int_edge_values(L, rng, dt):
+    if dt == np.bool_:
+        return np.concatenate([np.array([False, True]), rng.random(40) < 0.5])
     info = np.iinfo(dt)
     L = int(L)
     v = [0, -1, 1, L - 1, L, L + 1, -L, -L + 1, 2 * L, -2 * L, 6 * L - 1, -6 * L + 1,
@@ -421,8 +424,8 @@ def int_edge_values(L, rng, dt):
     if dt == np.int64:
         v += [2 ** 53 + 1, -(2 ** 53 + 1), 2 ** 62, -(2 ** 62), 2 ** 31, -(2 ** 31) - 1]
     v = [x for x in v if info.min <= x <= info.max]
-    u = rng.integers(-6 * L, 6 * L + 1, 200)
-    w = rng.integers(info.min, info.max, 100, dtype=dt, endpoint=True)
+    u = rng.integers(max(-6 * L, int(info.min)), min(6 * L, int(info.max)) + 1, 64)
+    w = rng.integers(info.min, info.max, 32, dtype=dt, endpoint=True)
     return np.concatenate([np.array(v, dtype=dt), u.astype(dt), w])
 
 
@@ -435,9 +438,9 @@ def f16_edge_values(L, rng):
                      np.nextafter(np.float16(0), np.float16(1))], dtype=np.float16)
     bits = np.array([0x7c01, 0xfc01, 0x7e00, 0xfe00, 0x7d55, 0x0001, 0x8001, 0x03ff, 0x0400],
                     dtype=np.uint16).view(np.float16)
-    rnd = rng.integers(0, 1 << 16, 200).astype(np.uint16).view(np.float16)
-    u = rng.uniform(-6 * float(L), 6 * float(L), 200).astype(np.float16)
-    w = rng.uniform(0, float(L), 100).astype(np.float16)
+    rnd = rng.integers(0, 1 << 16, 96).astype(np.uint16).view(np.float16)
+    u = rng.uniform(-6 * float(L), 6 * float(L), 64).astype(np.float16)
+    w = rng.uniform(0, float(L), 32).astype(np.float16)
     return np.concatenate([v, near, bits, rnd, u, w])
 
 
@@ -449,19 +452,23 @@ def make_bin_dtypes(ref, rng):
     combos = [(10, 3), (7, 2), (64, 4), (100, 7), (1, 1), (2.5, 2), (0.3, 3), (1000.0, 5)]
     plan = {"i32": (np.int32, list(BOX_KINDS)), "i64": (np.int64, list(BOX_KINDS)),
             "f16": (np.float16, list(BOX_KINDS)),
-            "f32": (np.float32, ["f16", "i8", "i16", "i32", "u32", "u64"])}
+            "f32": (np.float32, ["f16", "i8", "i16", "i32", "u32", "u64", "u8", "b1"]),
+            "i8": (np.int8, list(BOX_KINDS)), "i16": (np.int16, list(BOX_KINDS)),
+            "u8": (np.uint8, list(BOX_KINDS)), "u16": (np.uint16, list(BOX_KINDS)),
+            "u32": (np.uint32, list(BOX_KINDS)), "u64": (np.uint64, list(BOX_KINDS)),
+            "b1": (np.bool_, list(BOX_KINDS))}
     for ci, (L, n) in enumerate(combos):
         integral = float(L) == int(L)
         for pname, (pdt, boxes) in plan.items():
             for bk in boxes:
                 if bk not in ("f64", "f32", "f16") and not integral:
                     continue
-                if bk == "i8" and L > 127:
+                if bk == "i8" and L > 127 or bk == "u8" and L > 255 or bk == "b1" and L != 1:
                     continue
                 for periodic in (True, False):
                     box = BOX_KINDS[bk](L)
                     with np.errstate(all="ignore"):
-                        if pdt in (np.int32, np.int64):
+                        if np.dtype(pdt).kind in "iub":
                             vals = int_edge_values(L, rng, pdt)
                         elif pdt == np.float16:
                             vals = f16_edge_values(L, rng)
@@ -494,6 +501,8 @@ DTYPE_CASES = [
     ("p4_f16pos_f16box", [2, 2, 1], np.array([1.0, 2.0, 1.0], np.float16), np.float16,
      (-0.3, 1.3)),
     ("p6_321_i64pos_intbox", [3, 2, 1], [30, 20, 10], np.int64, (-2.0, 3.0)),
+    ("p2_u16pos_intbox", [2, 1, 1], [60, 30, 20], np.uint16, (0.0, 3.0)),
+    ("p4_i8pos_f16box", [2, 2, 1], np.array([40.0, 20.0, 10.0], np.float16), np.int8, (-2.0, 3.0)),
 ]
 
 
@@ -502,6 +511,8 @@ def _dtype_positions(rng, n, box, pdt, lo_hi):
     p = rng.uniform(lo_hi[0], lo_hi[1], (n, len(b))) * b
     if np.issubdtype(pdt, np.integer):
         p = np.floor(p * (1 if b.min() >= 10 else 4))   # integer grid positions
+        info = np.iinfo(pdt)
+        p = np.clip(p, info.min, info.max)
     return p.astype(pdt)
 
 

@@ -156,23 +156,25 @@ def test_rank_ids_contract(lib):
 
 
 def test_position_and_box_dtypes(lib):
-    """Every box dtype code makes a plan; positions take float16/32/64 and
-    int32/64 only; an integer box must hold integers below 2^53."""
+    """Every dtype code makes a plan and takes positions (every float,
+    integer and bool dtype); unknown codes are refused; an integer box must
+    hold integers below 2^53."""
     import numpy as np
     from mpi_grid_redistribute_amd import _lib
     topo = np.array([2], dtype=np.int64)
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     h = ctypes.c_void_p()
-    for code in range(1, 12):
+    for code in range(1, 13):
         assert lib.mgr_plan_create(1, vp(topo), vp(np.array([4.0])), code, 2, ctypes.byref(h)) == 0
         buf = ctypes.create_string_buffer(64)
         p = ctypes.cast(buf, ctypes.c_void_p)
-        for pc in (_lib.MGR_I8, _lib.MGR_U16, 0, 12):
+        for pc in (0, 13, -1):
             assert lib.mgr_bin_count(h, p, pc, 4, 1, 1, p, 64, p, None) == -1
             assert b"positions must be" in lib.mgr_last_error()
-        assert lib.mgr_bin_count(h, p, _lib.MGR_F16, 0, 1, 1, p, 64, p, None) == 0   # n = 0
+        for pc in range(1, 13):   # n = 0: validated, nothing launched
+            assert lib.mgr_bin_count(h, p, pc, 0, 1, 1, p, 64, p, None) == 0
         assert lib.mgr_plan_destroy(h) == 0
-    assert lib.mgr_plan_create(1, vp(topo), vp(np.array([4.0])), 12, 2, ctypes.byref(h)) < 0
+    assert lib.mgr_plan_create(1, vp(topo), vp(np.array([4.0])), 13, 2, ctypes.byref(h)) < 0
     assert lib.mgr_plan_create(1, vp(topo), vp(np.array([2.5])), _lib.MGR_I64, 2,
                                ctypes.byref(h)) < 0
     assert b"integer box_length" in lib.mgr_last_error()
@@ -184,7 +186,7 @@ def test_box_dtype_codes():
     from mpi_grid_redistribute_amd._arrays import box_dtype_code, pos_code
     exp = {np.float16: _lib.MGR_F16, np.float32: _lib.MGR_F32, np.float64: _lib.MGR_F64,
            np.int8: _lib.MGR_I8, np.int16: _lib.MGR_I16, np.int32: _lib.MGR_I32,
-           np.int64: _lib.MGR_I64, np.uint8: _lib.MGR_U8, np.bool_: _lib.MGR_U8,
+           np.int64: _lib.MGR_I64, np.uint8: _lib.MGR_U8, np.bool_: _lib.MGR_B8,
            np.uint16: _lib.MGR_U16, np.uint32: _lib.MGR_U32, np.uint64: _lib.MGR_U64}
     for dt, code in exp.items():
         assert box_dtype_code(np.ones(3, dt)) == code, dt
@@ -193,8 +195,11 @@ def test_box_dtype_codes():
         box_dtype_code(np.ones(2, np.complex128))
     with pytest.raises(NotImplementedError):
         box_dtype_code(np.array([2 ** 60]))
-    for dt in (np.float16, np.float32, np.float64, np.int32, np.int64):
+    for dt in (np.float16, np.float32, np.float64, np.int8, np.int16, np.int32, np.int64,
+               np.uint8, np.uint16, np.uint32, np.uint64, np.bool_):
         assert _lib.POS_ITEMSIZE[pos_code(dt)] == np.dtype(dt).itemsize
-    for dt in (np.int16, np.uint32, np.bool_):
+    for dt in (np.longdouble, np.complex64, np.complex128, object):
         with pytest.raises(TypeError):
             pos_code(dt)
+    with pytest.raises(TypeError):
+        box_dtype_code(np.ones(2, np.longdouble))

@@ -96,25 +96,37 @@ def test_bin_random_vs_c_oracle(dt, boxdt):
                                       (np.int32, np.int16), (np.float16, np.float64),
                                       (np.float16, np.float32), (np.float16, np.float16),
                                       (np.float16, np.int8), (np.float16, np.int64),
-                                      (np.float32, np.int16), (np.float32, np.float16)])
+                                      (np.float32, np.int16), (np.float32, np.float16),
+                                      (np.int8, np.int8), (np.int8, np.float16),
+                                      (np.int16, np.float32), (np.uint8, np.uint8),
+                                      (np.uint16, np.int64), (np.uint32, np.float64),
+                                      (np.uint32, np.uint32), (np.uint64, np.int64),
+                                      (np.uint64, np.uint64), (np.bool_, np.float64),
+                                      (np.bool_, np.bool_)])
 def test_bin_position_dtypes_vs_c_oracle(dt, boxdt):
-    """int32 / int64 / float16 positions (and float32 against narrow boxes)
-    over 300k rows, every numpy promotion of :68-69 -- against the C
-    restatement (pinned by bin_dtypes.npz), through the GPU API and the
+    """Positions of every integer width, float16 and bool (and float32 against
+    narrow boxes) over 300k rows, the numpy promotions of :68-69 -- against
+    the C restatement (pinned by bin_dtypes.npz), through the GPU API and the
     redistribution's own binning kernel (mgr_bin_count)."""
     rng = np.random.default_rng(sum(map(ord, np.dtype(dt).str + np.dtype(boxdt).str)))
     topo = [3, 5, 2]
-    box = np.array([14, 6, 100]).astype(boxdt) if np.dtype(boxdt).kind in "iu" else \
-        np.array([0.7, 6.5, 3.0]).astype(boxdt)
+    kb = np.dtype(boxdt).kind
+    box = (np.array([True, True, True]) if kb == "b" else
+           np.array([14, 6, 100]).astype(boxdt) if kb in "iu" else
+           np.array([0.7, 6.5, 3.0]).astype(boxdt))
     n = 300_000
     b64 = box.astype(np.float64)
     raw = rng.uniform(-3, 4, (n, 3)) * b64
     raw[::13] = rng.uniform(0, 1, (len(raw[::13]), 3)) * b64
-    if np.dtype(dt).kind == "i":
-        raw = np.floor(raw * (8 if b64.min() < 10 else 1))
-        raw[::101] = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, (len(raw[::101]), 3))
+    if np.dtype(dt).kind in "iu":
+        info = np.iinfo(dt)
+        raw = np.clip(np.floor(raw * (8 if b64.min() < 10 else 1)), info.min, info.max)
+        if info.bits < 64:
+            raw[::101] = rng.integers(info.min, info.max, (len(raw[::101]), 3))
     with np.errstate(all="ignore"):
         pos = raw.astype(dt)
+        if np.dtype(dt) == np.uint64:
+            pos[::97] = rng.integers(0, 2 ** 63, (len(pos[::97]), 3), dtype=np.uint64) * 2 + 1
     exp = pos.copy()
     cell_exp, idx_exp = c_oracle.bin_positions(exp, topo, box, want_idx=True)
     R = MPIGridRedistributor(SizedComm(30), topo, box)
