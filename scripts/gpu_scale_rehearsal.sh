@@ -14,5 +14,14 @@ for N in 2 4; do
       --config $cfg --particles 8000000 > gpurun_out/scale/n${N}_cfg${cfg}.log 2>&1
     rc=$?; echo "n=$N cfg=$cfg rc=$rc" >> gpurun_out/scale/summary.txt
     if [ $rc -ne 0 ]; then exit $rc; fi
+    # the self-checking keys of the line (rccl: version/nranks/transport; exchange_ab: both timings)
+    python - gpurun_out/scale/n${N}_cfg${cfg}.log >> gpurun_out/scale/summary.txt <<'PYEOF' || exit 1
+import json, sys
+line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
+rec = json.loads(line)
+print("  ms_per_step", rec["ms_per_step"], "value", rec["value"])
+print("  rccl", json.dumps(rec["rccl"]))
+print("  exchange_ab", json.dumps(rec["exchange_ab"]))
+PYEOF
   done
 done
