@@ -86,6 +86,37 @@ def count_skew(matrix):
             "entry_max_over_mean": float(c.max()) / emean if emean > 0 else None}
 
 
+def host_read_start(tensors):
+    """Start one device->host read of several small int64 tensors: enqueued
+    now on the current stream (into pinned memory, behind the work already
+    launched and ahead of what is launched next); host_read_wait waits for
+    this read alone, so kernels launched in between keep the GPU busy while
+    the host works on the result."""
+    flat = (torch.cat([t.reshape(-1) for t in tensors]) if len(tensors) > 1
+            else tensors[0].reshape(-1))
+    sizes = [t.numel() for t in tensors]
+    if flat.device.type != "cuda":
+        return flat.numpy(), None, sizes
+    host = torch.empty(flat.numel(), dtype=flat.dtype, pin_memory=True)
+    host.copy_(flat, non_blocking=True)
+    done = torch.cuda.Event()
+    done.record()
+    return host, done, sizes
+
+
+def host_read_wait(read):
+    """The arrays of a host_read_start, once its copy is done."""
+    host, done, sizes = read
+    if done is not None:
+        done.synchronize()
+        host = host.numpy()
+    out, o = [], 0
+    for k in sizes:
+        out.append(host[o:o + k].copy())
+        o += k
+    return out
+
+
 def plan_layout(send_counts, recv_counts, rank, redirect_self):
     """Send/receive offsets in rows.  Receives in source-rank order (S7).
     With ``redirect_self`` the self segment never enters the send buffer

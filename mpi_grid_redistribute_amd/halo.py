@@ -57,7 +57,7 @@ import torch
 
 from . import _lib
 from .comm import excl_cumsum
-from .exchange import check_counts
+from .exchange import check_counts, host_read_start, host_read_wait
 
 
 def _p2p(transport, ops):
@@ -125,11 +125,15 @@ def _self_halo(transport, sel, srcs, rbs, flags, n, dim, carry_pos, arena, dev, 
     h, cnt = sel.msel_masks(flags, n, pieces, "_self")
     F = len(rbs)
     placed = arena is not None and arena[3] > 0
+    # the one host read is enqueued BEFORE the placed pack and waited for on
+    # its own event: the host finishes this call (and launches the caller's
+    # next work) while the pack runs, instead of idling the GPU after it
+    read = sel.to_host_start([cnt] + list(pending))
     if placed:   # into the arena before the sizes are known: no gap at the sync
         ast = [arena[0]] + ([arena[1]] if carry_pos else [])
         sel.msel_pack_placed(h, srcs, rbs, [ast[f][arena[2] * rbs[f]:] for f in range(F)],
                              arena[3])
-    got = sel.to_host([cnt] + list(pending))              # the one host sync
+    got = sel.to_host_wait(read)                          # the one host sync
     counts = got[0]
     for c in got[1:]:   # the redistribution's deferred count check
         check_counts(c, [])
@@ -281,13 +285,15 @@ class DeviceSelect:
 
     def to_host(self, tensors):
         """One device->host read of several small int64 tensors (one sync)."""
-        flat = torch.cat([t.reshape(-1) for t in tensors]) if len(tensors) > 1 else tensors[0]
-        host = flat.cpu().numpy()
-        out, o = [], 0
-        for t in tensors:
-            out.append(host[o:o + t.numel()].copy())
-            o += t.numel()
-        return out
+        return self.to_host_wait(self.to_host_start(tensors))
+
+    @staticmethod
+    def to_host_start(tensors):
+        return host_read_start(tensors)
+
+    @staticmethod
+    def to_host_wait(read):
+        return host_read_wait(read)
 
 
 def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n,

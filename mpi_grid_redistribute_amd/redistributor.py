@@ -39,7 +39,7 @@ import torch
 from . import _lib
 from ._arrays import Positions, Rows, box_dtype_code, device, id_array, pos_code
 from .comm import SelfComm, as_transport
-from .exchange import check_counts, exchange, exchange_pipelined
+from .exchange import check_counts, exchange, exchange_pipelined, host_read_start, host_read_wait
 from .halo import DeviceSelect, exchange_overload, halo_capacity, thresholds
 
 
@@ -708,13 +708,22 @@ class MPIGridRedistributor:
                                            scratch=self._scratch.get)
             self._last_layout = lay
             return outs, lay.total_recv
-        known = None
-        if deferred is not None and P == 1 and not drop:
+        known, read = None, None
+        if P == 1 and not drop:
+            # one rank keeping every row: the output size is n, so the pack is
+            # launched without reading the counts first; they are checked (a
+            # failed scan) by the caller's next host read, or here by a read
+            # enqueued ahead of the pack and waited for while it runs
             known = n
-            deferred.append(bin_counts)
+            if deferred is not None:
+                deferred.append(bin_counts)
+            else:
+                read = host_read_start([bin_counts])
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
                              self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
                              pack_all=pack_all if side_ids else None, known_rows=known)
+        if read is not None:
+            check_counts(host_read_wait(read)[0], [])
         self._last_layout = lay
         return outs, lay.total_recv
 

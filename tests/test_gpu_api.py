@@ -212,6 +212,32 @@ def test_single_rank_scan_failure_raises():
         _lib.test_hook("scan_spins", 1 << 24)
 
 
+def test_single_rank_position_scan_failure_raises():
+    """One rank keeping every row: the pack is launched without a count read
+    (the output holds n rows); the counts, read behind the pack, still raise.
+    One bin has no bin-end words to poll, so the give-up (scan_spins = -1)
+    needs several chunks (scan_chunk = 256 tiles) and a look-back or done
+    count not yet published: a run either raises or is exact, and some run
+    of a few raises."""
+    pos, rec = mgr.synth_uniform(1 << 22, seed=7)
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    raised = 0
+    with _Hooks(scan_spins=-1, scan_chunk=256):
+        for _ in range(20):
+            try:
+                out = R.redistribute_by_position(rec, pos.clone())
+            except _lib.MgrError as e:
+                assert "scan failed" in str(e)
+                raised += 1
+                if raised >= 2:
+                    break
+            else:
+                assert torch.equal(out, rec)
+    assert raised >= 1
+    out = R.redistribute_by_position(rec, pos.clone())
+    assert torch.equal(out, rec)
+
+
 def test_halo_scan_failure_raises():
     """The halo's selection scans (mgr_msel_count + mgr_scan) failing: the -1
     counts are checked at the halo's first host sync and raise, instead of

@@ -96,6 +96,13 @@ class CpuSelect:
     def to_host(self, tensors):
         return [t.numpy().copy() for t in tensors]
 
+    def to_host_start(self, tensors):
+        return self.to_host(tensors)
+
+    @staticmethod
+    def to_host_wait(read):
+        return read
+
 
 def _flat(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy())
