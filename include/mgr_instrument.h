@@ -32,6 +32,12 @@ extern "C" {
  * snapshot of every hook (the library's launches read one snapshot each);
  * < 0 for an unknown key or an out-of-range value.                         */
 int mgr_test_hook(const char* key, int64_t value);
+/* The element types a plan computes in for positions of pos_dtype and a box
+ * of box_dtype (mgr_dtype codes): *wrap = numpy's type of position % box,
+ * *quot = of position / box (the bin's division), from the library's own
+ * promotion table.  Host only, no GPU: tests/test_capi.py checks every pair
+ * against numpy.  MGR_EINVAL for an unknown code.                          */
+int mgr_test_pos_modes(int pos_dtype, int box_dtype, int* wrap, int* quot);
 
 /* ----------------------------------------------------------- profiling --
  * Per-kernel HIP-event timing of every launch made while enabled, on the

@@ -83,6 +83,7 @@ SIGNATURES = {
 # include/mgr_instrument.h: measurement and test hooks (not the boundary).
 INSTRUMENT_SIGNATURES = {
     "mgr_test_hook": (_I, [ctypes.c_char_p, _I64]),
+    "mgr_test_pos_modes": (_I, [_I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "mgr_profile_enable": (_I, [_I]),
     "mgr_profile_reset": (_I, []),
     "mgr_profile_select": (_I, [_I64]),

@@ -194,6 +194,18 @@ static void pos_modes(mgr::Geom& g, int pos_dtype) {
     g.compute_f32 = pos_dtype == MGR_F32 && g.wmode == MGR_F32;
 }
 
+int mgr_test_pos_modes(int pos_dtype, int box_dtype, int* wrap, int* quot) {
+    Kind k;
+    if (!dtype_kind(pos_dtype, &k) || !dtype_kind(box_dtype, &k) || !wrap || !quot)
+        return fail(MGR_EINVAL, "pos_dtype %d, box_dtype %d", pos_dtype, box_dtype);
+    mgr::Geom g{};
+    g.box_dtype = box_dtype;
+    pos_modes(g, pos_dtype);
+    *wrap = g.wmode;
+    *quot = g.dmode;
+    return MGR_OK;
+}
+
 // Box geometry of a plan: L, 2L, fast-wrap and exact power-of-two division
 // flags per dimension, integer lengths of an integer box, and the
 // per-dimension cell counts n[d].

@@ -203,3 +203,26 @@ def test_box_dtype_codes():
             pos_code(dt)
     with pytest.raises(TypeError):
         box_dtype_code(np.ones(2, np.longdouble))
+
+
+def test_promotion_table_matches_numpy(lib):
+    """Every (position, box) dtype pair: the library's wrap type (numpy's
+    position % box) and quotient type (position / box) equal numpy 2.2's own
+    -- the promotion the reference's redist.py:68-69 arithmetic gets, with
+    the box a strongly typed numpy scalar (S11).  Host only."""
+    import ctypes
+    import numpy as np
+    from mpi_grid_redistribute_amd._arrays import pos_code
+    dts = [np.float16, np.float32, np.float64, np.int8, np.int16, np.int32, np.int64,
+           np.uint8, np.uint16, np.uint32, np.uint64, np.bool_]
+    w, q = ctypes.c_int(), ctypes.c_int()
+    for p in dts:
+        for b in dts:
+            zp, zb = np.zeros(1, p), np.ones(1, b)
+            with np.errstate(all="ignore"):
+                ew, eq = (zp % zb[0]).dtype, (zp / zb[0]).dtype
+            assert lib.mgr_test_pos_modes(pos_code(p), pos_code(b), ctypes.byref(w),
+                                          ctypes.byref(q)) == 0
+            assert (w.value, q.value) == (pos_code(ew), pos_code(eq)), (p, b, ew, eq)
+    assert lib.mgr_test_pos_modes(0, 2, ctypes.byref(w), ctypes.byref(q)) != 0
+    assert lib.mgr_test_pos_modes(2, 13, ctypes.byref(w), ctypes.byref(q)) != 0
