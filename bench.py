@@ -485,13 +485,17 @@ def main():
         dist.all_gather_object(every, mine)
         rccl = rccl_block(comm.rccl_info(), sorted({x for e in every for x in e}), world)
     # per-kernel algorithmic bytes per launch: per-row figure x the rows one
-    # launch processes (n: every launch of these kernels covers this rank's
-    # rows -- received rows at N > 1 are ~n for the uniform inputs), or the
-    # host-counted bytes of the halo's selections
+    # launch processes -- a step's launches of these kernels together cover
+    # this rank's n rows (received rows at N > 1 are ~n for the uniform
+    # inputs), so a pack pipelined in k chunks covers n / k per launch -- or
+    # the host-counted bytes of the halo's selections
     fine_tr = int(_lib.load().mgr_ranked_tile_rows(36, 512)) if cfg == 5 else 2048
     for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world).items():
         if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
-            kernels[k]["alg_bytes_per_launch"] = b * n
+            e = kernels[k]
+            per_step = e["launches"] / e["steps"] if e.get("steps") else 1
+            e["launches_per_step"] = per_step
+            e["alg_bytes_per_launch"] = b * n / max(per_step, 1)
     for k, e in kernels.items():
         if "alg_bytes_per_launch" in e:
             e["alg_GBps"] = e["alg_bytes_per_launch"] / (e["avg_ms"] / 1e3) / 1e9
