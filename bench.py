@@ -111,8 +111,10 @@ RCCL_LOG_PREFIX = "/tmp/mgr_bench_rccl"
 def rccl_log_env(environ):
     """N > 1: RCCL's connection lines ("Channel 00/0 : 0[0] -> 1[1] via
     P2P/IPC") to a per-process file, so the record can name the transport
-    RCCL chose (init-time logging only; the caller's own NCCL_DEBUG wins)."""
-    if "NCCL_DEBUG" in environ:
+    RCCL chose (init-time logging only).  A caller already logging at INFO or
+    TRACE keeps its own destination (transports then unread); a lower level
+    (VERSION, WARN -- some images preset one) is raised to INFO into the file."""
+    if environ.get("NCCL_DEBUG", "").strip().upper() in ("INFO", "TRACE"):
         return None
     path = f"{RCCL_LOG_PREFIX}.{os.getpid()}.log"
     environ["NCCL_DEBUG"] = "INFO"
@@ -478,7 +480,8 @@ def main():
             try:
                 with open(rccl_log) as f:
                     mine = rccl_transports(f.read())
-                os.remove(rccl_log)
+                if mine:      # an unparsed log stays in /tmp for a look
+                    os.remove(rccl_log)
             except OSError:
                 mine = []
         every = [None] * world

@@ -5,6 +5,7 @@
 # xGMI numbers; the point is that every N>1 code path runs to its JSON line.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/scale
 export MGR_BENCH_SHARED_GPU=1
+env | grep '^NCCL_' > gpurun_out/scale/nccl_env.txt || true
 P=29600
 for N in 2 4; do
   for cfg in 3 4 5; do
@@ -25,3 +26,4 @@ print("  exchange_ab", json.dumps(rec["exchange_ab"]))
 PYEOF
   done
 done
+ls -la /tmp/mgr_bench_rccl.* > gpurun_out/scale/left_rccl_logs.txt 2>&1 || true

@@ -454,7 +454,9 @@ def test_bench_scaling_record_schema():
     env = {}
     path = bench.rccl_log_env(env)
     assert env["NCCL_DEBUG"] == "INFO" and env["NCCL_DEBUG_FILE"] == path
-    assert bench.rccl_log_env({"NCCL_DEBUG": "WARN"}) is None      # the caller's setting wins
+    assert bench.rccl_log_env({"NCCL_DEBUG": "INFO"}) is None      # the caller's INFO wins
+    low = {"NCCL_DEBUG": "VERSION"}                                  # a preset low level: raised
+    assert bench.rccl_log_env(low) == low["NCCL_DEBUG_FILE"] and low["NCCL_DEBUG"] == "INFO"
     log = ("host:1:2 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC/read\n"
            "host:1:2 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC\n"
            "host:1:2 [0] NCCL INFO Channel 00/1 : 1[0] -> 0[0] [send] via NET/Socket/0\n"
