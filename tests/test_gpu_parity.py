@@ -14,6 +14,7 @@ import torch
 from oracle import c_oracle
 from oracle import redist_oracle as ro
 from tests import golden_io as G
+from tests.dtype_cases import ALL_DTYPES, dtype_case
 from tests.fake_mpi import run_ranks
 
 pytestmark = pytest.mark.gpu
@@ -91,6 +92,36 @@ def test_bin_random_vs_c_oracle(dt, boxdt):
     assert np.array_equal(idx.cpu().numpy(), idx_exp)
 
 
+@pytest.mark.parametrize("boxdt", ALL_DTYPES, ids=lambda d: np.dtype(d).name)
+def test_bin_every_dtype_pair_vs_c_oracle(boxdt):
+    """All 12 x 12 (position, box) dtype pairs, 20k rows each: wrapped
+    positions, cell indexes and cell numbers equal the C restatement (whose
+    modes are numpy's own, and whose promotion the library shares:
+    test_capi.py::test_promotion_table_matches_numpy)."""
+    for dt in ALL_DTYPES:
+        topo, box, pos = dtype_case(dt, boxdt, 20_000)
+        exp = pos.copy()
+        cell_exp, idx_exp = c_oracle.bin_positions(exp, topo, box, want_idx=True)
+        R = MPIGridRedistributor(SizedComm(30), topo, box)
+        got = torch.from_numpy(pos.copy()).cuda()
+        idx = R.get_cell_indexes_from_position(got.clone())
+        cell = R.get_cell_number_from_position(got)
+        name = (np.dtype(dt).name, np.dtype(boxdt).name)
+        assert G.same_bytes(got.cpu().numpy(), exp), (name, G.diff_report(got.cpu().numpy(), exp))
+        assert np.array_equal(cell.cpu().numpy(), cell_exp), name
+        assert np.array_equal(idx.cpu().numpy(), idx_exp), name
+        cell_np = c_oracle.bin_positions(pos.copy(), topo, box, periodic=False)
+        cell_n = R.get_cell_number_from_position(torch.from_numpy(pos.copy()).cuda(),
+                                                 periodic=False)
+        assert np.array_equal(cell_n.cpu().numpy(), cell_np), name + ("nonperiodic",)
+        # the hot path's binning kernel (mgr_bin_count) on the same rows
+        gp = torch.from_numpy(pos.copy()).cuda()
+        out, _ = GridPartitioner(topo, box).partition_by_position(
+            torch.arange(len(pos), dtype=torch.int64, device="cuda"), gp)
+        assert G.same_bytes(gp.cpu().numpy(), exp), name
+        assert np.array_equal(out.cpu().numpy(), np.argsort(cell_exp, kind="stable")), name
+
+
 @pytest.mark.parametrize("dt,boxdt", [(np.int32, np.int64), (np.int64, np.int64),
                                       (np.int32, np.float64), (np.int64, np.float32),
                                       (np.int32, np.int16), (np.float16, np.float64),
@@ -108,25 +139,8 @@ def test_bin_position_dtypes_vs_c_oracle(dt, boxdt):
     narrow boxes) over 300k rows, the numpy promotions of :68-69 -- against
     the C restatement (pinned by bin_dtypes.npz), through the GPU API and the
     redistribution's own binning kernel (mgr_bin_count)."""
-    rng = np.random.default_rng(sum(map(ord, np.dtype(dt).str + np.dtype(boxdt).str)))
-    topo = [3, 5, 2]
-    kb = np.dtype(boxdt).kind
-    box = (np.array([True, True, True]) if kb == "b" else
-           np.array([14, 6, 100]).astype(boxdt) if kb in "iu" else
-           np.array([0.7, 6.5, 3.0]).astype(boxdt))
     n = 300_000
-    b64 = box.astype(np.float64)
-    raw = rng.uniform(-3, 4, (n, 3)) * b64
-    raw[::13] = rng.uniform(0, 1, (len(raw[::13]), 3)) * b64
-    if np.dtype(dt).kind in "iu":
-        info = np.iinfo(dt)
-        raw = np.clip(np.floor(raw * (8 if b64.min() < 10 else 1)), info.min, info.max)
-        if info.bits < 64:
-            raw[::101] = rng.integers(info.min, info.max, (len(raw[::101]), 3))
-    with np.errstate(all="ignore"):
-        pos = raw.astype(dt)
-        if np.dtype(dt) == np.uint64:
-            pos[::97] = rng.integers(0, 2 ** 63, (len(pos[::97]), 3), dtype=np.uint64) * 2 + 1
+    topo, box, pos = dtype_case(dt, boxdt, n)
     exp = pos.copy()
     cell_exp, idx_exp = c_oracle.bin_positions(exp, topo, box, want_idx=True)
     R = MPIGridRedistributor(SizedComm(30), topo, box)

@@ -207,3 +207,24 @@ def test_local_partition_omp_matches_serial(threads, topo):
     assert p1.tobytes() == p2.tobytes()
     assert np.array_equal(off, exp_off)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("boxdt", __import__("tests.dtype_cases", fromlist=["x"]).ALL_DTYPES,
+                         ids=lambda d: np.dtype(d).name)
+def test_c_oracle_every_dtype_pair_matches_numpy(boxdt):
+    """All 12 x 12 (position, box) dtype pairs, 5k rows each: the C
+    restatement (the GPU tests' large-N checker) equals the NumPy one, which
+    runs the reference's own numpy expressions (redist.py:63-90, :328-329) --
+    beyond the pairs the reference-run fixtures hold."""
+    from tests.dtype_cases import ALL_DTYPES, dtype_case
+    for dt in ALL_DTYPES:
+        topo, box, pos = dtype_case(dt, boxdt, 5000)
+        geo = ro.Geometry(topo, box, 30)
+        for periodic in (True, False):
+            p_np, p_c = pos.copy(), pos.copy()
+            with np.errstate(all="ignore"):
+                cell_np = ro.cell_number_from_position(geo, p_np, periodic)
+            cell_c = c_oracle.bin_positions(p_c, topo, box, periodic=periodic)
+            name = (np.dtype(dt).name, np.dtype(boxdt).name, periodic)
+            assert G.same_bytes(p_c, p_np), name
+            assert np.array_equal(cell_c, cell_np), name
