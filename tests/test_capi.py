@@ -120,6 +120,16 @@ def test_product_refuses_without_gpu():
         m.GridPartitioner([2], [1.0])
 
 
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No libmgr.so: the package raises at its first native call, naming the
+    build step -- nothing falls back to a host path."""
+    from mpi_grid_redistribute_amd import _lib
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "libmgr.so"))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.load()
+
+
 def test_msel_validation(lib):
     """mgr_msel_count / mgr_msel_pack argument checks run on the host before
     any launch."""
