@@ -97,7 +97,8 @@ class Rows:
 
 
 class Positions:
-    """(N, >=dim) float32/float64 positions as (device pointer, row stride).
+    """(N, >=dim) positions of any float, integer or bool dtype (redist.py
+    bins any numeric column) as (device pointer, row stride, mgr_dtype code).
 
     ``finish()`` must run right after the binning kernel: it makes the
     caller's array hold the wrapped values (S1) before anything reads it."""
