@@ -174,14 +174,15 @@ def cpu_baseline():
     wrap + bin, one mask pass per destination, pickled all-to-all,
     concatenate) run as 8 spawned rank processes on a 2x2x2 grid -- the
     `mpirun -n 8` shape of BASELINE config 1 (mpi4py/mpirun are absent on the
-    box; pipes carry the pickled all-to-all).  Bounded sample: 8 x 2M
-    particles, best of 3 iterations (slowest rank each)."""
+    box; pipes carry the pickled all-to-all).  Bounded sample: 8 x 4M
+    particles, best of 3 iterations (slowest rank each) -- ~20 s of CPU work
+    over the 8 cores."""
     from oracle import mp_baseline
 
     avail = len(os.sched_getaffinity(0))
     ranks = 8 if avail >= 8 else max(1, avail)
     topo = {8: (2, 2, 2), 4: (2, 2, 1), 2: (2, 1, 1)}.get(ranks, (1, 1, 1))
-    n = 1 << 21
+    n = 1 << 22
     t0 = time.perf_counter()
     r = mp_baseline.run(size=int(np.prod(topo)), n_per_rank=n, iters=3, topo=topo)
     el = time.perf_counter() - t0
