@@ -262,7 +262,8 @@ int mgr_bin_starts(int64_t n, int nbins, int tile_rows, const void* workspace,
  * with position[:, d] > rank_cell_limits[d,1] - overload_lengths[d] (:271,
  * :274) and left with position[:, d] < rank_cell_limits[d,0] +
  * overload_lengths[d] (:272, :275), compared in float64 (numpy promotion of
- * the float32/float64 column against a float64 scalar; NaN selects none).
+ * the column, of any mgr_dtype, against a float64 scalar: integers above
+ * 2^53 round to float64 as numpy converts them; NaN selects none).
  *
  * mgr_halo_flags  : one pass over n position rows; flags[r] (uint16) bit 2d =
  *                   coordinate d > hi[d], bit 2d+1 = coordinate d < lo[d].

@@ -301,7 +301,7 @@ def exchange_overload(R, transport, data_flat, rbd, pos_flat, ncols, pos_code, n
                       pending=()):
     """Overload rows of rank R (redist.py:202-309).  ``data_flat``: flat uint8
     tensor of this rank's n payload rows of ``rbd`` bytes; ``pos_flat``: their
-    positions (n, ncols) float32/float64 rows (ncols >= dim), or None when the
+    positions (n, ncols) rows of any position dtype (ncols >= dim), or None when the
     positions are not wanted back and ``flags`` is given.  ``flags``: the
     rows' face flags (int16 [n]) when the binning computed them, else one pass
     computes them from the positions here.  The overload buffer only grows at

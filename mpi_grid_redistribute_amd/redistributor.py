@@ -809,7 +809,7 @@ class GridPartitioner:
                          fine_cells=None):
         """Hot-path call on device buffers (no host sync).  ``data_flat``:
         uint8 device tensor of n*row_bytes; ``pos_tensor``: (n, >=dim)
-        float32/float64 device tensor with unit column stride (wrapped in
+        device tensor of any position dtype, unit column stride (wrapped in
         place).  Returns (out_flat, bin_counts) device tensors; with
         ``fine_cells`` (config 5's source side) also every row's fine cell
         inside its destination cell, partitioned like the rows (uint16 ids
