@@ -800,8 +800,8 @@ static hipError_t pack_t(const void* src, int64_t row_bytes, int64_t n, const vo
 template <int W, int UPR>
 static hipError_t pack_coop_u(const void* src, int64_t n, const void* dest, int nb, int drop_bin,
                               int tile_rows, const Workspace& ws, void* dst, int redirect_bin,
-                              void* redirect_dst, hipStream_t s, SideField* side) {
-    if (hooks().pack_generic || tile_rows > 2048) return hipErrorNotSupported;
+                              void* redirect_dst, hipStream_t s, SideField* side, const Hooks& h) {
+    if (h.pack_generic || tile_rows > 2048) return hipErrorNotSupported;
     // one wave per RPW 64-row rounds of the tile (<= 16 waves)
     const int rpw = tile_rows > 1024 ? 2 : 1;
     const int threads = tile_rows / rpw;
@@ -828,8 +828,8 @@ template <int W>
 static hipError_t pack_coop_t(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                                int nb, int drop_bin, int tile_rows, const Workspace& ws,
                                void* dst, int redirect_bin, void* redirect_dst, hipStream_t s,
-                               SideField* side) {
-#define MGR_PS(U_) case U_: return pack_coop_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
+                               SideField* side, const Hooks& h) {
+#define MGR_PS(U_) case U_: return pack_coop_u<W, U_>(src, n, dest, nb, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side, h);
     if constexpr (W >= 4) {
         switch ((int)(row_bytes / W)) {
             MGR_PS(1) MGR_PS(2) MGR_PS(3) MGR_PS(4)
@@ -1116,13 +1116,14 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
 // the outputs 4-byte aligned, <= 64 bins and <= 16 waves per tile.
 static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const void* dest,
                            int nb, int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                           int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side) {
+                           int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side,
+                           const Hooks& h) {
     uintptr_t a = (uintptr_t)dst | (uintptr_t)row_bytes;
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
     // pack_img 1: rows of >= 24 bytes (A/B: 36 B 0.90 vs 1.05 ms, 40 B 0.97 vs
     // 1.00, 24 B 0.70 vs 0.71; 12 B 0.56 vs 0.48 -- the LDS passes cost more
     // than narrow units for small rows); 2: every size it takes (tests)
-    const int64_t min_rb = hooks().pack_img_all ? 12 : 24;
+    const int64_t min_rb = h.pack_img_all ? 12 : 24;
     if (((uintptr_t)src & 15) || (a & 3) || row_bytes % 16 == 0 ||
         row_bytes < min_rb || row_bytes > 60 || nb > 64 || tile_rows > 1024 ||
         dest_bytes(nb) != 1)
@@ -1140,7 +1141,8 @@ static hipError_t pack_img(const void* src, int64_t row_bytes, int64_t n, const 
 template <int W>
 static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const void* dest, int nb,
                          int drop_bin, int tile_rows, const Workspace& ws, void* dst,
-                         int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side) {
+                         int redirect_bin, void* redirect_dst, hipStream_t s, SideField* side,
+                         const Hooks& h) {
     if constexpr (W >= 4) {
         if (nb > 64 && nb <= 1024 && row_bytes <= 64 && tile_rows == many_round_rows(nb)) {
             const hipError_t e = dest_bytes(nb) == 1
@@ -1152,13 +1154,13 @@ static hipError_t pack_w(const void* src, int64_t row_bytes, int64_t n, const vo
     if constexpr (W == 2) {   // 2-byte rows (the fine cells travelling with config-5 rows)
         if (nb <= 64 && row_bytes == 2) {
             const hipError_t e = pack_coop_u<2, 1>(src, n, dest, nb, drop_bin, tile_rows, ws, dst,
-                                                   redirect_bin, redirect_dst, s, nullptr);
+                                                   redirect_bin, redirect_dst, s, nullptr, h);
             if (e != hipErrorNotSupported) return e;
         }
     }
     if (nb <= 64 && row_bytes <= 64 && W >= 4) {
         const hipError_t e = pack_coop_t<W>(src, row_bytes, n, dest, nb, drop_bin, tile_rows,
-                                             ws, dst, redirect_bin, redirect_dst, s, side);
+                                             ws, dst, redirect_bin, redirect_dst, s, side, h);
         if (e != hipErrorNotSupported) return e;
     }
     const bool wide = row_bytes > 256;
@@ -1198,18 +1200,19 @@ static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n
     if (redirect_dst) a |= (uintptr_t)redirect_dst;
     // profiler: narrow (< 4-byte) rows apart
     const int kid = row_bytes < 4 ? K_PACK_NARROW : K_PACK;
+    const Hooks& h = hooks();   // one snapshot for the whole launch
     prof_begin(s, kid);
     hipError_t e = pack_img(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
-                            redirect_bin, redirect_dst, s, side);
+                            redirect_bin, redirect_dst, s, side, h);
     if (e != hipErrorNotSupported) {
         prof_end(s, kid);
         return e;
     }
-    if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
-    else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
-    else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
-    else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
-    else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side);
+    if ((a & 15) == 0) e = pack_w<16>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side, h);
+    else if ((a & 7) == 0) e = pack_w<8>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side, h);
+    else if ((a & 3) == 0) e = pack_w<4>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side, h);
+    else if ((a & 1) == 0) e = pack_w<2>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side, h);
+    else e = pack_w<1>(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst, redirect_bin, redirect_dst, s, side, h);
     prof_end(s, kid);
     return e;
 }
