@@ -317,10 +317,17 @@ __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __re
         __shared__ int hist_s[kWaves][NC];
         int* hist = hist_s[w];
         for (int i = lane; i < NC; i += 64) hist[i] = 0;
+        // the next chunk's flags are in flight while this one is counted
+        uint32_t fn[kSelWords];
+        chunk_flags(flags, row0, min(kSelChunk, rows), lane, fn);
         wave_sync();
         for (int c0 = 0; c0 < rows; c0 += kSelChunk) {
             uint32_t fw[kSelWords];
-            chunk_flags(flags, row0 + c0, min(kSelChunk, rows - c0), lane, fw);
+#pragma unroll
+            for (int i = 0; i < kSelWords; ++i) fw[i] = fn[i];
+            if (c0 + kSelChunk < rows)
+                chunk_flags(flags, row0 + c0 + kSelChunk, min(kSelChunk, rows - c0 - kSelChunk),
+                            lane, fn);
 #pragma unroll
             for (int i = 0; i < kSelWords; ++i) {
                 const unsigned f0 = fw[i] & (NC - 1), f1 = (fw[i] >> 16) & (NC - 1);
@@ -335,11 +342,10 @@ __global__ __launch_bounds__(kBlock) void msel_count_kernel(const uint16_t* __re
                 if (!((c >> b) & 1)) hist[c] += hist[c | (1 << b)];
             wave_sync();
         }
-        if (lane == 0) {
-            for (int k = 0; k < nsets; ++k) {
-                const unsigned m = masks.m[k];
-                counts[(int64_t)k * T + tile] = m ? hist[m] : rows;
-            }
+        // one set per lane: the tile's counts go out as parallel stores
+        for (int k = lane; k < nsets; k += 64) {
+            const unsigned m = masks.m[k];
+            counts[(int64_t)k * T + tile] = m ? hist[m] : rows;
         }
     } else {
         int c[kMaxSets];
