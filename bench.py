@@ -168,7 +168,7 @@ def topology_for(n):
     return dims
 
 
-def cpu_baseline():
+def cpu_baseline(n_per_rank=1 << 22):
     """The reference algorithm on this host's cores (oracle/, the checker): the
     NumPy restatement of redistribute_by_position (redist.py:157-199: in-place
     wrap + bin, one mask pass per destination, pickled all-to-all,
@@ -182,7 +182,7 @@ def cpu_baseline():
     avail = len(os.sched_getaffinity(0))
     ranks = 8 if avail >= 8 else max(1, avail)
     topo = {8: (2, 2, 2), 4: (2, 2, 1), 2: (2, 1, 1)}.get(ranks, (1, 1, 1))
-    n = 1 << 22
+    n = int(n_per_rank)
     t0 = time.perf_counter()
     r = mp_baseline.run(size=int(np.prod(topo)), n_per_rank=n, iters=3, topo=topo)
     el = time.perf_counter() - t0

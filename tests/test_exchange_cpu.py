@@ -492,3 +492,13 @@ def test_rccl_runtime_version_is_the_loaded_library():
     assert ctypes.CDLL(path).ncclGetVersion(ctypes.byref(v)) == 0
     assert runtime == v.value
     assert runtime // 10000 == compiled // 10000 and runtime >= 21800
+
+
+def test_bench_cpu_baseline_record():
+    """bench.py's cpu_baseline object (the contract's keys), on a tiny sample:
+    the oracle's 8-process numpy restatement of redist.py:157-199."""
+    import bench
+    r = bench.cpu_baseline(n_per_rank=4096)
+    assert set(r) == {"value", "unit", "cores", "kind", "sample"}
+    assert r["value"] > 0 and r["unit"] == "particles/s" and r["kind"] == "port"
+    assert r["cores"] >= 1 and "4096 uniform particles" in r["sample"]
