@@ -136,7 +136,10 @@ def rccl_transports(text):
 def rccl_block(info, transports, world):
     """The scaling record's RCCL facts: versions (built against / loaded),
     the library path, ranks as RCCL counts them (must equal the world size)
-    and the transports its connections use (P2P/IPC = xGMI on one node)."""
+    and the transports its connections use (P2P/IPC = xGMI on one node).
+    A failed query is reported, not raised: the record still prints."""
+    if "error" in info:
+        return {"error": info["error"], "transports": transports}
     return {"version_compiled": info["version_compiled"],
             "version_runtime": info["version_runtime"], "library": info["library"],
             "nranks": info["nranks"], "nranks_ok": info["nranks"] == world,
@@ -485,9 +488,13 @@ def main():
                     os.remove(rccl_log)
             except OSError:
                 mine = []
+        try:      # local queries only: a failure must not skip the collective below
+            info = comm.rccl_info()
+        except Exception as e:   # noqa: BLE001 -- reported in the record
+            info = {"error": repr(e)}
         every = [None] * world
         dist.all_gather_object(every, mine)
-        rccl = rccl_block(comm.rccl_info(), sorted({x for e in every for x in e}), world)
+        rccl = rccl_block(info, sorted({x for e in every for x in e}), world)
     # per-kernel algorithmic bytes per launch: per-row figure x the rows one
     # launch processes -- a step's launches of these kernels together cover
     # this rank's n rows (received rows at N > 1 are ~n for the uniform

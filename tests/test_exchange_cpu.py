@@ -468,6 +468,8 @@ def test_bench_scaling_record_schema():
     assert set(r) == {"version_compiled", "version_runtime", "library", "nranks", "nranks_ok",
                       "transports"}
     assert r["nranks_ok"] and not bench.rccl_block(info, [], 4)["nranks_ok"]
+    assert bench.rccl_block({"error": "x"}, ["NET/Socket"], 2) == {"error": "x",
+                                                                   "transports": ["NET/Socket"]}
     ab = bench.exchange_ab_block(2.0, 4, 3.0, 10)
     assert set(ab) == {"pipelined_ms_per_step", "chunks", "one_message_ms_per_step",
                        "one_message_steps", "pipelined_speedup", "in_timed_region"}
