@@ -56,7 +56,6 @@ import numpy as np
 import torch
 
 from . import _lib
-from .comm import excl_cumsum
 from .exchange import check_counts, host_read_start, host_read_wait
 
 

@@ -4,7 +4,6 @@ import ctypes
 import json
 import os
 import subprocess
-import sys
 
 import torch
 
