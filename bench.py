@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: particles redistributed/sec (whole node), HBM / xGMI roofline.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--soa]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...,
+         or bare `python bench.py --gpus N`: with no WORLD_SIZE in the
+         environment the script starts its N rank processes itself (children,
+         127.0.0.1 rendezvous), relays rank 0's line and exits non-zero if a
+         rank fails or the run exceeds --launch-timeout.
 
 One step = one pass of the hot path over one batch of synthetic particles
 already resident in HBM (SURVEY §8d generator, generated on the device):
@@ -26,7 +30,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -49,7 +57,23 @@ N_CFG5_PER_GPU = 512_000_000 // 8    # config 5: 512M over 8 GPUs
 
 # Algorithmic bytes per row of one launch (DESIGN.md §4 Measurement): what
 # the kernel must read and write at least, per row it processes.
-def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1):
+def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1, soa=False):
+    if cfg == 5 and soa:
+        # four arrays: pos f32 x3 (also the binned positions), vel f32 x3,
+        # mass f32, id i64 -- 36 bytes a row in 12 + 12 + 4 + 8
+        ts = 2.0 * fine_bins / fine_tile_rows
+        return {
+            "bin_fine": 12 + 1 + 2,          # read the (n,3) f32 positions, dest, fine id
+            "pack": 1 + 36 + 2 + 36 + 2,     # dest, every field + fine id in, out
+            "count_ids": 2 + 2 + ts,         # mgr_rank_ids
+            # mgr_pack_ranked once per field: ids, ranks, starts + the field
+            "pack_fine": 4 * (2 + 2 + ts) + 36 + 36,
+        }
+    if soa:   # configs 2 / 4 as two arrays: pos f64 x3 (binned, wrapped) + id i64
+        return {
+            "bin_count": 24 + 24 + 1,
+            "pack": 1 + 24 + 8 + 24 + 8,
+        }
     if cfg == 5:
         ts = 2.0 * fine_bins / fine_tile_rows        # u16 tile starts per row
         return {
@@ -178,8 +202,8 @@ def cpu_baseline(n_per_rank=1 << 22):
     concatenate) run as 8 spawned rank processes on a 2x2x2 grid -- the
     `mpirun -n 8` shape of BASELINE config 1 (mpi4py/mpirun are absent on the
     box; pipes carry the pickled all-to-all).  Bounded sample: 8 x 4M
-    particles, best of 3 iterations (slowest rank each) -- ~20 s of CPU work
-    over the 8 cores."""
+    particles, the median of 5 iterations (slowest rank each) with the spread
+    -- ~20 s of CPU work over the 8 cores."""
     from oracle import mp_baseline
 
     avail = len(os.sched_getaffinity(0))
@@ -187,37 +211,41 @@ def cpu_baseline(n_per_rank=1 << 22):
     topo = {8: (2, 2, 2), 4: (2, 2, 1), 2: (2, 1, 1)}.get(ranks, (1, 1, 1))
     n = int(n_per_rank)
     t0 = time.perf_counter()
-    r = mp_baseline.run(size=int(np.prod(topo)), n_per_rank=n, iters=3, topo=topo)
+    r = mp_baseline.run(size=int(np.prod(topo)), n_per_rank=n, iters=5, topo=topo)
     el = time.perf_counter() - t0
     return {"value": r["value"], "unit": "particles/s", "cores": r["ranks"], "kind": "port",
+            "stat": "median", "spread": r["spread"],
             "sample": f"{r['ranks']} rank processes x {n} uniform particles, grid {list(topo)}, "
                       f"f64 (N,3) positions + 32-byte records, numpy {np.__version__} "
                       f"restatement of redist.py:157-199 with a pickled all-to-all over pipes "
-                      f"(mpirun/mpi4py absent), best of 3 iterations "
+                      f"(mpirun/mpi4py absent), median of 5 iterations "
                       f"{[round(x, 3) for x in r['seconds']]} s, {el:.1f} s wall"}
 
 
 def cpu_baseline_cfg1():
     """BASELINE config 1's own shape on the oracle: 8 rank processes x 125k
-    uniform particles (1M total) on a 2x2x2 grid, best of 5 iterations."""
+    uniform particles (1M total) on a 2x2x2 grid, median of 7 iterations."""
     from oracle import mp_baseline
 
     avail = len(os.sched_getaffinity(0))
     if avail < 8:
         return None
     n = 125_000
-    r = mp_baseline.run(size=8, n_per_rank=n, iters=5, topo=(2, 2, 2))
+    r = mp_baseline.run(size=8, n_per_rank=n, iters=7, topo=(2, 2, 2))
     return {"value": r["value"], "unit": "particles/s", "cores": r["ranks"], "kind": "port",
+            "stat": "median", "spread": r["spread"],
             "sample": f"BASELINE config 1: 8 rank processes x {n} uniform particles (1M), grid "
                       f"[2, 2, 2], numpy restatement of redist.py:157-199, pickled all-to-all "
-                      f"over pipes, best of 5 {[round(x, 4) for x in r['seconds']]} s"}
+                      f"over pipes, median of 7 {[round(x, 4) for x in r['seconds']]} s"}
 
 
-def cpu_baseline_c():
+def cpu_baseline_c(iters=7):
     """Optimised host comparison point (oracle/, the checker): the threaded C
     restatement of the local stage (wrap + bin + stable partition, exactly the
     GPU step's work at N=1) on this host's cores, 16M particles of the same
-    layout, best of 3."""
+    layout.  Output and scratch are allocated and touched by an untimed first
+    call; the timed calls allocate nothing.  The median of ``iters`` with the
+    spread (min..max rate): single iterations on a shared host vary."""
     from oracle import c_oracle
 
     # 8 threads: the same core count as the 8-rank port baselines
@@ -228,15 +256,22 @@ def cpu_baseline_c():
     rec[:, :3] = pos
     rec.view(np.int64)[:, 3] = ids
     out = np.empty_like(rec)
+    ws = c_oracle.local_partition_workspace(n, 8, threads)
+    c_oracle.local_partition_omp(pos, rec, [2, 2, 2], [1.0, 1.0, 1.0], threads=threads, out=out,
+                                 workspace=ws)   # untimed: first touch of out and scratch
     secs = []
-    for _ in range(3):
+    for _ in range(iters):
         t0 = time.perf_counter()
-        c_oracle.local_partition_omp(pos, rec, [2, 2, 2], [1.0, 1.0, 1.0], threads=threads, out=out)
+        c_oracle.local_partition_omp(pos, rec, [2, 2, 2], [1.0, 1.0, 1.0], threads=threads,
+                                     out=out, workspace=ws)
         secs.append(time.perf_counter() - t0)
-    return {"value": n / min(secs), "unit": "particles/s", "cores": threads, "kind": "port",
+    med = float(np.median(secs))
+    return {"value": n / med, "unit": "particles/s", "cores": threads, "kind": "port",
+            "stat": "median", "spread": [n / max(secs), n / min(secs)],
             "sample": f"{n} uniform particles, f64 (N,3) positions + 32-byte records, 2x2x2, "
                       f"threaded C restatement (oracle/mgr_oracle.c oracle_local_partition_omp) "
-                      f"of the local stage, best of 3 {[round(x, 3) for x in secs]} s"}
+                      f"of the local stage, median of {iters} after an untimed first call "
+                      f"{[round(x, 3) for x in secs]} s"}
 
 
 def load_traffic(kernel, workload):
@@ -249,6 +284,84 @@ def load_traffic(kernel, workload):
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         return None
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(nranks, argv, timeout_s, script=None, python=None, grace_s=20.0, out=None):
+    """The bare `python bench.py --gpus N` form: start N rank processes of
+    ``script`` (this file) as children -- never exec -- with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, each in
+    its own process group; relay rank 0's stdout (its JSON line) to ``out``;
+    wait at most ``timeout_s`` for all of them.  A rank that fails gets its
+    peers (likely stuck in a collective) killed after ``grace_s``; a timeout
+    kills every group.  Returns 0 only if every rank exited 0 and rank 0
+    printed a JSON line; else the first failing rank's code (124: timeout,
+    3: no line)."""
+    script = script or os.path.abspath(__file__)
+    python = python or sys.executable
+    out = out or sys.stdout
+    port = _free_port()
+    procs, lines = [], []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([python, script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None,
+                                      start_new_session=True, text=True))
+
+    def relay():
+        for line in procs[0].stdout:
+            lines.append(line)
+            out.write(line)
+            out.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        for p in procs:
+            p.wait()
+
+    t_end = time.monotonic() + timeout_s
+    first_fail, fail_at = None, None
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            break
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad and first_fail is None:
+            first_fail, fail_at = bad[0], time.monotonic()
+            print(f"bench launcher: rank {bad[0][0]} exited {bad[0][1]}", file=sys.stderr)
+        now = time.monotonic()
+        if now > t_end or (fail_at is not None and now - fail_at > grace_s):
+            if now > t_end:
+                print(f"bench launcher: timeout after {timeout_s:.0f} s, killing the ranks",
+                      file=sys.stderr)
+                first_fail = first_fail or (-1, 124)
+            kill_all()
+            break
+        time.sleep(0.2)
+    th.join(timeout=5)
+    if first_fail is not None:
+        return int(first_fail[1]) if first_fail[1] > 0 else 1
+    codes = [p.returncode for p in procs]
+    if any(c != 0 for c in codes):
+        return next(c for c in codes if c != 0) or 1
+    if not any(ln.lstrip().startswith("{") for ln in lines):
+        print("bench launcher: rank 0 printed no JSON line", file=sys.stderr)
+        return 3
+    return 0
 
 
 def main():
@@ -274,7 +387,18 @@ def main():
                     help="N > 1: pack the tiles in this many chunks, each chunk's rows sent "
                          "while the next is packed (exchange_pipelined); 0 = the product default "
                          "(redistributor.exchange_chunks_for)")
+    ap.add_argument("--soa", action="store_true",
+                    help="SoA payload: the fields as separate arrays moved by one multi-field "
+                         "pack (config 5: pos f32 x3, vel f32 x3, mass f32, id i64; configs "
+                         "2-4: pos f64 x3 + id i64); the position array is field 0")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="bare --gpus N > 1 (no WORLD_SIZE): seconds before the rank "
+                         "processes are killed")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # bare multi-GPU launch: start the ranks as children before anything
+        # touches the GPU (no exec from this process)
+        return launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout)
 
     import mpi_grid_redistribute_amd as mgr
     from mpi_grid_redistribute_amd import _lib
@@ -316,7 +440,27 @@ def main():
     if not multi:
         n = args.n or N_CFG2
         part = mgr.GridPartitioner([2, 2, 2], [1.0, 1.0, 1.0])
-        if cfg == 5:
+        if cfg == 5 and args.soa:
+            # config 5 with the record's fields as four arrays (SoA): one fine
+            # binning of the (n,3) f32 positions, ONE multi-field pack of the
+            # four arrays + fine ids; at the destination the fine sort of every
+            # field by the received ids
+            workload = f"cfg5_{_m(n)}_soa_pos_vel_mass_id_2x2x2_local_partition_plus_fine_sort_888"
+            rb, pos_desc = 36, "f32 (N,3) array, also payload field 0, wrapped in place"
+            src = mgr.synth_wide_soa(n, seed=SEED, gid0=0)
+            rcv = mgr.synth_wide_soa(n, seed=SEED + 1, gid0=0, hi=0.5)
+            R1 = mgr.MPIGridRedistributor(None, [1, 1, 1], [0.5, 0.5, 0.5])
+            flats = [t.reshape(-1).view(torch.uint8) for t in src]
+            rbs = [12, 12, 4, 8]
+            _, recv_fids, _ = mgr.GridPartitioner([1, 1, 1], [0.5] * 3).partition_fields_device(
+                [t.reshape(-1).view(torch.uint8).clone() for t in rcv], rbs, rcv[0].clone(),
+                fine_cells=[8, 8, 8])
+            recv_fids = recv_fids.clone()
+
+            def step():
+                part.partition_fields_device(flats, rbs, src[0], fine_cells=[8, 8, 8])
+                R1.fine_cell_sort(rcv, rcv[0], [8, 8, 8], fine_ids=recv_fids)
+        elif cfg == 5:
             # one GPU's share of config 5: 64M 36-byte records; the local stage
             # (bin + scan + pack into 8 destinations) and the destination-side
             # fine-cell sort (8x8x8) of 64M rows inside one cell
@@ -345,21 +489,38 @@ def main():
                 workload = f"cfg2_{_m(n)}_uniform_2x2x2_local_partition"
                 pos, rec = mgr.synth_uniform(n, seed=SEED, gid0=0)
             flat = rec.reshape(-1)
+            if args.soa:
+                # two arrays: the positions (field 0, binned and wrapped) and the ids
+                workload = workload.replace("_local_partition", "_soa_pos_id_local_partition")
+                pos_desc = "(N,3) float64, also payload field 0, wrapped in place"
+                ids = rec.view(torch.int64)[:, 3].contiguous()
+                flats = [pos.reshape(-1).view(torch.uint8), ids.view(torch.uint8)]
 
-            def step():
-                part.partition_device(flat, 32, pos)
+                def step():
+                    part.partition_fields_device(flats, [24, 8], pos)
+            else:
+                def step():
+                    part.partition_device(flat, 32, pos)
     else:
         n = args.n or (N_CFG5_PER_GPU if cfg == 5 else N_CFG3_PER_GPU)
         comm = mgr.RcclComm.from_torch_distributed()
         R = mgr.MPIGridRedistributor(comm, topo, [1.0, 1.0, 1.0])
         R.exchange_chunks = chunks
-        chunks = chunks or mgr.redistributor.exchange_chunks_for(world, rb + (2 if cfg == 5 else 0))
-        if cfg == 5:
+        chunks = chunks or mgr.redistributor.exchange_chunks_for(world, 36 if cfg == 5 else 32)
+        if cfg == 5 and args.soa:
+            workload = f"cfg5_soa_per_gpu_{_m(n)}_full_exchange_plus_fine_sort_888"
+            rb, pos_desc = 36, "f32 (N,3) array, also payload field 0, wrapped in place"
+            soa = mgr.synth_wide_soa(n, seed=SEED, gid0=rank * n)
+
+            def step_with(Rx):
+                Rx.redistribute_by_position(soa, soa[0], fine_cells=[8, 8, 8])
+        elif cfg == 5:
             workload = f"cfg5_rec36_per_gpu_{_m(n)}_full_exchange_plus_fine_sort_888"
             rb, pos_desc = 36, "f32 (N,3) view into the 36-byte records, wrapped in place"
             rec, pos = mgr.synth_wide(n, seed=SEED, gid0=rank * n)
-            def step():
-                R.redistribute_by_position(rec, pos, fine_cells=[8, 8, 8])
+
+            def step_with(Rx):
+                Rx.redistribute_by_position(rec, pos, fine_cells=[8, 8, 8])
         else:
             if cfg == 4:
                 workload = f"cfg4_clustered_per_gpu_{_m(n)}_full_exchange"
@@ -371,9 +532,22 @@ def main():
             ol = [args.overload] * 3 if args.overload > 0 else None
             if ol:
                 workload += f"_halo{args.overload:g}"
+            if args.soa:
+                if ol:
+                    raise SystemExit("--soa with --overload: the halo takes one payload array")
+                workload = workload.replace("_full_exchange", "_soa_pos_id_full_exchange")
+                pos_desc = "(N,3) float64, also payload field 0, wrapped in place"
+                soa = (pos, rec.view(torch.int64)[:, 3].contiguous())
+                del rec
 
-            def step():
-                R.redistribute_by_position(rec, pos, overload_lengths=ol)
+                def step_with(Rx):
+                    Rx.redistribute_by_position(soa, pos)
+            else:
+                def step_with(Rx):
+                    Rx.redistribute_by_position(rec, pos, overload_lengths=ol)
+
+        def step():
+            step_with(R)
 
     # Fresh f64 input needs the in-place wrap written back (redist.py:68: x + L
     # rounds, so most in-box coordinates change on the first call).  The bin
@@ -429,7 +603,8 @@ def main():
                           "in_timed_region": True}
             if _lib.alg_read(k):   # host-counted bytes (the halo's selections)
                 kernels[k]["alg_bytes_per_launch"] = _lib.alg_read(k) / cnt
-    missing = [k for k in list(row_bytes_per_kernel(cfg, bool(args.overload > 0))) + ["scan"]
+    missing = [k for k in list(row_bytes_per_kernel(cfg, bool(args.overload > 0),
+                                                    soa=args.soa)) + ["scan"]
                if k not in kernels]
     if missing:
         # detail pass (not timed): the kernels left out of the timed region
@@ -451,7 +626,7 @@ def main():
     # gathered after the timed region
     skew = None
     if not multi and cfg in (2, 4):
-        skew = count_skew(part.buffers(n, 32)[4].cpu().numpy().reshape(1, -1))
+        skew = count_skew(part.last_counts.cpu().numpy().reshape(1, -1))
     elif multi:
         sc = torch.as_tensor(R.last_counts[0], dtype=torch.int64, device="cuda")
         rows = [torch.empty_like(sc) for _ in range(world)] if world > 1 else [sc]
@@ -461,7 +636,7 @@ def main():
     xgmi = None
     if multi and "exchange" in kernels:
         xgmi = xgmi_report(R.last_traffic, kernels["exchange"], dist, world, chunks)
-    rccl, exchange_ab = None, None
+    rccl, exchange_ab, n1_same_ms = None, None, None
     if multi and world > 1:
         # untimed: one message per peer (exchange_chunks = 1) on the same
         # inputs, beside the pipelined steps of the timed region
@@ -479,6 +654,24 @@ def main():
         R.exchange_chunks = args.chunks or None
         exchange_ab = exchange_ab_block(elapsed / args.steps * 1e3, chunks,
                                         float(t.item()) / k1 * 1e3, k1)
+        # the same workload at N = 1: this rank's own rows through a one-rank
+        # redistributor (bin + scan + pack, no exchange), untimed pass, max
+        # over ranks -- the same-workload base of the scaling curve (the N = 1
+        # bench line itself is config 2)
+        R1 = mgr.MPIGridRedistributor(None, [1, 1, 1], [1.0, 1.0, 1.0])
+        if cfg != 5:
+            R1.set_write_back("all")
+        for _ in range(2):
+            step_with(R1)
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(k1):
+            step_with(R1)
+        barrier()
+        t = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n1_same_ms = float(t.item()) / k1 * 1e3
+        del R1
         mine = []
         if rccl_log:
             try:
@@ -500,8 +693,10 @@ def main():
     # this rank's n rows (received rows at N > 1 are ~n for the uniform
     # inputs), so a pack pipelined in k chunks covers n / k per launch -- or
     # the host-counted bytes of the halo's selections
-    fine_tr = int(_lib.load().mgr_ranked_tile_rows(36, 512)) if cfg == 5 else 2048
-    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world).items():
+    fine_tr = (int(_lib.load().mgr_ranked_tile_rows(12 if args.soa else 36, 512)) if cfg == 5
+               else 2048)
+    for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world,
+                                     soa=args.soa).items():
         if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
             e = kernels[k]
             per_step = e["launches"] / e["steps"] if e.get("steps") else 1
@@ -537,6 +732,10 @@ def main():
                      5: "synthetic (uniform 36-byte records, torch RNG on device)"}[cfg],
             "config": {"workload": workload, "particles_per_gpu": n,
                        "grid": topo, "payload_bytes": rb, "position": pos_desc,
+                       "payload_layout": ("SoA: " + ("pos f32x3, vel f32x3, mass f32, id i64"
+                                                     if cfg == 5 else "pos f64x3, id i64")
+                                          + " as separate arrays") if args.soa
+                       else "one record array",
                        "parallelism": f"{world} rank(s), one GPU per grid cell" if multi
                        else "1 GPU, 8 virtual subdomains",
                        "exchange_chunks": chunks if multi else None},
@@ -545,6 +744,7 @@ def main():
             "xgmi": xgmi,
             "rccl": rccl,
             "exchange_ab": exchange_ab,
+            "n1_same_workload_ms": n1_same_ms,
             "count_skew": skew,
             "cpu_baseline": cpu,
             "cpu_baseline_cfg1": cpu_1,
@@ -558,4 +758,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

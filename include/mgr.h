@@ -33,6 +33,7 @@ extern "C" {
 
 #define MGR_MAX_DIM 8
 #define MGR_MAX_BINS 4096
+#define MGR_MAX_FIELDS 16
 #define MGR_UNIQUE_ID_BYTES 128
 
 typedef enum {
@@ -213,6 +214,27 @@ int mgr_pack_tiles(const void* src, int64_t row_bytes, int64_t n, const void* de
                    void* redirect_dst, const uint16_t* ids_src, uint16_t* ids_dst,
                    uint16_t* ids_redirect_dst, int64_t tile_begin, int64_t tile_end,
                    void* stream);
+/* Multi-field (SoA) stable partition: the nfields payload arrays of the same
+ * n rows -- e.g. positions, velocities, masses and ids as separate arrays --
+ * partitioned by ONE destination array and ONE ranking, in one pass where
+ * the fields allow (redist.py:195-198 applied to every field with the same
+ * rank_to_send: the reference's own :160-164 pattern, which redistributes
+ * `position` with the destinations computed for `data`).  Field f: srcs[f]
+ * holds n rows of row_bytes[f] opaque bytes, its packed rows go to dsts[f]
+ * (and its redirect_bin rows to redirect_dsts[f]) exactly as mgr_pack would
+ * place them; ids_src (or NULL): an optional 2-byte side field moved alike
+ * (mgr_pack_ids).  tile_end < 0: every tile; else only the tiles
+ * [tile_begin, tile_end) (mgr_pack_tiles).  nfields <= MGR_MAX_FIELDS.
+ * Fields of 4-byte-multiple rows on 16-byte aligned sources (4-byte aligned
+ * outputs), <= 64 bins, move together in one launch of the multi-field
+ * kernel (each destination byte read and ranked once); any other field is
+ * packed on its own with the same destinations.                          */
+int mgr_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                    const void* dest, int nbins, int drop_bin, int tile_rows,
+                    const void* workspace, void* const* dsts, int redirect_bin,
+                    void* const* redirect_dsts, const uint16_t* ids_src, uint16_t* ids_dst,
+                    uint16_t* ids_redirect_dst, int64_t tile_begin, int64_t tile_end,
+                    void* stream);
 /* After mgr_scan: out[i * nbins + b] (device int64) = the first row of bin b
  * at tile tiles[i] in the packed layout (tiles[i] = the tile count: the bin's
  * end), i.e. where a chunk of tiles starts inside every bin's segment.

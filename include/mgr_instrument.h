@@ -28,7 +28,9 @@ extern "C" {
  * storing its inclusive word: the visibility order relaxed atomics on two
  * words allow, forced) and "scan_end_spins" (polls of the bin-end words by
  * the scan's last chunk, -1 = scan_spins; 0 = one look, which then reports
- * the forced race as a failed scan).  Each call publishes a new immutable
+ * the forced race as a failed scan), "scan_poison_chunk" (the scan chunk with
+ * this ticket publishes its prefix poisoned: a deterministic failed scan,
+ * -1 = none).  Each call publishes a new immutable
  * snapshot of every hook (the library's launches read one snapshot each);
  * < 0 for an unknown key or an out-of-range value.                         */
 int mgr_test_hook(const char* key, int64_t value);

@@ -68,6 +68,22 @@ def synth_clustered(n, seed=20261015, gid0=0, box=1.0, n_halos=64, sigma=0.02, f
     return pos.contiguous(), rec
 
 
+def synth_wide_soa(n, seed=20261015, gid0=0, box=1.0, lo=0.0, hi=None):
+    """BASELINE config 5 input as a SoA payload: the fields of synth_wide's
+    records (same values) as four GPU arrays -- positions (n, 3) float32,
+    velocities (n, 3) float32, masses (n,) float32, ids (n,) int64.  The
+    positions array is both a payload field and the ``position`` argument.
+    Test/bench input only."""
+    import torch
+
+    rec, pos = synth_wide(n, seed=seed, gid0=gid0, box=box, lo=lo, hi=hi)
+    f = rec.view(torch.float32)
+    out = (pos.contiguous(), f[:, 3:6].contiguous(), f[:, 6].contiguous(),
+           rec[:, 28:36].contiguous().view(torch.int64).reshape(-1))
+    del rec, f, pos
+    return out
+
+
 def synth_wide(n, seed=20261015, gid0=0, box=1.0, lo=0.0, hi=None):
     """BASELINE config 5 input: 36-byte records [pos f32 x3, vel f32 x3, mass
     f32, id i64] as an (n, 36) uint8 GPU tensor, positions uniform in

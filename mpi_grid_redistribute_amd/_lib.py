@@ -55,6 +55,8 @@ SIGNATURES = {
     "mgr_pack_ids": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P]),
     "mgr_pack_tiles": (_I, [_P, _I64, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _I64, _I64,
                             _P]),
+    "mgr_pack_fields": (_I, [_I, _P, _P, _I64, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _I64,
+                             _I64, _P]),
     "mgr_tile_offsets": (_I, [_P, _I64, _I, _I, _P, _I, _P, _P]),
     "mgr_partition_by_position": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I64, _P, _P, _P, _I,
                                        _P, _P]),
@@ -188,7 +190,7 @@ def test_hook(key, value):
 HOOK_DEFAULTS = {"tile_rounds": 0, "scan_chunk": 2048, "scan_max_chunks": 1024,
                  "scan_spins": 1 << 24, "pack_img_all": 0, "rank_rows": 0, "bin_unstaged": 0,
                  "bin_generic": 0, "pack_generic": 0, "scan_delay_bin": -1,
-                 "scan_delay_sleeps": 0, "scan_end_spins": -1}
+                 "scan_delay_sleeps": 0, "scan_end_spins": -1, "scan_poison_chunk": -1}
 
 
 # --------------------------------------------------------------- profiler

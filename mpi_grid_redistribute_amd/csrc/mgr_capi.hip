@@ -648,6 +648,43 @@ int mgr_pack_tiles(const void* src, int64_t row_bytes, int64_t n, const void* de
     return MGR_OK;
 }
 
+int mgr_pack_fields(int nfields, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                    const void* dest, int nbins, int drop_bin, int tile_rows,
+                    const void* workspace, void* const* dsts, int redirect_bin,
+                    void* const* redirect_dsts, const uint16_t* ids_src, uint16_t* ids_dst,
+                    uint16_t* ids_redirect_dst, int64_t tile_begin, int64_t tile_end,
+                    void* stream) {
+    int rc = check_tile(tile_rows);
+    if (rc) return rc;
+    if (nfields < 1 || nfields > MGR_MAX_FIELDS) return fail(MGR_EINVAL, "nfields %d", nfields);
+    if (!srcs || !row_bytes || !dsts) return fail(MGR_EINVAL, "null field arrays");
+    if (nbins < 1 || nbins > MGR_MAX_BINS) return fail(MGR_EINVAL, "nbins %d", nbins);
+    if (redirect_bin >= nbins) return fail(MGR_EINVAL, "redirect_bin out of range");
+    for (int f = 0; f < nfields; ++f) {
+        if (row_bytes[f] < 1) return fail(MGR_EINVAL, "field %d: row_bytes %lld", f, (long long)row_bytes[f]);
+        if (n > 0 && !srcs[f]) return fail(MGR_EINVAL, "field %d: null source", f);
+        if (n > 0 && redirect_bin >= 0 && (!redirect_dsts || !redirect_dsts[f]))
+            return fail(MGR_EINVAL, "field %d: redirect without buffer", f);
+    }
+    if (n > 0 && (!dest || !workspace)) return fail(MGR_EINVAL, "null argument");
+    if (n > 0 && redirect_bin >= 0 && ids_src && !ids_redirect_dst)
+        return fail(MGR_EINVAL, "redirect without an ids buffer");
+    if (n > 0 && ids_src && !ids_dst) return fail(MGR_EINVAL, "ids without an output");
+    mgr::Workspace ws = mgr::carve((void*)workspace, n, nbins, tile_rows);
+    if (tile_end >= 0) {
+        if (tile_begin < 0 || tile_end < tile_begin || tile_end > ws.T)
+            return fail(MGR_EINVAL, "tiles [%lld, %lld) of %lld", (long long)tile_begin,
+                        (long long)tile_end, (long long)ws.T);
+        if (tile_end == tile_begin) return MGR_OK;
+        ws.t0 = tile_begin;
+        ws.tn = tile_end - tile_begin;
+    }
+    HIP_OK(mgr::launch_pack_fields(nfields, srcs, row_bytes, n, dest, nbins, drop_bin, tile_rows,
+                                   ws, dsts, redirect_bin, redirect_bin >= 0 ? redirect_dsts : nullptr,
+                                   (hipStream_t)stream, ids_src, ids_dst, ids_redirect_dst));
+    return MGR_OK;
+}
+
 int mgr_tile_offsets(const void* workspace, int64_t n, int nbins, int tile_rows,
                      const int64_t* tiles, int ntiles, int64_t* out, void* stream) {
     int rc = check_tile(tile_rows);

@@ -222,7 +222,9 @@ __device__ __forceinline__ double pos_as_f64(PosT v) {
 
 // numpy's float -> integer casts on x86 (the in-place write-back of integer
 // positions wrapped in a float type; probed on numpy 2.2.6, pinned by
-// tests/golden/bin_dtypes.npz): <= 32-bit signed and <= 16-bit unsigned
+// tests/golden/bin_dtypes.npz, and -- the NaN / out-of-range branches, from
+// zero, negative and infinite boxes -- by tests/golden/bin_dtype_edges.npz,
+// both made by the reference): <= 32-bit signed and <= 16-bit unsigned
 // types through a 32-bit cvttsd2si (NaN / out of range -> INT_MIN, then the
 // low bits), int64 through the 64-bit one; uint32 / uint64: values at or
 // above 2^(w-1) converted after subtracting it, the top bit flipped back;

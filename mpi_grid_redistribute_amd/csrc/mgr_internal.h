@@ -135,6 +135,11 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
                        int redirect_bin, void* redirect_dst, hipStream_t s,
                        const uint16_t* ids_src = nullptr, uint16_t* ids_dst = nullptr,
                        uint16_t* ids_red = nullptr);
+hipError_t launch_pack_fields(int nf, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                              const void* dest, int nbins, int drop_bin, int tile_rows,
+                              const Workspace& ws, void* const* dsts, int redirect_bin,
+                              void* const* reds, hipStream_t s, const uint16_t* ids_src,
+                              uint16_t* ids_dst, uint16_t* ids_red);
 hipError_t launch_synth_uniform(uint64_t seed, int64_t gid0, int64_t n, int dim,
                                 const double* box, double* pos, void* rec32, hipStream_t s);
 int pack_tile_rows(int64_t row_bytes, int nbins);
@@ -169,10 +174,11 @@ struct Hooks {
     int scan_delay_bin = -1;
     int scan_delay_sleeps = 0;
     int scan_end_spins = -1;
+    int scan_poison_chunk = -1;   // >= 0: that scan chunk publishes poisoned (a failed scan)
 };
 // The scan kernel's copy of the race-test hooks (kernel argument).
 struct ScanTest {
-    int delay_bin, delay_sleeps, end_spins;
+    int delay_bin, delay_sleeps, end_spins, poison_chunk;
 };
 const Hooks& hooks();
 int set_hook(const char* key, int64_t value);   // mgr_test_hook

@@ -56,6 +56,7 @@ int set_hook(const char* key, int64_t v) {
     else if (!strcmp(key, "scan_delay_bin") && in(-1, MGR_MAX_BINS)) h->scan_delay_bin = (int)v;
     else if (!strcmp(key, "scan_delay_sleeps") && in(0, 1 << 16)) h->scan_delay_sleeps = (int)v;
     else if (!strcmp(key, "scan_end_spins") && in(-1, 1 << 30)) h->scan_end_spins = (int)v;
+    else if (!strcmp(key, "scan_poison_chunk") && in(-1, 1 << 30)) h->scan_poison_chunk = (int)v;
     else return -1;
     g_hooks.store(h.get(), std::memory_order_release);
     kept.push_back(std::move(h));
@@ -126,14 +127,16 @@ __global__ __launch_bounds__(kBlock) void scan_onepass_kernel(const int32_t* __r
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         long long excl = 0;
-        uint64_t poison = 0;
+        // test hook: this chunk's prefix is published poisoned -- every
+        // prefix built on it carries the bit, the scan reports a failure
+        uint64_t poison = j == tst.poison_chunk ? kScanPoison : 0;
         // test hook: the chunk ending bin tst.delay_bin stores its inclusive
         // word only after counting itself done
         const bool late = tst.delay_bin >= 0 && j == (tst.delay_bin + 1) * cpb - 1 &&
                           j != (int)gridDim.x - 1;
         if (j == 0) {
-            if (lane == 0 && !late) flag_store(&flags[0], kScanInc | (uint64_t)agg);
-            if (lane == 0) s_incl = kScanInc | (uint64_t)agg;
+            if (lane == 0 && !late) flag_store(&flags[0], kScanInc | poison | (uint64_t)agg);
+            if (lane == 0) s_incl = kScanInc | poison | (uint64_t)agg;
         } else {
             if (lane == 0) flag_store(&flags[j], kScanAgg | (uint64_t)agg);
             for (int base = j - 1;; base -= 64) {
@@ -517,7 +520,7 @@ hipError_t launch_scan(int64_t n, int nbins, int tile_rows, const Workspace& ws,
     hipLaunchKernelGGL(k, dim3((unsigned)(nbins * cpb)), dim3(kBlock), 0, s, ws.counts, ws.T,
                        chunk, (int)cpb, nbins, ws.flags, ws.offsets, ws.bin_starts, bin_counts,
                        h.scan_spins, ScanTest{h.scan_delay_bin, h.scan_delay_sleeps,
-                                              h.scan_end_spins});
+                                              h.scan_end_spins, h.scan_poison_chunk});
     prof_end(s, K_SCAN);
     return hipGetLastError();
 }

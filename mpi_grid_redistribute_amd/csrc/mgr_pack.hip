@@ -2,6 +2,8 @@
 // payload field into the bin-major send buffer / output (redist.py:195-198,
 // send_buff[i] = data[rank_to_send == i], order kept), with their launchers
 // and tile-size policy.  Helpers: mgr_device.h.
+#include <vector>
+
 #include "mgr_device.h"
 
 namespace mgr {
@@ -616,6 +618,162 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
     }
 }
 
+// Multi-field (SoA) pack, <= 64 bins: the fields of the same rows -- e.g.
+// positions, velocities, masses and ids held as separate arrays -- moved by
+// ONE launch that reads every row's destination byte once and ranks it once
+// (redist.py:195-198 applied to every field with the same rank_to_send, the
+// :160-164 pattern).  The cooperative shape of pack_img_kernel: one wave per
+// 128 rows (two 64-row rounds), per-bin bases exchanged through LDS behind
+// one barrier.  Every field's 128 rows (128 * rb bytes, 16-byte aligned) are
+// copied into wave-private LDS by LDS-DMA (global_load_lds_dwordx4: no
+// registers, so any number of fields up to kFieldsLds bytes), the rows'
+// image slots (destination-major, stable) are written as an inverse
+// permutation (slot -> row) plus the bin of every slot, and each field's
+// destination-ordered image is streamed out in 16-byte units gathered from
+// the LDS rows: a unit inside one bin's run is one 16-byte store to the
+// run's (4-byte aligned) place, a unit straddling two runs goes dword by
+// dword.  Row bytes of every field are 4-byte multiples; the optional 2-byte
+// side field (fine cells) is stored per row as in pack_img_kernel.
+constexpr int kFieldsMax = 8;          // fields per launch
+constexpr int kFieldsWR = 128;         // rows per wave
+struct PackFieldsArgs {
+    const uint8_t* src[kFieldsMax];
+    uint8_t* dst[kFieldsMax];
+    uint8_t* red[kFieldsMax];
+    int rb[kFieldsMax];          // row bytes, 4-byte multiples
+    uint32_t rinv[kFieldsMax];   // floor(2^32 / rb) + 1: x / rb == umulhi(x, rinv) for x < 2^18
+    int loff[kFieldsMax];        // byte offset of field f's rows in a wave's LDS area
+    int nf;
+    int wave_lds;                // LDS bytes per wave
+};
+
+__global__ __launch_bounds__(1024) void pack_fields_kernel(
+    PackFieldsArgs fa, int64_t n, const uint8_t* __restrict__ dest, int nb, int nbits,
+    int drop_bin, const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts,
+    int64_t T, int64_t t0, int64_t tn, int tile_rows, int redirect_bin, int xcd,
+    const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
+    uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
+    constexpr int WR = kFieldsWR, RPW = WR / 64;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
+    const int nw = blockDim.x >> 6;
+    int* s_cnt = (int*)smem;                                    // [nw][64]
+    uint8_t* wl = smem + nw * 64 * 4 + w * fa.wave_lds;         // the fields' rows
+    long long* rowoff = (long long*)(wl + fa.wave_lds - 64 * 8 - 2 * WR);   // [64]
+    uint8_t* inv = (uint8_t*)(rowoff + 64);                     // image slot -> wave row
+    uint8_t* ibin = inv + WR;                                   // image slot -> bin
+    const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
+    const int64_t row0 = tile * (int64_t)tile_rows + (int64_t)WR * w;
+    const int nrows = __builtin_amdgcn_readfirstlane((int)max((int64_t)0, min((int64_t)WR, n - row0)));
+    unsigned braw[RPW], b[RPW], idv[RPW];
+    bool valid[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        valid[q] = 64 * q + lane < nrows;
+        const int64_t r = min(row0 + 64 * q + lane, n - 1);
+        braw[q] = (unsigned)dest[r];
+        idv[q] = id_src ? (unsigned)id_src[r] : 0u;
+    }
+    const SegLoad seg = seg_load(offsets, bin_starts, T, tile, lane, nb, redirect_bin);
+    // every field's rows into LDS: unit x = 16 * (64 i + lane) of the field's
+    // 128 rows lands at loff + x (LDS-DMA: wave-uniform base + lane * 16;
+    // lanes past the rows are masked off, so nothing lands beyond them); the
+    // last unit of the array reads up to 12 bytes past its end, inside the
+    // 16-byte-aligned unit's page
+#pragma unroll
+    for (int f = 0; f < kFieldsMax; ++f) {
+        if (f >= fa.nf) break;
+        const int rb = fa.rb[f];
+        const int nbytes = nrows * rb;
+        const uint8_t* sp = fa.src[f] + row0 * rb;
+        for (int i = 0; 1024 * i < nbytes; ++i) {
+            const int x = 16 * (64 * i + lane);
+            if (x < nbytes)
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(sp + x),
+                    (__attribute__((address_space(3))) void*)(wl + fa.loff[f] + 1024 * i), 16, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) b[q] = valid[q] ? braw[q] : 0u;
+    long long tbase = lane < nb ? seg_value(seg, lane, redirect_bin) : 0;
+    // rank inside each round; lane l counts bin l per round, cnt over the wave
+    unsigned long long pe[RPW];
+    int cq[RPW], cnt = 0;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        unsigned long long p = __ballot(valid[q]), mine = p;
+        for (int i = 0; i < nbits; ++i) {
+            const unsigned long long m = __ballot((b[q] >> i) & 1u);
+            p &= ((b[q] >> i) & 1u) ? m : ~m;
+            mine &= ((lane >> i) & 1) ? m : ~m;
+        }
+        pe[q] = p;
+        cq[q] = __popcll(mine);
+        cnt += cq[q];
+    }
+    s_cnt[w * 64 + lane] = cnt;
+    __syncthreads();   // (also retires the LDS-DMA loads: vmcnt(0) before the barrier)
+    if (scan_failed(scan_err)) return;
+    for (int j = 0; j < w; ++j) tbase += s_cnt[j * 64 + lane];
+    // wave image order: exclusive prefix of the wave's bin counts
+    const int excl = wave_incl_dpp(cnt) - cnt;
+    int run = excl;   // lane b: bin b's next image slot, round by round
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        // (shuffles in uniform control flow: a bpermute from a lane outside
+        // the exec mask does not read that lane's value)
+        const int slot = __shfl(run, (int)b[q], 64) + (valid[q] ? rank_in(pe[q]) : 0);
+        const long long gr = id_src ? __shfl(tbase - excl, (int)b[q], 64) + slot : 0;
+        run += cq[q];
+        if (valid[q]) {
+            inv[slot] = (uint8_t)(64 * q + lane);
+            ibin[slot] = (uint8_t)b[q];
+            if (id_src && (int)b[q] != drop_bin)
+                ((int)b[q] == redirect_bin ? id_red : id_dst)[gr] = (uint16_t)idv[q];
+        }
+    }
+    if (lane < nb) rowoff[lane] = tbase - excl;   // output row of image slot 0, bin lane
+    wave_sync();
+    // every field's image, gathered from the LDS rows through the inverse
+    // permutation, streamed out in 16-byte units
+#pragma unroll
+    for (int f = 0; f < kFieldsMax; ++f) {
+        if (f >= fa.nf) break;
+        const int rb = fa.rb[f];
+        const uint32_t rinv = fa.rinv[f];
+        const uint8_t* rows = wl + fa.loff[f];
+        const unsigned long long dbase = (unsigned long long)fa.dst[f];
+        const unsigned long long rbase = (unsigned long long)fa.red[f];
+        const int nbytes = nrows * rb;
+        auto addr = [&](int bb) -> unsigned long long {
+            return (bb == redirect_bin ? rbase : dbase) + (unsigned long long)(rowoff[bb] * rb);
+        };
+        for (int x = 16 * lane; x < nbytes; x += 1024) {
+            int s[4];
+            u32x4_t q;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int xd = min(x + 4 * d, nbytes - 4);
+                s[d] = (int)__umulhi((unsigned)xd, rinv);
+                const int o = xd - s[d] * rb;
+                q[d] = *(const uint32_t*)(rows + (int)inv[s[d]] * rb + o);
+            }
+            const int bf = ibin[s[0]], bl = ibin[s[3]];
+            if (x + 16 <= nbytes && bf == bl) {
+                if (bf != drop_bin) gstore<u32x4_a4>(addr(bf) + x, q);
+            } else {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const int xd = x + 4 * d;
+                    const int bd = ibin[s[d]];
+                    if (xd < nbytes && bd != drop_bin) gstore<uint32_t>(addr(bd) + xd, q[d]);
+                }
+            }
+        }
+    }
+}
+
 // Many-destination pack (65..1024 bins, e.g. the 512 fine cells of config
 // 5) in the cooperative shape: one workgroup of 16 waves per tile of R = 16*RPW
 // rounds, wave w ranking and moving rounds w*RPW.. with unit-transposed
@@ -1189,6 +1347,83 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
     // the kernel that moved the rows cannot carry the ids: a 2-byte-row pack
     return launch_pack_rows(ids_src, 2, n, dest, nbins, drop_bin, tile_rows, ws, ids_dst,
                             redirect_bin, ids_red, s, nullptr);
+}
+
+// mgr_pack_fields: several fields of the same rows, one ranking.  With one
+// field this is launch_pack (the coop / image kernels A/B'd for it).  With
+// more, the fields pack_fields_kernel takes (4-byte-multiple rows, 16-byte
+// aligned sources, 4-byte aligned outputs, <= 64 bins on 1-byte
+// destinations, tiles of 128-row waves) move in as few launches as their LDS
+// rows allow -- one for every realistic SoA set -- carrying the side field;
+// any other field is packed by launch_pack on the same destinations.
+hipError_t launch_pack_fields(int nf, const void* const* srcs, const int64_t* row_bytes, int64_t n,
+                              const void* dest, int nbins, int drop_bin, int tile_rows,
+                              const Workspace& ws, void* const* dsts, int redirect_bin,
+                              void* const* reds, hipStream_t s, const uint16_t* ids_src,
+                              uint16_t* ids_dst, uint16_t* ids_red) {
+    if (n <= 0) return hipSuccess;
+    if (nf == 1)
+        return launch_pack(srcs[0], row_bytes[0], n, dest, nbins, drop_bin, tile_rows, ws, dsts[0],
+                           redirect_bin, reds ? reds[0] : nullptr, s, ids_src, ids_dst, ids_red);
+    const Hooks& h = hooks();
+    const int nw = tile_rows / kFieldsWR;
+    const bool shape = !h.pack_generic && nbins <= 64 && dest_bytes(nbins) == 1 &&
+                       tile_rows % kFieldsWR == 0 && nw >= 1 && nw <= 16;
+    // rows of one wave's fields, within the LDS a workgroup may take
+    const int budget = (160 * 1024 - nw * 256) / max(nw, 1) - (64 * 8 + 2 * kFieldsWR);
+    std::vector<int> fast, slow;
+    for (int f = 0; f < nf; ++f) {
+        uintptr_t a = (uintptr_t)dsts[f] | (uintptr_t)row_bytes[f];
+        if (redirect_bin >= 0 && reds) a |= (uintptr_t)reds[f];
+        const bool ok = shape && row_bytes[f] >= 4 && row_bytes[f] % 4 == 0 &&
+                        (int64_t)kFieldsWR * row_bytes[f] <= budget &&
+                        ((uintptr_t)srcs[f] & 15) == 0 && (a & 3) == 0;
+        (ok ? fast : slow).push_back(f);
+    }
+    if (fast.size() < 2) {   // nothing to share: each field by its own kernel
+        slow.insert(slow.end(), fast.begin(), fast.end());
+        fast.clear();
+    }
+    bool side_done = ids_src == nullptr;
+    size_t i = 0;
+    while (i < fast.size()) {
+        PackFieldsArgs fa{};
+        int rows = 0;
+        for (; i < fast.size() && fa.nf < kFieldsMax; ++i) {
+            const int f = fast[i];
+            const int rb = (int)row_bytes[f];
+            if (rows + kFieldsWR * rb > budget) break;
+            fa.src[fa.nf] = (const uint8_t*)srcs[f];
+            fa.dst[fa.nf] = (uint8_t*)dsts[f];
+            fa.red[fa.nf] = reds ? (uint8_t*)reds[f] : nullptr;
+            fa.rb[fa.nf] = rb;
+            fa.rinv[fa.nf] = (uint32_t)(0x100000000ull / (unsigned)rb + 1);
+            fa.loff[fa.nf] = rows;
+            rows += kFieldsWR * rb;   // a multiple of 512 bytes
+            ++fa.nf;
+        }
+        fa.wave_lds = rows + 64 * 8 + 2 * kFieldsWR;
+        const int lds = nw * 64 * 4 + nw * fa.wave_lds;
+        ensure_lds(pack_fields_kernel, lds);
+        prof_begin(s, K_PACK);
+        hipLaunchKernelGGL(pack_fields_kernel, dim3((unsigned)ws.tn), dim3(64 * nw), (size_t)lds, s,
+                           fa, n, (const uint8_t*)dest, nbins, nbits_for(nbins), drop_bin,
+                           ws.offsets, ws.bin_starts, ws.T, ws.t0, ws.tn, tile_rows, redirect_bin,
+                           kXcdPackChunk, ws.scan_err, side_done ? nullptr : ids_src, ids_dst,
+                           ids_red);
+        prof_end(s, K_PACK);
+        side_done = true;
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    for (const int f : slow) {
+        const hipError_t e = launch_pack(srcs[f], row_bytes[f], n, dest, nbins, drop_bin, tile_rows,
+                                         ws, dsts[f], redirect_bin, reds ? reds[f] : nullptr, s,
+                                         side_done ? nullptr : ids_src, ids_dst, ids_red);
+        side_done = true;
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 static hipError_t launch_pack_rows(const void* src, int64_t row_bytes, int64_t n,

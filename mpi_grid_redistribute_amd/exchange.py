@@ -14,6 +14,7 @@ Steps 1, 2 and 4 are device-agnostic (CPU tensors + gloo in the tests).
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from dataclasses import dataclass
 
 import numpy as np
@@ -179,20 +180,28 @@ def exchange(transport, row_bytes, bin_counts, rank, device, pack, extra_rows=No
     return outs, lay
 
 
-_COMM_STREAMS = {}
+_COMM_STREAMS = OrderedDict()
+_COMM_STREAMS_MAX = 16
 
 
 def _comm_stream(device):
     """The side stream the pipelined exchange posts its row messages on: one
     per (device, compute stream) for the process, not one per call -- calls on
     different compute streams (the Scratch sets of redistributor.py) get
-    different comm streams, so neither queues behind the other's messages."""
+    different comm streams, so neither queues behind the other's messages.
+    The cache is bounded (least recently used out beyond _COMM_STREAMS_MAX
+    keys): a caller cycling through short-lived compute streams does not grow
+    it, and a stale entry for a reused raw handle only means a shared comm
+    stream -- every use is ordered by wait_stream on both sides."""
     d = torch.device(device)
     idx = d.index if d.index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(idx).cuda_stream)
-    st = _COMM_STREAMS.get(key)
+    st = _COMM_STREAMS.pop(key, None)
     if st is None:
-        st = _COMM_STREAMS[key] = torch.cuda.Stream(device=idx)
+        st = torch.cuda.Stream(device=idx)
+    _COMM_STREAMS[key] = st                      # most recently used last
+    while len(_COMM_STREAMS) > _COMM_STREAMS_MAX:
+        _COMM_STREAMS.popitem(last=False)
     return st
 
 

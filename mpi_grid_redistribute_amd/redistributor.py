@@ -155,6 +155,65 @@ def _sort_by_ids(fields, ids, n, nb, dev, scratch=None, check_ids=True):
     return outs, counts
 
 
+def _payload(data, dev):
+    """The payload of a call as a list of fields (Rows): one array, or --
+    SoA -- a tuple / list of arrays sharing axis 0 (positions, velocities,
+    masses, ids ...), each of any dtype and trailing shape, moved with the
+    same destinations (redist.py:160-164 redistributes ``position`` with the
+    ``rank_to_send`` computed for ``data``: the reference's multi-field
+    pattern).  Returns (fields, multi)."""
+    if isinstance(data, (tuple, list)):
+        if not data:
+            raise ValueError("data: an empty sequence of fields")
+        if len(data) > MAX_FIELDS:
+            raise ValueError(f"data: at most {MAX_FIELDS} fields (got {len(data)})")
+        fields = [Rows(d, dev) for d in data]
+        for i, f in enumerate(fields[1:], 1):
+            if f.n != fields[0].n:
+                raise ValueError(f"data field {i} has {f.n} rows, field 0 has {fields[0].n}")
+        return fields, True
+    return [Rows(data, dev)], False
+
+
+def _alias_rows(position, fields):
+    """The numpy payload field ``position`` shares memory with (the wrap then
+    writes into that field's device copy, Positions), else None."""
+    if not isinstance(position, np.ndarray):
+        return None
+    for f in fields:
+        if f.kind == "numpy" and f.n and np.shares_memory(position, f.host):
+            return f
+    return fields[0] if len(fields) == 1 else None
+
+
+def _results(fields, outs, m, multi):
+    """Outputs of m rows in the caller's containers: one array, or a tuple in
+    the order of the fields."""
+    res = tuple(f.wrap(o, m) for f, o in zip(fields, outs))
+    return res if multi else res[0]
+
+
+MAX_FIELDS = 16   # mgr.h MGR_MAX_FIELDS
+
+
+def _tile_hint(row_bytes, side=None):
+    """The row size the tile policy (mgr_tile_rows) sizes tiles for: one
+    field's row bytes, or -- when several fields move together through the
+    multi-field kernel -- their sum (the bytes a tile of rows moves); a 2-byte
+    side field (index ``side``) rides along and does not count."""
+    rb = [int(b) for i, b in enumerate(row_bytes) if i != side]
+    return max(sum(rb) if len(rb) > 1 else max(rb + [1]), 1)
+
+
+def _ptrs(addrs):
+    """A C array of device addresses (void* const*)."""
+    return (ctypes.c_void_p * len(addrs))(*[int(a) for a in addrs])
+
+
+def _i64s(vals):
+    return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+
+
 def _offsets_like(data, counts, dev):
     """offsets[nb+1] from device counts, in the container of ``data``; host
     results are checked for a failed scan (-1 counts) at the copy, device
@@ -174,17 +233,17 @@ def _fine_sort(plan, coarse, dim, dev, data, position, return_positions, fine_id
     coarse plan, periodic=0: no wrap, no write-back; the fine cell is the fine
     plan's binning by construction, mgr_device.h bin_coord) -- then the
     stable sort by them (_sort_by_ids)."""
-    rows = Rows(data, dev)
-    pos = Positions(position, dim, dev, data_rows=rows)
-    if pos.n != rows.n:
-        raise ValueError(f"data has {rows.n} rows, position has {pos.n}")
-    n, nb = rows.n, plan.nbins
+    rows, multi = _payload(data, dev)
+    pos = Positions(position, dim, dev, data_rows=_alias_rows(position, rows))
+    if pos.n != rows[0].n:
+        raise ValueError(f"data has {rows[0].n} rows, position has {pos.n}")
+    n, nb = rows[0].n, plan.nbins
     prow = Rows(position, dev) if return_positions else None
-    fields = [rows] + ([prow] if prow else [])
+    fields = rows + ([prow] if prow else [])
     check = fine_ids is not None
     if fine_ids is None:
         ids = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
-        hint = max(rows.row_bytes, prow.row_bytes if prow else 1)
+        hint = max(f.row_bytes for f in fields)
         tile_rows, ws, dest = _scratch(n, coarse.nbins, hint, dev)
         _lib.call("mgr_bin_count_fine", coarse.h, plan.h, ctypes.c_void_p(pos.addr), pos.code, n,
                   pos.stride, 0, _lib.ptr(dest), _lib.ptr(ids), tile_rows, _lib.ptr(ws),
@@ -193,8 +252,11 @@ def _fine_sort(plan, coarse, dim, dev, data, position, return_positions, fine_id
     else:
         ids = _as_ids(fine_ids, n, dev, nb)
     outs, counts = _sort_by_ids(fields, ids, n, nb, dev, check_ids=check)
-    res = [f.wrap(o, n) for f, o in zip(fields, outs)]
-    return tuple(res) + (_offsets_like(data, counts, dev),)
+    nd = len(rows)
+    res = [_results(rows, outs[:nd], n, multi)]
+    if prow:
+        res.append(prow.wrap(outs[nd], n))
+    return tuple(res) + (_offsets_like(rows[0].obj, counts, dev),)
 
 
 class _IdField:
@@ -394,31 +456,42 @@ class MPIGridRedistributor:
                                  return_positions=False, fine_cells=None):
         """redist.py:115-166.  Returns the rows of ``data`` whose position
         falls in this rank's cell, from every rank, in source-rank order;
-        ``position`` is wrapped in place when periodic (S1).  With
-        ``overload_lengths`` the halo rows follow (redist.py:161-166; the
+        ``position`` is wrapped in place when periodic (S1).  ``data`` may be
+        one array or -- SoA -- a tuple / list of arrays sharing axis 0 (e.g.
+        ``(pos, vel, mass, ids)``): every field moves with the same
+        destinations (one binning, one scan, one count exchange, one pack
+        launch, one RCCL group) and the result is a tuple in the same order.
+        With ``overload_lengths`` the halo rows follow (redist.py:161-166; the
         halo exchange always runs periodic, :165).  With ``fine_cells``
         (config 5, no reference counterpart) the received rows come back
         stably sorted by fine cell with their offsets, = ``fine_cell_sort``
-        of the plain result, computed from fine cells binned at the source."""
-        self._check_host_alias(data, position)
+        of the plain result, computed from fine cells binned at the source.
+        ``return_positions``: (data, positions) -- (data, [positions,]
+        offsets) with ``fine_cells``; ``data`` is the tuple of fields for a
+        SoA payload."""
+        fields, multi = _payload(data, self._dev)
+        for d in (data if multi else [data]):
+            self._check_host_alias(d, position)
         self.comm.reset_traffic()
-        rows = Rows(data, self._dev)
-        pos = Positions(position, self.dim, self._dev, data_rows=rows)
-        if pos.n != rows.n:
-            raise ValueError(f"data has {rows.n} rows, position has {pos.n}")
+        pos = Positions(position, self.dim, self._dev, data_rows=_alias_rows(position, fields))
+        n = fields[0].n
+        if pos.n != n:
+            raise ValueError(f"data has {n} rows, position has {pos.n}")
         if fine_cells is not None:
             if overload_lengths is not None:
                 raise NotImplementedError("fine_cells together with overload_lengths")
-            return self._redistribute_fine(data, position, rows, pos, periodic, fine_cells,
-                                           return_positions)
+            return self._redistribute_fine(data, position, fields, multi, pos, periodic,
+                                           fine_cells, return_positions)
         halo = overload_lengths is not None
         if halo:
+            if multi:
+                raise NotImplementedError("overload_lengths with a SoA (tuple) payload: pass "
+                                          "one array (e.g. a structured record)")
             self._check_halo(overload_lengths)
-            return self._redistribute_halo(data, position, rows, pos, periodic,
+            return self._redistribute_halo(data, position, fields[0], pos, periodic,
                                            overload_lengths, return_positions)
-        fields = [rows]
-        if return_positions:
-            fields.append(None)  # filled after binning (wrapped values)
+        nd = len(fields)
+        run_fields = list(fields) + ([None] if return_positions else [])
 
         def binner(dest, tile_rows, ws):
             _lib.call("mgr_bin_count", self._plan.h, ctypes.c_void_p(pos.addr), pos.code, pos.n,
@@ -426,15 +499,15 @@ class MPIGridRedistributor:
                       _lib.stream_handle())
             pos.finish()
             if return_positions:  # the wrapped positions, full rows
-                fields[1] = Rows(position, self._dev)
+                run_fields[nd] = Rows(position, self._dev)
 
-        row_bytes_hint = [rows.row_bytes]
+        row_bytes_hint = [f.row_bytes for f in fields]
         if return_positions:
             row_bytes_hint.append(self._pos_row_bytes(position, pos))
-        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=row_bytes_hint)
-        res = rows.wrap(outs[0], m)
+        outs, m = self._run(run_fields, binner, n, drop=False, row_bytes_hint=row_bytes_hint)
+        res = _results(fields, outs[:nd], m, multi)
         if return_positions:
-            return res, fields[1].wrap(outs[1], m)
+            return res, run_fields[nd].wrap(outs[nd], m)
         return res
 
     def _redistribute_halo(self, data, position, rows, pos, periodic, overload_lengths,
@@ -470,7 +543,7 @@ class MPIGridRedistributor:
         extra = lambda m_: halo_capacity(self, m_, overload_lengths)  # noqa: E731
         pending = []   # one rank: the scan's counts checked at the halo's host read
         outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=hint,
-                            extra_rows=extra, side_ids=not one, deferred=pending)
+                            extra_rows=extra, side=None if one else 1, deferred=pending)
         rbd = rows.row_bytes
         rbp = fields[ip].row_bytes if rp else 0
         cap = outs[0].numel() // max(rbd, 1) - m
@@ -505,16 +578,17 @@ class MPIGridRedistributor:
                                                  fine=fine)
         return plan
 
-    def _redistribute_fine(self, data, position, rows, pos, periodic, fine_cells,
+    def _redistribute_fine(self, data, position, fields, multi, pos, periodic, fine_cells,
                            return_positions):
         """Source: bin + fine cell of every row (mgr_bin_count_fine), the
-        fine cells packed and exchanged as a 2-byte field beside the rows;
-        destination: count -> scan -> pack by the received fine cells."""
+        fine cells packed and exchanged as a 2-byte side field beside the
+        payload's fields; destination: rank -> scan -> pack of every field by
+        the received fine cells."""
         fplan = self._fine_plan(fine_cells)
-        fids = self._scratch.get("fine_src", max(rows.n, 1) * 2)
-        fields = [rows, _IdField(fids)]
-        if return_positions:
-            fields.append(None)
+        n = fields[0].n
+        nd = len(fields)
+        fids = self._scratch.get("fine_src", max(n, 1) * 2)
+        run_fields = list(fields) + [_IdField(fids)] + ([None] if return_positions else [])
 
         def binner(dest, tile_rows, ws):
             _lib.call("mgr_bin_count_fine", self._plan.h, fplan.h, ctypes.c_void_p(pos.addr),
@@ -522,24 +596,26 @@ class MPIGridRedistributor:
                       _lib.ptr(fids), tile_rows, _lib.ptr(ws), _lib.stream_handle())
             pos.finish()
             if return_positions:
-                fields[2] = Rows(position, self._dev)
+                run_fields[nd + 1] = Rows(position, self._dev)
 
-        hint = [rows.row_bytes, 2]
+        hint = [f.row_bytes for f in fields] + [2]
         if return_positions:
             hint.append(self._pos_row_bytes(position, pos))
-        outs, m = self._run(fields, binner, rows.n, drop=False, row_bytes_hint=hint, side_ids=True)
-        ids = outs[1][: 2 * m].view(torch.int16) if m else torch.empty(0, dtype=torch.int16,
-                                                                        device=self._dev)
-        recv = [_IdField(outs[0])] + ([_IdField(outs[2])] if return_positions else [])
-        recv[0].row_bytes = rows.row_bytes
-        if return_positions:
-            recv[1].row_bytes = fields[2].row_bytes
+        outs, m = self._run(run_fields, binner, n, drop=False, row_bytes_hint=hint, side=nd)
+        ids = outs[nd][: 2 * m].view(torch.int16) if m else torch.empty(0, dtype=torch.int16,
+                                                                         device=self._dev)
+        sort = [i for i in range(len(run_fields)) if i != nd]
+        recv = []
+        for i in sort:
+            r = _IdField(outs[i])
+            r.row_bytes = run_fields[i].row_bytes
+            recv.append(r)
         sorted_, counts = _sort_by_ids(recv, ids, m, fplan.nbins, self._dev, self._scratch,
                                        check_ids=False)   # binned here: in range
-        res = [rows.wrap(sorted_[0], m)]
+        res = [_results(fields, sorted_[:nd], m, multi)]
         if return_positions:
-            res.append(fields[2].wrap(sorted_[1], m))
-        return tuple(res) + (_offsets_like(data, counts, self._dev),)
+            res.append(run_fields[nd + 1].wrap(sorted_[nd], m))
+        return tuple(res) + (_offsets_like(fields[0].obj, counts, self._dev),)
 
     def exchange_overload_by_position(self, data, position, overload_lengths,
                                       return_positions=False, periodic=True):
@@ -616,55 +692,64 @@ class MPIGridRedistributor:
 
     def redistribute_by_cell_number(self, data, rank_to_send):
         """redist.py:169-200: send row i to rank ``rank_to_send[i]``; ids
-        outside [0, size) are dropped (S6)."""
+        outside [0, size) are dropped (S6).  ``data``: one array or a tuple /
+        list of arrays sharing axis 0 (SoA), all sent with the same ids in one
+        pass; the result is then a tuple in the same order."""
         self.comm.reset_traffic()
-        rows = Rows(data, self._dev)
+        fields, multi = _payload(data, self._dev)
+        n = fields[0].n
         ids, code = id_array(rank_to_send, self._dev)
-        if ids.numel() != rows.n:
-            raise ValueError(f"data has {rows.n} rows, rank_to_send has {ids.numel()}")
+        if ids.numel() != n:
+            raise ValueError(f"data has {n} rows, rank_to_send has {ids.numel()}")
 
         def binner(dest, tile_rows, ws):
-            _lib.call("mgr_bin_ids", self._plan.h, _lib.ptr(ids), code, rows.n, _lib.ptr(dest),
+            _lib.call("mgr_bin_ids", self._plan.h, _lib.ptr(ids), code, n, _lib.ptr(dest),
                       tile_rows, _lib.ptr(ws), _lib.stream_handle())
 
-        outs, m = self._run([rows], binner, rows.n, drop=True)
-        return rows.wrap(outs[0], m)
+        outs, m = self._run(fields, binner, n, drop=True)
+        return _results(fields, outs, m, multi)
 
-    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None, side_ids=None,
+    def _run(self, fields, binner, n, drop, row_bytes_hint=None, extra_rows=None, side=None,
              deferred=None):
-        """bin -> scan -> count exchange -> pack -> row exchange.  ``side_ids``:
-        field 1 is the rows' 2-byte side field (fine cells), packed by the
-        same kernel as field 0 (mgr_pack_ids).  ``deferred`` (a list): on one
-        rank without drops the counts are not read back; the scan's count
-        tensor is appended to it for the caller's next host read to check."""
+        """bin -> scan -> count exchange -> pack -> row exchange.  Every field
+        (the payload's SoA fields, positions, side fields) is partitioned by
+        the same destinations in one mgr_pack_fields call.  ``side``: the
+        index of the rows' 2-byte side field (fine cells, halo flags), moved
+        by the kernel that moves the other fields.  ``deferred`` (a
+        list): on one rank without drops the counts are not read back; the
+        scan's count tensor is appended to it for the caller's next host read
+        to check."""
         P = self.size
         nb = P + 1 if drop else P
         hint = row_bytes_hint or [f.row_bytes for f in fields]
-        tile_rows, ws, dest = _scratch(n, nb, max(max(hint), 1), self._dev, self._scratch)
+        tile_rows, ws, dest = _scratch(n, nb, _tile_hint(hint, side), self._dev,
+                                       self._scratch)
         binner(dest, tile_rows, ws)
         stream = _lib.stream_handle()
         bin_counts = torch.empty(nb, dtype=torch.int64, device=self._dev)
         _lib.call("mgr_scan", n, nb, tile_rows, _lib.ptr(ws), _lib.ptr(bin_counts), stream)
 
-        def red_ptr(out, off):
-            # address arithmetic, not a slice: an empty tail slice has no data pointer
-            return ctypes.c_void_p(out.data_ptr() + off if out is not None else 0)
+        # the rows' 2-byte side field travels inside the pack of the other
+        # fields (one ranking for all of them)
+        side_ids = side is not None
+        side_i = side if side_ids else -1
+        main = [f for f in range(len(fields)) if f != side_i]
 
-        def pack(f, snd, redirect_bin, out, out_offset):
-            fld = fields[f]
-            _lib.call("mgr_pack", _lib.ptr(fld.flat), fld.row_bytes, n, _lib.ptr(dest), nb,
-                      P if drop else -1, tile_rows, _lib.ptr(ws), _lib.ptr(snd), redirect_bin,
-                      red_ptr(out, out_offset), stream)
-
-        def pack_all(sends, outs, redirect_bin, offs):
+        def pack_fields(sends, outs, redirect_bin, offs, t0=0, t1=-1):
+            """Every field in ONE mgr_pack_fields call: one ranking of the
+            destinations for all of them (the multi-field kernel where the
+            fields allow); the redirect bin's rows straight into ``outs``."""
             r = redirect_bin >= 0
-            _lib.call("mgr_pack_ids", _lib.ptr(fields[0].flat), fields[0].row_bytes, n,
-                      _lib.ptr(dest), nb, P if drop else -1, tile_rows, _lib.ptr(ws),
-                      _lib.ptr(sends[0]), redirect_bin, red_ptr(outs[0] if r else None, offs[0]),
-                      _lib.ptr(fields[1].flat), _lib.ptr(sends[1]),
-                      red_ptr(outs[1] if r else None, offs[1]), stream)
-            for f in range(2, len(fields)):
-                pack(f, sends[f], redirect_bin, outs[f] if r else None, offs[f])
+            _lib.call("mgr_pack_fields", len(main),
+                      _ptrs([fields[f].flat.data_ptr() for f in main]),
+                      _i64s([fields[f].row_bytes for f in main]), n, _lib.ptr(dest), nb,
+                      P if drop else -1, tile_rows, _lib.ptr(ws),
+                      _ptrs([sends[f].data_ptr() for f in main]), redirect_bin,
+                      _ptrs([outs[f].data_ptr() + offs[f] for f in main]) if r else None,
+                      _lib.ptr(fields[side_i].flat) if side_ids else None,
+                      _lib.ptr(sends[side_i]) if side_ids else None,
+                      ctypes.c_void_p(outs[side_i].data_ptr() + offs[side_i])
+                      if side_ids and r else None, t0, t1, stream)
 
         T = (n + tile_rows - 1) // tile_rows
         # the chunk count is part of the exchange protocol: the same on every
@@ -686,21 +771,7 @@ class MPIGridRedistributor:
                 return out.view(k + 1, nb)[:, :P]   # device: read with the count message
 
             def pack_chunk(c, sends, outs, redirect_bin, offs):
-                t0, t1 = bounds[c], bounds[c + 1]
-                first = 0
-                if side_ids:   # field 1: the 2-byte side field of field 0, same pass
-                    _lib.call("mgr_pack_tiles", _lib.ptr(fields[0].flat), fields[0].row_bytes, n,
-                              _lib.ptr(dest), nb, P if drop else -1, tile_rows, _lib.ptr(ws),
-                              _lib.ptr(sends[0]), redirect_bin, red_ptr(outs[0], offs[0]),
-                              _lib.ptr(fields[1].flat), _lib.ptr(sends[1]),
-                              red_ptr(outs[1], offs[1]), t0, t1, stream)
-                    first = 2
-                for f in range(first, len(fields)):
-                    fld = fields[f]
-                    _lib.call("mgr_pack_tiles", _lib.ptr(fld.flat), fld.row_bytes, n,
-                              _lib.ptr(dest), nb, P if drop else -1, tile_rows, _lib.ptr(ws),
-                              _lib.ptr(sends[f]), redirect_bin, red_ptr(outs[f], offs[f]),
-                              None, None, None, t0, t1, stream)
+                pack_fields(sends, outs, redirect_bin, offs, bounds[c], bounds[c + 1])
 
             outs, lay = exchange_pipelined(self.comm, [f.row_bytes for f in fields],
                                            bin_counts[:P], self.rank, self._dev, chunk_offsets,
@@ -720,8 +791,8 @@ class MPIGridRedistributor:
             else:
                 read = host_read_start([bin_counts])
         outs, lay = exchange(self.comm, [f.row_bytes for f in fields], bin_counts[:P], self.rank,
-                             self._dev, pack, extra_rows=extra_rows, scratch=self._scratch.get,
-                             pack_all=pack_all if side_ids else None, known_rows=known)
+                             self._dev, None, extra_rows=extra_rows, scratch=self._scratch.get,
+                             pack_all=pack_fields, known_rows=known)
         if read is not None:
             check_counts(host_read_wait(read)[0], [])
         self._last_layout = lay
@@ -791,6 +862,7 @@ class GridPartitioner:
         self._cache = {}
         self._fine_plans = {}
         self._fine_buf = None
+        self.last_counts = None
 
     def set_write_back(self, mode):
         """"changed" (default) / "all": MPIGridRedistributor.set_write_back."""
@@ -817,6 +889,7 @@ class GridPartitioner:
         (out_flat, fine_ids_out, bin_counts)."""
         n = int(pos_tensor.shape[0])
         tile_rows, ws, dest, out, counts = self.buffers(n, row_bytes)
+        self.last_counts = counts   # device bin counts of the last device call
         code = pos_code(pos_tensor.dtype)
         s = _lib.stream_handle(stream)
         if fine_cells is None:
@@ -824,11 +897,7 @@ class GridPartitioner:
                       pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(data_flat), row_bytes,
                       _lib.ptr(out), _lib.ptr(dest), _lib.ptr(counts), tile_rows, _lib.ptr(ws), s)
             return out, counts
-        key = tuple(int(x) for x in fine_cells)
-        if key not in self._fine_plans:
-            self._fine_plans[key] = _Plan(self.grid_topology, self.box_length, 0,
-                                          fine=np.array(key))
-        fplan = self._fine_plans[key]
+        fplan = self._fine_plan(fine_cells)
         fid, fid_out = self.fine_buffers(n)
         _lib.call("mgr_bin_count_fine", self._plan.h, fplan.h, _lib.ptr(pos_tensor), code, n,
                   pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(dest), _lib.ptr(fid),
@@ -845,32 +914,87 @@ class GridPartitioner:
                                    for _ in range(2))
         return self._fine_buf
 
+    def partition_fields_device(self, flats, row_bytes, pos_tensor, periodic=True, stream=None,
+                                fine_cells=None):
+        """partition_device of a SoA payload: ``flats`` (uint8 device tensors
+        of n * row_bytes[f] bytes each, e.g. positions, velocities, masses,
+        ids) partitioned by ONE binning of ``pos_tensor`` (wrapped in place;
+        it may itself be one of the fields' arrays) and one mgr_pack_fields
+        launch.  Returns ([out_flat per field], bin_counts) device tensors, or
+        with ``fine_cells`` ([out_flat ...], fine_ids_out, bin_counts)."""
+        n = int(pos_tensor.shape[0])
+        nf = len(flats)
+        hint = _tile_hint(list(row_bytes))
+        key = ("fields", n, tuple(int(b) for b in row_bytes))
+        if key not in self._cache:
+            tile_rows, ws, dest = _scratch(n, self.nbins, hint, self._dev)
+            outs = [torch.empty(max(n * int(b), 1), dtype=torch.uint8, device=self._dev)
+                    for b in row_bytes]
+            counts = torch.empty(self.nbins, dtype=torch.int64, device=self._dev)
+            self._cache = {key: (tile_rows, ws, dest, outs, counts)}
+        tile_rows, ws, dest, outs, counts = self._cache[key]
+        self.last_counts = counts
+        code = pos_code(pos_tensor.dtype)
+        s = _lib.stream_handle(stream)
+        fid = fid_out = None
+        if fine_cells is None:
+            _lib.call("mgr_bin_count", self._plan.h, _lib.ptr(pos_tensor), code, n,
+                      pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(dest), tile_rows,
+                      _lib.ptr(ws), s)
+        else:
+            fplan = self._fine_plan(fine_cells)
+            fid, fid_out = self.fine_buffers(n)
+            _lib.call("mgr_bin_count_fine", self._plan.h, fplan.h, _lib.ptr(pos_tensor), code, n,
+                      pos_tensor.stride(0), int(bool(periodic)), _lib.ptr(dest), _lib.ptr(fid),
+                      tile_rows, _lib.ptr(ws), s)
+        _lib.call("mgr_scan", n, self.nbins, tile_rows, _lib.ptr(ws), _lib.ptr(counts), s)
+        _lib.call("mgr_pack_fields", nf, _ptrs([f.data_ptr() for f in flats]), _i64s(row_bytes),
+                  n, _lib.ptr(dest), self.nbins, -1, tile_rows, _lib.ptr(ws),
+                  _ptrs([o.data_ptr() for o in outs]), -1, None, _lib.ptr(fid),
+                  _lib.ptr(fid_out), None, 0, -1, s)
+        if fine_cells is None:
+            return outs, counts
+        return outs, fid_out.view(torch.int16)[:n], counts
+
+    def _fine_plan(self, fine_cells):
+        key = tuple(int(x) for x in fine_cells)
+        if key not in self._fine_plans:
+            self._fine_plans[key] = _Plan(self.grid_topology, self.box_length, 0,
+                                          fine=np.array(key))
+        return self._fine_plans[key]
+
     def partition_by_position(self, data, position, periodic=True):
         """Arrays in, (partitioned data, offsets[nbins+1]) out; position
-        wrapped in place (S1).  Same container types as the inputs."""
-        rows = Rows(data, self._dev)
-        pos = Positions(position, self.dim, self._dev, data_rows=rows)
-        if pos.n != rows.n:
+        wrapped in place (S1).  Same container types as the inputs.  ``data``:
+        one array, or a tuple / list of arrays sharing axis 0 (SoA: every
+        field partitioned by the same destinations in one pack; the result is
+        then a tuple in the same order)."""
+        fields, multi = _payload(data, self._dev)
+        pos = Positions(position, self.dim, self._dev, data_rows=_alias_rows(position, fields))
+        n = fields[0].n
+        if pos.n != n:
             raise ValueError("data and position row counts differ")
-        n, rb = rows.n, rows.row_bytes
-        tile_rows, ws, dest = _scratch(n, self.nbins, rb, self._dev)
+        rbs = [f.row_bytes for f in fields]
+        tile_rows, ws, dest = _scratch(n, self.nbins, _tile_hint(rbs), self._dev)
         stream = _lib.stream_handle()
         counts = torch.empty(self.nbins, dtype=torch.int64, device=self._dev)
         _lib.call("mgr_bin_count", self._plan.h, ctypes.c_void_p(pos.addr), pos.code, n,
                   pos.stride, int(bool(periodic)), _lib.ptr(dest), tile_rows, _lib.ptr(ws), stream)
         pos.finish()
         _lib.call("mgr_scan", n, self.nbins, tile_rows, _lib.ptr(ws), _lib.ptr(counts), stream)
-        out = torch.empty(max(n * rb, 1), dtype=torch.uint8, device=self._dev)
-        _lib.call("mgr_pack", _lib.ptr(rows.flat), rb, n, _lib.ptr(dest), self.nbins, -1,
-                  tile_rows, _lib.ptr(ws), _lib.ptr(out), -1, None, stream)
+        outs = [torch.empty(max(n * rb, 1), dtype=torch.uint8, device=self._dev) for rb in rbs]
+        _lib.call("mgr_pack_fields", len(fields), _ptrs([f.flat.data_ptr() for f in fields]),
+                  _i64s(rbs), n, _lib.ptr(dest), self.nbins, -1, tile_rows, _lib.ptr(ws),
+                  _ptrs([o.data_ptr() for o in outs]), -1, None, None, None, None, 0, -1, stream)
         offsets = torch.zeros(self.nbins + 1, dtype=torch.int64, device=self._dev)
         offsets[1:] = torch.cumsum(counts, 0)
-        if isinstance(data, torch.Tensor) and data.is_cuda:
+        first = fields[0].obj
+        if isinstance(first, torch.Tensor) and first.is_cuda:
             # device results stay asynchronous: a failed scan shows as -1 counts
-            return rows.wrap(out, n), offsets
+            return _results(fields, outs, n, multi), offsets
         check_counts(counts.cpu().numpy(), [])   # a failed scan reports -1 counts
-        res = rows.wrap(out, n)
-        if isinstance(data, torch.Tensor):
+        res = _results(fields, outs, n, multi)
+        if isinstance(first, torch.Tensor):
             return res, offsets.cpu()
         return res, offsets.cpu().numpy()
 

@@ -43,7 +43,8 @@ def lib():
         L.oracle_trunc_i64.argtypes = [ctypes.c_double]
         L.oracle_trunc_i64.restype = ctypes.c_int64
         L.oracle_local_partition_omp.argtypes = [_P, _I64, _I64, ctypes.c_int, _P, _P,
-                                                 ctypes.c_int, _P, _I64, _P, _P, ctypes.c_int]
+                                                 ctypes.c_int, _P, _I64, _P, _P, ctypes.c_int,
+                                                 _P, _P]
         L.oracle_local_partition_omp.restype = _I64
         L.oracle_bin_ext.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, _I64,
                                      ctypes.c_int, _P, _P, ctypes.c_int, _P, _P]
@@ -72,6 +73,10 @@ def bin_positions(position, grid_topology, box_length, periodic=True, compute_f3
     """Bin ``position`` ((N, >=dim) float32/float64, C-contiguous rows) in place.
 
     Returns int64 cell ids (and per-dim indexes when ``want_idx``)."""
+    if position.ndim == 2 and position.shape[0] == 0:   # an empty rank (numpy strides 0)
+        cell = np.empty(0, dtype=np.int64)
+        idx = np.empty((0, len(grid_topology)), dtype=np.int64)
+        return (cell, idx) if want_idx else cell
     assert position.ndim == 2 and position.strides[1] == position.itemsize
     topo = np.ascontiguousarray(np.asarray(grid_topology).astype(np.int64))
     box_arr = np.asarray(box_length)
@@ -116,11 +121,19 @@ def partition(data, dest, nbins):
     return out[:total], offsets
 
 
+def local_partition_workspace(n, nbins, threads):
+    """Scratch of local_partition_omp (destinations, per-thread bin starts),
+    allocated and touched once, outside any timed call."""
+    ws = (np.zeros(max(int(n), 1), dtype=np.int32), np.zeros(int(threads) * int(nbins), np.int64))
+    return ws
+
+
 def local_partition_omp(position, data, grid_topology, box_length, periodic=True, threads=1,
-                        out=None):
+                        out=None, workspace=None):
     """Threaded host restatement of the local stage (wrap + bin of f64
     positions in place, stable partition of ``data`` rows): the optimised
-    CPU comparison point of bench.py.  Returns (out, offsets)."""
+    CPU comparison point of bench.py.  ``workspace``: local_partition_workspace
+    (else allocated inside the call).  Returns (out, offsets)."""
     assert position.dtype == np.float64 and position.strides[1] == 8
     topo = np.ascontiguousarray(np.asarray(grid_topology).astype(np.int64))
     box = np.ascontiguousarray(np.asarray(box_length, dtype=np.float64))
@@ -132,7 +145,9 @@ def local_partition_omp(position, data, grid_topology, box_length, periodic=True
     offsets = np.zeros(int(np.prod(topo)) + 1, dtype=np.int64)
     lib().oracle_local_partition_omp(_ptr(position), n, position.strides[0] // 8, len(topo),
                                      _ptr(box), _ptr(topo), int(bool(periodic)), _ptr(data),
-                                     row_bytes, _ptr(out), _ptr(offsets), int(threads))
+                                     row_bytes, _ptr(out), _ptr(offsets), int(threads),
+                                     _ptr(workspace[0]) if workspace else None,
+                                     _ptr(workspace[1]) if workspace else None)
     return out, offsets
 
 

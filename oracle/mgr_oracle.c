@@ -344,19 +344,24 @@ void oracle_bin_ext(void* pos, int pos_dtype, int wmode, int dmode, int64_t n, i
  * thread bins a contiguous chunk and counts its bins, the per-(thread, bin)
  * starts follow in (bin, thread) order, and every thread scatters its own
  * chunk -- the same result as oracle_bin + oracle_partition.  Returns rows
- * written; offsets[nbins+1].
+ * written; offsets[nbins+1].  dest_ws (int32 [n]) and start_ws (int64
+ * [nthreads * nbins]): caller-owned scratch, so a timed call allocates and
+ * first-touches nothing (NULL: allocated here).
  */
 int64_t oracle_local_partition_omp(double* pos, int64_t n, int64_t row_stride, int dim,
                                    const double* box, const int64_t* topo, int periodic,
                                    const void* data, int64_t row_bytes, void* out,
-                                   int64_t* offsets, int nthreads) {
+                                   int64_t* offsets, int nthreads, int32_t* dest_ws,
+                                   int64_t* start_ws) {
     int64_t offset[64];
     int64_t off = 1;
     for (int d = dim - 1; d >= 0; --d) { offset[d] = off; off *= topo[d]; }
     const int64_t nbins = off;
     if (nthreads < 1) nthreads = 1;
-    int32_t* dest = (int32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
-    int64_t* start = (int64_t*)calloc((size_t)nthreads * (size_t)nbins, sizeof(int64_t));
+    int32_t* dest = dest_ws ? dest_ws : (int32_t*)malloc((size_t)(n > 0 ? n : 1) * sizeof(int32_t));
+    int64_t* start = start_ws ? start_ws
+                              : (int64_t*)malloc((size_t)nthreads * (size_t)nbins * sizeof(int64_t));
+    memset(start, 0, (size_t)nthreads * (size_t)nbins * sizeof(int64_t));
     const char* src = (const char*)data;
     char* dst = (char*)out;
     int fast = 1;   /* the in-box fast wrap needs L > 0 with 2L finite */
@@ -400,8 +405,8 @@ int64_t oracle_local_partition_omp(double* pos, int64_t n, int64_t row_stride, i
         }
     }
     const int64_t total = offsets[nbins];
-    free(start);
-    free(dest);
+    if (!start_ws) free(start);
+    if (!dest_ws) free(dest);
     return total;
 }
 

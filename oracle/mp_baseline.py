@@ -78,6 +78,8 @@ def run(size=8, n_per_rank=1 << 21, iters=3, topo=(2, 2, 2), box=(1.0, 1.0, 1.0)
     for p in procs:
         p.join(timeout=60)
     per_iter = np.max(np.array([t for _, t in sorted(res)]), axis=0)  # slowest rank
-    best = float(per_iter.min())
-    return {"value": size * n_per_rank / best, "seconds": per_iter.tolist(), "ranks": size,
-            "n_per_rank": n_per_rank}
+    med = float(np.median(per_iter))
+    return {"value": size * n_per_rank / med, "seconds": per_iter.tolist(), "ranks": size,
+            "n_per_rank": n_per_rank, "stat": "median",
+            "spread": [size * n_per_rank / float(per_iter.max()),
+                       size * n_per_rank / float(per_iter.min())]}

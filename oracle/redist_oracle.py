@@ -177,6 +177,35 @@ def redistribute_by_cell_number_all_ranks(size, data_list, ids_list):
     return alltoall_concat([stable_split(d, i, size) for d, i in zip(data_list, ids_list)])
 
 
+def redistribute_fields_by_position_all_ranks(grid_topology, box_length, size, fields_list,
+                                              pos_list, periodic=True):
+    """SoA redistribution -- several arrays sharing axis 0 -- by the
+    reference's own multi-field pattern (redist.py:157-164): ONE binning of
+    the positions per rank (:157, wrapping ``pos_list[r]`` in place, S1), then
+    every field split with that same ``rank_to_send`` (:160 for ``data``,
+    :164 for ``position``; :195-198) and exchanged (:199).  A field that IS
+    ``pos_list[r]`` moves its wrapped values.  Returns per-rank lists of the
+    fields' outputs (S7 order)."""
+    nf = len(fields_list[0]) if fields_list else 0
+    sends = [[] for _ in range(nf)]
+    for r in range(size):
+        geo = Geometry(grid_topology, box_length, size, r)
+        dest = cell_number_from_position(geo, pos_list[r], periodic=periodic)
+        for i in range(nf):
+            sends[i].append(stable_split(fields_list[r][i], dest, size))
+    per_field = [alltoall_concat(sends[i]) for i in range(nf)]
+    return [[per_field[i][r] for i in range(nf)] for r in range(size)]
+
+
+def redistribute_fields_by_cell_number_all_ranks(size, fields_list, ids_list):
+    """``redistribute_by_cell_number`` (redist.py:169-200) of every field of a
+    SoA payload with the same ids, for every rank: per-rank lists."""
+    nf = len(fields_list[0]) if fields_list else 0
+    per_field = [redistribute_by_cell_number_all_ranks(size, [f[i] for f in fields_list], ids_list)
+                 for i in range(nf)]
+    return [[per_field[i][r] for i in range(nf)] for r in range(size)]
+
+
 # ------------------------------------------------------- position helpers
 def stack_position(columns):
     """``stack_position`` (redist.py:311-312): d columns of N -> (N, d),

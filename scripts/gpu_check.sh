@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU check: smoke, then the named tests first (new this round), then
+# GPU check: smoke, then the named tests first (new this round), then
 # the whole -m gpu suite.  Stops at the first failing step.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1

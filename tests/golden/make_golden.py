@@ -2,7 +2,7 @@
 """Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
 
 Run in the survey container only (needs /root/reference, never on the GPU
-box):   python tests/golden/make_golden.py [all|redist|halo|fine]
+box):   python tests/golden/make_golden.py [all|redist|halo|fine|dtypes|dtype_edges|soa]
 
 How the reference is run (SURVEY.md §8c recipe; nothing is copied):
   * stub ``mpi4py`` / ``mpi4py.MPI`` modules are placed in ``sys.modules``
@@ -26,7 +26,11 @@ import os
 import sys
 import types
 
-import numpy as np
+# the reference is imported read-only: no bytecode cache is written next to
+# /root/reference/redist.py (nothing under /root/reference is created)
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
 
 REF_PATH = "/root/reference/redist.py"
 OUT_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -493,6 +497,48 @@ def make_bin_dtypes(ref, rng):
     return len(out)
 
 
+def make_bin_dtype_edges(ref, rng):
+    """Degenerate boxes for every non-float64 position dtype: float boxes 0,
+    negative and +-inf (the float wrap gives NaN / out-of-range values that
+    numpy's x86 casts write back into integer columns: cvttsd2si's INT_MIN,
+    then the low bits), integer boxes 0 and negative (x % 0 == 0; floor-mod
+    by a negative divisor), a float16 box 0 -- single-rank binning, n = 3."""
+    out = {}
+    boxes = {"f64_zero": [0.0], "f64_neg": [-2.5], "f64_inf": [np.inf], "f64_ninf": [-np.inf],
+             "f32_inf": np.array([np.inf], np.float32), "int_zero": [0], "int_neg": [-3],
+             "f16_zero": np.array([0.0], np.float16)}
+    pdts = {"i8": np.int8, "i16": np.int16, "i32": np.int32, "i64": np.int64, "u8": np.uint8,
+            "u16": np.uint16, "u32": np.uint32, "u64": np.uint64, "b1": np.bool_,
+            "f16": np.float16, "f32": np.float32}
+    n = 3
+    for pname, pdt in pdts.items():
+        for bname, box in boxes.items():
+            for periodic in (True, False):
+                with np.errstate(all="ignore"):
+                    if np.dtype(pdt).kind in "iub":
+                        vals = int_edge_values(3, rng, pdt)
+                    elif pdt == np.float16:
+                        vals = f16_edge_values(3.0, rng)
+                    else:
+                        vals = edge_values(3.0, rng).astype(np.float32)
+                pos = vals.reshape(-1, 1)
+                pos_in = pos.copy()
+                R = ref.MPIGridRedistributor(SingleComm(n), [n], box)
+                p2 = pos.copy()
+                with np.errstate(all="ignore"):
+                    idx = R.get_cell_indexes_from_position(p2, periodic=periodic)
+                    cell = R.get_cell_number_from_position(pos, periodic=periodic)
+                key = f"e_{pname}_box{bname}" + ("" if periodic else "_nonperiodic")
+                out[key + "_L"] = np.asarray(box)
+                out[key + "_n"] = np.int64(n)
+                out[key + "_pos_in"] = pos_in
+                out[key + "_pos_out"] = pos
+                out[key + "_idx"] = idx
+                out[key + "_cell"] = cell
+    np.savez_compressed(os.path.join(OUT_DIR, "bin_dtype_edges.npz"), **out)
+    return len(out)
+
+
 DTYPE_CASES = [
     # name, topology, box, pos dtype, position range (in box units)
     ("p4_2d_i32pos_intbox", [2, 2], [100, 60], np.int32, (-1.5, 2.5)),
@@ -578,6 +624,114 @@ def make_dtypes(ref, rng):
     return n_files + 1
 
 
+SOA_CASES = [
+    # name, topology, box, pos dtype, periodic, fields (pos = the position
+    # array itself moves as field 0), empty ranks
+    ("p8_cfg5_soa", [2, 2, 2], [1.0, 1.0, 1.0], np.float32, True,
+     ["pos", "vel_f32x3", "mass_f32", "id_i64"], ()),
+    ("p4_f64_two_fields_empty", [2, 2, 1], [1.0, 2.0, 1.0], np.float64, True,
+     ["id_i64", "mat_f64x3"], (2,)),
+    ("p6_321_nonperiodic_mixed", [3, 2, 1], [3.0, 2.0, 1.5], np.float64, False,
+     ["pos", "vel_f32x3", "id_i32", "flag_u8", "tri_i16x3", "rec32"], ()),
+    ("p2_f32_intbox_three", [2, 1, 1], [4, 2, 2], np.float32, True,
+     ["mass_f32", "pos", "id_i64"], (1,)),
+]
+
+
+def soa_field(kind, pos, rng, gid0):
+    n = len(pos)
+    if kind == "pos":
+        return pos
+    if kind == "vel_f32x3":
+        return rng.normal(size=(n, 3)).astype(np.float32)
+    if kind == "mass_f32":
+        return rng.uniform(1, 2, n).astype(np.float32)
+    if kind == "id_i64":
+        return np.arange(gid0, gid0 + n, dtype=np.int64)
+    if kind == "id_i32":
+        return np.arange(gid0, gid0 + n, dtype=np.int32)
+    if kind == "mat_f64x3":
+        return rng.normal(size=(n, 3))
+    if kind == "flag_u8":
+        return rng.integers(0, 256, n).astype(np.uint8)
+    if kind == "tri_i16x3":
+        return rng.integers(-30000, 30000, (n, 3)).astype(np.int16)
+    if kind == "rec32":
+        return rec32(pos.astype(np.float64), gid0)
+    raise ValueError(kind)
+
+
+def make_soa(ref, rng):
+    """SoA payloads -- several arrays sharing axis 0 -- through the
+    REFERENCE's own multi-field pattern (redist.py:157-164): the destinations
+    are binned ONCE from the positions (get_cell_number_from_position, which
+    wraps them in place, :157), then every field is redistributed with that
+    same rank_to_send (redistribute_by_cell_number, :160 for data, :164 for
+    position).  A field named "pos" is the position array itself (its
+    wrapped values travel).  Plus a caller-ids case (:169-200, out-of-range
+    ids dropped) with three fields."""
+    n_files = 0
+    for name, topo, box, pdt, periodic, kinds, empty in SOA_CASES:
+        size = int(np.prod(topo))
+        pos_in, fields_in = [], []
+        gid = 0
+        for r in range(size):
+            n = 0 if r in empty else int(rng.integers(60, 400))
+            p = positions(rng, n, len(topo), box, dtype=pdt)
+            pos_in.append(p)
+            fields_in.append([soa_field(k, p, rng, gid) for k in kinds])
+            gid += n
+        pos_work = [p.copy() for p in pos_in]
+        work = [[pos_work[r] if k == "pos" else f for k, f in zip(kinds, fields_in[r])]
+                for r in range(size)]
+
+        def fn(comm, r):
+            R = ref.MPIGridRedistributor(comm, topo, box)
+            with np.errstate(all="ignore"):
+                rank_to_send = R.get_cell_number_from_position(pos_work[r], periodic=periodic)
+                return rank_to_send, [R.redistribute_by_cell_number(f, rank_to_send)
+                                      for f in work[r]]
+
+        res = run_ranks(size, fn)
+        f = {"topology": np.asarray(topo, dtype=np.int64), "box": np.asarray(box),
+             "size": np.int64(size), "periodic": np.bool_(periodic),
+             "nfields": np.int64(len(kinds)),
+             "pos_field": np.int64(kinds.index("pos") if "pos" in kinds else -1)}
+        for r in range(size):
+            f[f"r{r}_pos_in"] = pos_in[r]
+            f[f"r{r}_pos_out"] = pos_work[r]
+            f[f"r{r}_cell"] = res[r][0]
+            for i in range(len(kinds)):
+                f[f"r{r}_f{i}_in"] = fields_in[r][i] if kinds[i] != "pos" else pos_in[r]
+                f[f"r{r}_f{i}_out"] = res[r][1][i]
+        np.savez_compressed(os.path.join(OUT_DIR, f"soa_{name}.npz"), **f)
+        n_files += 1
+
+    # caller ids (redistribute_by_cell_number), three fields, ids out of range
+    size = 5
+    ids_in, fields_in = [], []
+    for r in range(size):
+        n = 0 if r == 3 else int(rng.integers(30, 300))
+        ids_in.append(rng.integers(-2, size + 3, n).astype(np.int64))
+        fields_in.append([rng.normal(size=(n, 3)).astype(np.float32),
+                          np.arange(n, dtype=np.int64) + 1000 * r,
+                          rng.integers(0, 1 << 16, n).astype(np.uint16)])
+
+    def fn2(comm, r):
+        R = ref.MPIGridRedistributor(comm, [size], [1.0])
+        return [R.redistribute_by_cell_number(x, ids_in[r]) for x in fields_in[r]]
+
+    res = run_ranks(size, fn2)
+    f = {"size": np.int64(size), "nfields": np.int64(3)}
+    for r in range(size):
+        f[f"r{r}_ids"] = ids_in[r]
+        for i in range(3):
+            f[f"r{r}_f{i}_in"] = fields_in[r][i]
+            f[f"r{r}_f{i}_out"] = res[r][i]
+    np.savez_compressed(os.path.join(OUT_DIR, "soa_cellnum_p5_three.npz"), **f)
+    return n_files + 1
+
+
 def main():
     ref = load_reference()
     only = sys.argv[1] if len(sys.argv) > 1 else "all"
@@ -595,6 +749,12 @@ def main():
     if only in ("all", "fine"):
         e = make_fine(ref, np.random.default_rng(20261017))
         print(f"fine-cell fixtures: {e}")
+    if only in ("all", "dtype_edges"):
+        k = make_bin_dtype_edges(ref, np.random.default_rng(20261020))
+        print(f"degenerate-box dtype arrays: {k}")
+    if only in ("all", "soa"):
+        g = make_soa(ref, np.random.default_rng(20261019))
+        print(f"SoA fixtures: {g}")
 
 
 if __name__ == "__main__":

@@ -25,6 +25,37 @@ def halo_direct_cases():
     return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "halo_direct_*.npz")))
 
 
+def soa_cases():
+    """SoA fixtures of the position path (make_golden.py make_soa)."""
+    return sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "soa_p*.npz")))
+
+
+def soa_inputs(f, size, as_torch=False):
+    """Per-rank (fields, position) of a soa_* fixture: numpy copies, or GPU
+    torch tensors; the field at ``pos_field`` is the position array itself
+    (the same object / tensor, so its wrapped values travel)."""
+    nf, pf = int(f["nfields"]), int(f["pos_field"])
+    fields, pos = [], []
+    for r in range(size):
+        p = f[f"r{r}_pos_in"].copy()
+        fl = [p if i == pf else f[f"r{r}_f{i}_in"].copy() for i in range(nf)]
+        if as_torch:
+            import torch
+            tp = torch.from_numpy(p).cuda()
+            tl = []
+            for i, x in enumerate(fl):
+                if i == pf:
+                    tl.append(tp)
+                    continue
+                if x.dtype.names:
+                    x = x.view(np.uint8).reshape(len(x), -1)
+                tl.append(torch.from_numpy(np.ascontiguousarray(x)).cuda())
+            fl, p = tl, tp
+        fields.append(fl)
+        pos.append(p)
+    return fields, pos
+
+
 def fixture_inputs(f, case, size, as_torch):
     """Per-rank (data, position) inputs of a redist_* fixture: numpy copies, or
     GPU torch tensors with the same aliasing (position = data, or a view of

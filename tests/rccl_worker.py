@@ -164,6 +164,67 @@ def case_fine_fused(mgr, comm, fine, seed):
 REC36 = np.dtype([("pos", "f4", 3), ("vel", "f4", 3), ("mass", "f4"), ("id", "i8")])
 
 
+def case_soa_golden(mgr, comm, name, as_torch):
+    """SoA payload (several arrays) against the reference's multi-field
+    pattern (make_golden.py make_soa: one binning, every field redistributed
+    with the same destinations, redist.py:157-164)."""
+    f = G.load(name)
+    fields, pos = G.soa_inputs(f, WORLD, as_torch)
+    R = mgr.MPIGridRedistributor(comm, f["topology"], f["box"])
+    out = R.redistribute_by_position(tuple(fields[RANK]), pos[RANK], periodic=bool(f["periodic"]))
+    torch.cuda.synchronize()
+    assert np.array_equal(as_bytes(pos[RANK]), as_bytes(f[f"r{RANK}_pos_out"])), "positions"
+    for i in range(int(f["nfields"])):
+        assert np.array_equal(as_bytes(out[i]), as_bytes(f[f"r{RANK}_f{i}_out"])), f"field {i}"
+
+
+def soa_inputs(seed, sizes):
+    """Config 5's fields as four arrays per rank: pos f32 x3 (the position
+    array itself), vel f32 x3, mass f32, id i64."""
+    out = []
+    for r, n in enumerate(sizes):
+        rng = np.random.default_rng(seed + r)
+        out.append([rng.uniform(-0.5, 1.5, (n, 3)).astype(np.float32),
+                    rng.normal(size=(n, 3)).astype(np.float32),
+                    rng.uniform(1, 2, n).astype(np.float32),
+                    np.arange(n, dtype=np.int64) + 1_000_000 * r])
+    return out
+
+
+def case_soa_random(mgr, comm, seed, as_torch, chunks=1, fine=None):
+    """SoA redistribution over RCCL (one count exchange, one RCCL group with a
+    send per field and peer; pipelined when chunks > 1), skewed sizes with an
+    empty rank, optionally with fine cells -- against the oracle's per-field
+    restatement of redist.py:157-164 (+ fine_cell_ids and a stable sort)."""
+    topo = TOPO[WORLD]
+    sizes = [int(np.random.default_rng(seed + 7 * r).integers(2_000, 50_000)) for r in range(WORLD)]
+    sizes[WORLD // 2] = 0
+    fields = soa_inputs(seed, sizes)
+    ofields = [[x.copy() for x in fl] for fl in fields]
+    exp = ro.redistribute_fields_by_position_all_ranks(topo, BOX, WORLD, ofields,
+                                                       [fl[0] for fl in ofields])[RANK]
+    mine = fields[RANK]
+    if as_torch:
+        mine = [torch.from_numpy(x).cuda() for x in mine]
+    R = mgr.MPIGridRedistributor(comm, topo, BOX)
+    R.exchange_chunks = chunks
+    if fine is None:
+        out = R.redistribute_by_position(tuple(mine), mine[0])
+        torch.cuda.synchronize()
+        for i in range(4):
+            assert np.array_equal(as_bytes(out[i]), as_bytes(exp[i])), f"field {i}"
+    else:
+        out, off = R.redistribute_by_position(mine, mine[0], fine_cells=fine)
+        torch.cuda.synchronize()
+        fid = ro.fine_cell_ids(topo, fine, BOX, exp[0])
+        order = np.argsort(fid, kind="stable")
+        for i in range(4):
+            assert np.array_equal(as_bytes(out[i]), as_bytes(exp[i][order])), f"fine field {i}"
+        assert np.array_equal(np.diff(np.asarray(off.cpu() if hasattr(off, "cpu") else off)),
+                              np.bincount(fid, minlength=int(np.prod(fine)))), "fine offsets"
+    assert np.array_equal(as_bytes(mine[0]), as_bytes(ofields[RANK][0])), "wrapped positions"
+
+
 def case_fine_rec36(mgr, comm, fine, seed, as_torch, chunks=1):
     """BASELINE config 5's exact layout over RCCL: 36-byte records (f32 pos +
     vel + mass + i64 id), the position the f32 view into the record (the
@@ -407,6 +468,11 @@ def _parity_cases(mgr, comm):
             for as_torch in (False, True):
                 cases.append((f"{name}[torch={as_torch}]",
                               lambda n=name, t=as_torch: case_redist_golden(mgr, comm, n, t)))
+    for name in G.soa_cases():
+        if int(G.load(name)["size"]) == WORLD:
+            for as_torch in (False, True):
+                cases.append((f"{name}[torch={as_torch}]",
+                              lambda n=name, t=as_torch: case_soa_golden(mgr, comm, n, t)))
     for name in G.halo_cases():
         if int(G.load(name)["size"]) == WORLD:
             for as_torch in (False, True):
@@ -441,6 +507,11 @@ def _parity_cases(mgr, comm):
                                                              chunks=3)),
             ("pipelined_halo", lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], True, 55,
                                                         chunks=3)),
+            ("soa_random", lambda: case_soa_random(mgr, comm, 71, False)),
+            ("soa_random_torch_pipelined", lambda: case_soa_random(mgr, comm, 72, True, chunks=3)),
+            ("soa_fine_888", lambda: case_soa_random(mgr, comm, 73, True, fine=[8, 8, 8])),
+            ("soa_fine_888_pipelined",
+             lambda: case_soa_random(mgr, comm, 74, False, chunks=4, fine=[8, 8, 8])),
             ("clustered_empty_rank", lambda: case_clustered(mgr, comm, 41, False)),
             ("clustered_torch", lambda: case_clustered(mgr, comm, 42, True)),
             ("halo_random", lambda: case_halo_random(mgr, comm, [0.06, 0.1, 0.04], False, 23)),

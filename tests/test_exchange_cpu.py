@@ -487,7 +487,16 @@ def test_rccl_runtime_version_is_the_loaded_library():
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                             "include", "mgr.h")).read()
     assert "mgr_rccl_version" in hdr
-    assert compiled == 22707                      # /opt/rocm/include/rccl/rccl.h NCCL_VERSION_CODE
+    # the version code of the rccl.h libmgr.so was built against (csrc/Makefile:
+    # $(ROCM)/include), parsed from that header rather than hard-coded
+    import re
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    with open(os.path.join(rocm, "include", "rccl", "rccl.h")) as fh:
+        txt = fh.read()
+    ver = {k: int(re.search(rf"#define NCCL_{k}\s+(\d+)", txt).group(1))
+           for k in ("MAJOR", "MINOR", "PATCH")}
+    want = ver["MAJOR"] * 10000 + ver["MINOR"] * 100 + ver["PATCH"]
+    assert compiled == want, (compiled, want)
     path = loaded_rccl_path()
     assert path is not None
     v = ctypes.c_int(0)
@@ -501,6 +510,7 @@ def test_bench_cpu_baseline_record():
     the oracle's 8-process numpy restatement of redist.py:157-199."""
     import bench
     r = bench.cpu_baseline(n_per_rank=4096)
-    assert set(r) == {"value", "unit", "cores", "kind", "sample"}
+    assert set(r) == {"value", "unit", "cores", "kind", "sample", "stat", "spread"}
+    assert r["stat"] == "median" and r["spread"][0] <= r["value"] <= r["spread"][1]
     assert r["value"] > 0 and r["unit"] == "particles/s" and r["kind"] == "port"
     assert r["cores"] >= 1 and "4096 uniform particles" in r["sample"]

@@ -212,28 +212,19 @@ def test_single_rank_scan_failure_raises():
         _lib.test_hook("scan_spins", 1 << 24)
 
 
-def test_single_rank_position_scan_failure_raises():
+@pytest.mark.parametrize("n", [1, 1 << 22])
+def test_single_rank_position_scan_failure_raises(n):
     """One rank keeping every row: the pack is launched without a count read
     (the output holds n rows); the counts, read behind the pack, still raise.
-    One bin has no bin-end words to poll, so the give-up (scan_spins = -1)
-    needs several chunks (scan_chunk = 256 tiles) and a look-back or done
-    count not yet published: a run either raises or is exact, and some run
-    of a few raises."""
-    pos, rec = mgr.synth_uniform(1 << 22, seed=7)
+    The failure is forced deterministically: scan chunk 0 publishes its
+    prefix poisoned (test hook scan_poison_chunk), every prefix built on it
+    carries the bit, the scan reports -1 counts and the pack writes nothing
+    -- on the first call, with one chunk or many."""
+    pos, rec = mgr.synth_uniform(n, seed=7)
     R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
-    raised = 0
-    with _Hooks(scan_spins=-1, scan_chunk=256):
-        for _ in range(20):
-            try:
-                out = R.redistribute_by_position(rec, pos.clone())
-            except _lib.MgrError as e:
-                assert "scan failed" in str(e)
-                raised += 1
-                if raised >= 2:
-                    break
-            else:
-                assert torch.equal(out, rec)
-    assert raised >= 1
+    with _Hooks(scan_poison_chunk=0):
+        with pytest.raises(_lib.MgrError, match="scan failed"):
+            R.redistribute_by_position(rec, pos.clone())
     out = R.redistribute_by_position(rec, pos.clone())
     assert torch.equal(out, rec)
 

@@ -38,7 +38,7 @@ def _gpu():
 
 
 # ------------------------------------------------------------ binning
-EDGE_FILES = ["bin_edges.npz", "bin_dtypes.npz"]   # f32/f64; int32/int64/f16 (+ narrow boxes)
+EDGE_FILES = ["bin_edges.npz", "bin_dtypes.npz", "bin_dtype_edges.npz"]   # f32/f64; other dtypes; degenerate boxes
 
 
 @pytest.mark.parametrize("edges", EDGE_FILES)

@@ -15,7 +15,7 @@ from tests import golden_io as G
 
 # bin_edges: float32/float64 positions; bin_dtypes: int32/int64/float16
 # positions (and float32 against narrow boxes) over every box dtype
-@pytest.fixture(scope="module", params=["bin_edges.npz", "bin_dtypes.npz"])
+@pytest.fixture(scope="module", params=["bin_edges.npz", "bin_dtypes.npz", "bin_dtype_edges.npz"])
 def edges(request):
     return G.load(request.param)
 
@@ -104,6 +104,56 @@ def test_cell_number_redistribute():
                                                     G.per_rank(f, "ids", size))
     for r in range(size):
         assert G.same_bytes(outs[r], f[f"r{r}_out"])
+
+
+@pytest.mark.parametrize("case", G.soa_cases())
+def test_soa_redistribute_numpy(case):
+    """The multi-field (SoA) restatement == the reference's :157-164 pattern
+    run on every field (make_golden.py make_soa)."""
+    f = G.load(case)
+    size = int(f["size"])
+    fields, pos = G.soa_inputs(f, size)
+    outs = ro.redistribute_fields_by_position_all_ranks(f["topology"], f["box"], size, fields,
+                                                        pos, bool(f["periodic"]))
+    for r in range(size):
+        assert G.same_bytes(pos[r], f[f"r{r}_pos_out"]), (case, r)
+        for i in range(int(f["nfields"])):
+            assert G.same_bytes(outs[r][i], f[f"r{r}_f{i}_out"]), (case, r, i)
+
+
+@pytest.mark.parametrize("case", G.soa_cases())
+def test_soa_redistribute_c(case):
+    """C binning once, C stable partition of every field, source-ordered
+    concat == the reference's per-field outputs."""
+    f = G.load(case)
+    size = int(f["size"])
+    nf, pf = int(f["nfields"]), int(f["pos_field"])
+    sends = []
+    for r in range(size):
+        pin = f[f"r{r}_pos_in"].copy()
+        cell = c_oracle.bin_positions(pin, f["topology"], f["box"], periodic=bool(f["periodic"]))
+        assert G.same_bytes(pin, f[f"r{r}_pos_out"]), (case, r)
+        assert np.array_equal(cell, f[f"r{r}_cell"]), (case, r)
+        per = []
+        for i in range(nf):
+            part, off = c_oracle.partition(pin if i == pf else f[f"r{r}_f{i}_in"], cell, size)
+            per.append([part[off[d]:off[d + 1]] for d in range(size)])
+        sends.append(per)
+    for r in range(size):
+        for i in range(nf):
+            out = np.concatenate([sends[s][i][r] for s in range(size)])
+            assert G.same_bytes(out, f[f"r{r}_f{i}_out"]), (case, r, i)
+
+
+def test_soa_cell_number():
+    f = G.load("soa_cellnum_p5_three.npz")
+    size, nf = int(f["size"]), int(f["nfields"])
+    fields = [[f[f"r{r}_f{i}_in"] for i in range(nf)] for r in range(size)]
+    outs = ro.redistribute_fields_by_cell_number_all_ranks(size, fields,
+                                                           G.per_rank(f, "ids", size))
+    for r in range(size):
+        for i in range(nf):
+            assert G.same_bytes(outs[r][i], f[f"r{r}_f{i}_out"]), (r, i)
 
 
 def test_geometry():
