@@ -57,7 +57,17 @@ N_CFG5_PER_GPU = 512_000_000 // 8    # config 5: 512M over 8 GPUs
 
 # Algorithmic bytes per row of one launch (DESIGN.md §4 Measurement): what
 # the kernel must read and write at least, per row it processes.
-def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1, soa=False):
+def row_bytes_per_kernel(cfg, halo, fine_tile_rows=2048, fine_bins=512, world=1, soa=False,
+                         onepass=False):
+    if cfg == 5 and onepass:
+        ts = 2.0 * fine_bins / fine_tile_rows
+        return {
+            # one read of the 36-B records (their f32 positions in-box: no
+            # write-back), the record into its bin's region, its fine id beside
+            "onepass": 36 + 36 + 2,
+            "count_ids": 2 + 2 + ts,
+            "pack_fine": 2 + 2 + ts + 36 + 36,
+        }
     if cfg == 5 and soa:
         # four arrays: pos f32 x3 (also the binned positions), vel f32 x3,
         # mass f32, id i64 -- 36 bytes a row in 12 + 12 + 4 + 8
@@ -391,6 +401,9 @@ def main():
                     help="SoA payload: the fields as separate arrays moved by one multi-field "
                          "pack (config 5: pos f32 x3, vel f32 x3, mass f32, id i64; configs "
                          "2-4: pos f64 x3 + id i64); the position array is field 0")
+    ap.add_argument("--onepass", action="store_true",
+                    help="config 5 at one GPU: the source partition by the one-pass kernel "
+                         "(records read once, the send_buff list of per-destination regions)")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="bare --gpus N > 1 (no WORLD_SIZE): seconds before the rank "
                          "processes are killed")
@@ -478,9 +491,16 @@ def main():
                 recv.reshape(-1), 36, rpos, fine_cells=[8, 8, 8])
             recv_fids = recv_fids.clone()
 
-            def step():
-                part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])
-                R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=recv_fids)
+            if args.onepass:
+                workload = workload.replace("_local_partition", "_onepass_partition")
+
+                def step():
+                    part.partition_onepass_device(flat, 36, pos, fine_cells=[8, 8, 8])
+                    R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=recv_fids)
+            else:
+                def step():
+                    part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])
+                    R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=recv_fids)
         else:
             if cfg == 4:
                 workload = f"cfg4_{_m(n)}_clustered_2x2x2_local_partition"
@@ -574,7 +594,7 @@ def main():
     # exchange inside the timed region: every timed launch adds two event
     # records to the stream (measured ~2-3 us of step time per kernel).  The
     # other kernels are timed in an untimed detail pass after the region.
-    timed = {"report": ["pack", "exchange", "halo", "halo_pack", "pack_fine"],
+    timed = {"report": ["pack", "exchange", "halo", "halo_pack", "pack_fine", "onepass"],
              "all": list(_lib.PROFILE_KERNELS),
              "none": []}[args.prof]
     _lib.profile_select(timed)
@@ -604,7 +624,7 @@ def main():
             if _lib.alg_read(k):   # host-counted bytes (the halo's selections)
                 kernels[k]["alg_bytes_per_launch"] = _lib.alg_read(k) / cnt
     missing = [k for k in list(row_bytes_per_kernel(cfg, bool(args.overload > 0),
-                                                    soa=args.soa)) + ["scan"]
+                                                    soa=args.soa, onepass=args.onepass)) + ["scan"]
                if k not in kernels]
     if missing:
         # detail pass (not timed): the kernels left out of the timed region
@@ -696,7 +716,7 @@ def main():
     fine_tr = (int(_lib.load().mgr_ranked_tile_rows(12 if args.soa else 36, 512)) if cfg == 5
                else 2048)
     for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world,
-                                     soa=args.soa).items():
+                                     soa=args.soa, onepass=args.onepass).items():
         if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
             e = kernels[k]
             per_step = e["launches"] / e["steps"] if e.get("steps") else 1

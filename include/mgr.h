@@ -273,6 +273,26 @@ int mgr_partition_by_position(const mgr_plan* plan, void* pos, int pos_dtype, in
                               int64_t row_stride, int periodic, const void* src,
                               int64_t row_bytes, void* dst, void* dest, int64_t* bin_counts,
                               int tile_rows, void* workspace, void* stream);
+/* One-pass source partition of records that hold their own positions (the
+ * 36-byte config-5 records with their f32 position view, S9; positions at
+ * byte pos_offset of every row, float32 / float64, 3-D, <= 64 bins): bin,
+ * rank and scatter in ONE read of the records -- the classic path (bin pass +
+ * pack) reads the record lines twice.  The output is the reference's
+ * send_buff list itself (redist.py:195-198): bin b's rows, in their original
+ * order, from out + b * cap_rows * row_bytes (its fine cells -- fine_plan as
+ * in mgr_bin_count_fine, else NULL -- from fine_out + b * cap_rows).
+ * Positions are wrapped in place as mgr_bin_count does (S1).  bin_counts
+ * (int64 [nbins], device) = the rows of every bin; rows at or beyond cap_rows
+ * are NOT written, so a count above cap_rows means the caller redoes the
+ * partition with the classic path (mgr_bin_count with periodic = 0 re-bins
+ * the stored, wrapped positions identically, S2) -- or -1 everywhere when a
+ * look-back gave up (nothing written).  Workspace: mgr_onepass_workspace_bytes
+ * (zeroed by the call).  MGR_EUNSUPPORTED for shapes it does not take.      */
+int64_t mgr_onepass_workspace_bytes(int64_t n, int nbins);
+int mgr_partition_onepass(const mgr_plan* plan, const mgr_plan* fine_plan, void* data,
+                          int64_t row_bytes, int64_t pos_offset, int pos_dtype, int64_t n,
+                          int periodic, void* out, uint16_t* fine_out, int64_t cap_rows,
+                          int64_t* bin_counts, void* workspace, void* stream);
 /* bin starts (int64[nbins+1], device) left in the workspace by mgr_scan.   */
 int mgr_bin_starts(int64_t n, int nbins, int tile_rows, const void* workspace,
                    const int64_t** out);

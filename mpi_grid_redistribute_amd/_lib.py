@@ -61,6 +61,8 @@ SIGNATURES = {
     "mgr_partition_by_position": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _I64, _P, _P, _P, _I,
                                        _P, _P]),
     "mgr_bin_starts": (_I, [_I64, _I, _I, _P, ctypes.POINTER(_P)]),
+    "mgr_onepass_workspace_bytes": (_I64, [_I64, _I]),
+    "mgr_partition_onepass": (_I, [_P, _P, _P, _I64, _I64, _I, _I64, _I, _P, _P, _I64, _P, _P, _P]),
     "mgr_halo_flags": (_I, [_P, _I, _I64, _I64, _I, _P, _P, _P, _P]),
     "mgr_bin_count_halo": (_I, [_P, _P, _I, _I64, _I64, _I, _P, _P, _P, _P, _I, _P, _P]),
     "mgr_msel_count": (_I, [_P, _I64, _I, _P, _I, _P, _P]),
@@ -197,7 +199,7 @@ HOOK_DEFAULTS = {"tile_rounds": 0, "scan_chunk": 2048, "scan_max_chunks": 1024,
 # Profiler kernel names (mgr_internal.h KernelId).
 PROFILE_KERNELS = ("bin_count", "scan", "pack", "cell_ids", "bin_ids", "cellnum_idx", "synth",
                    "exchange", "halo", "bin_fine", "count_ids", "pack_fine", "pack_narrow",
-                   "halo_pack")
+                   "halo_pack", "onepass")
 
 
 _prof_on = False

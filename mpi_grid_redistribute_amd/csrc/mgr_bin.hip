@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void cellnum_from_idx_kernel(const int64_t*
 // dimension with the fast wrap and a power-of-two box length, 32-bit index
 // math, not a fine plan -- then kGeoF32 / kGeoF64 by the quotient's type
 // (f32 positions with an f32 box compute in f32, everything else in f64).
-static int geo_kind(const Geom& g, bool pos_f32) {
+int geo_kind(const Geom& g, bool pos_f32) {
     if (g.dim != 3 || g.fine || !g.fast32) return kGeoAny;
     const bool f32c = pos_f32 && g.compute_f32;
     for (int d = 0; d < 3; ++d) {

@@ -98,7 +98,8 @@ const char* kernel_name(int k) {
     static const char* names[K_NUM_KERNELS] = {"bin_count", "scan", "pack", "cell_ids",
                                                "bin_ids", "cellnum_idx", "synth",
                                                "exchange", "halo", "bin_fine", "count_ids",
-                                               "pack_fine", "pack_narrow", "halo_pack"};
+                                               "pack_fine", "pack_narrow", "halo_pack",
+                                               "onepass"};
     return (k >= 0 && k < K_NUM_KERNELS) ? names[k] : "?";
 }
 
@@ -365,12 +366,10 @@ int mgr_bin_count(const mgr_plan* plan, void* pos, int pos_dtype, int64_t n, int
     return MGR_OK;
 }
 
-int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* pos, int pos_dtype,
-                       int64_t n, int64_t row_stride, int periodic, void* dest,
-                       uint16_t* fine_ids, int tile_rows, void* workspace, void* stream) {
-    int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
-    if (rc) return rc;
-    if ((rc = check_tile(tile_rows))) return rc;
+// The fine geometry of fine_plan over plan (same box and dimension,
+// topology * fine), for the bin kernels' fine side output.
+static int fine_geom(const mgr_plan* plan, const mgr_plan* fine_plan, mgr::Geom& g,
+                     mgr::FineGeom& fg) {
     if (!fine_plan || !fine_plan->g.fine) return fail(MGR_EINVAL, "fine_plan is not a fine-cell plan");
     if (fine_plan->g.dim != plan->g.dim) return fail(MGR_EINVAL, "plans of different dimensions");
     for (int d = 0; d < plan->g.dim; ++d)
@@ -378,10 +377,6 @@ int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* po
             fine_plan->g.n[d] != plan->g.n[d] * fine_plan->g.fmod[d] ||
             fine_plan->g.box_dtype != plan->g.box_dtype)
             return fail(MGR_EINVAL, "fine_plan is not over this plan's box and topology (dim %d)", d);
-    if (n > 0 && (!dest || !workspace || !fine_ids)) return fail(MGR_EINVAL, "null dest/fine_ids/workspace");
-    mgr::Geom g = plan->g;
-    pos_modes(g, pos_dtype);
-    mgr::FineGeom fg;
     memset(&fg, 0, sizeof fg);
     for (int d = 0; d < g.dim; ++d) {
         fg.nd[d] = fine_plan->g.nd[d];
@@ -391,6 +386,20 @@ int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* po
     }
     fg.nbins = fine_plan->g.nbins;
     if (!fine_plan->g.fast32) g.fast32 = 0;   // the fine indexes must fit 32 bits too
+    return MGR_OK;
+}
+
+int mgr_bin_count_fine(const mgr_plan* plan, const mgr_plan* fine_plan, void* pos, int pos_dtype,
+                       int64_t n, int64_t row_stride, int periodic, void* dest,
+                       uint16_t* fine_ids, int tile_rows, void* workspace, void* stream) {
+    int rc = check_pos(plan, pos, pos_dtype, n, row_stride);
+    if (rc) return rc;
+    if ((rc = check_tile(tile_rows))) return rc;
+    mgr::Geom g = plan->g;
+    pos_modes(g, pos_dtype);
+    mgr::FineGeom fg;
+    if ((rc = fine_geom(plan, fine_plan, g, fg))) return rc;
+    if (n > 0 && (!dest || !workspace || !fine_ids)) return fail(MGR_EINVAL, "null dest/fine_ids/workspace");
     const mgr::Workspace ws = mgr::carve(workspace, n, g.nbins, tile_rows);
     HIP_OK(mgr::launch_bin_count(g, pos, pos_dtype, n, row_stride, periodic, dest,
                                  tile_rows, ws, (hipStream_t)stream, &fg, fine_ids));
@@ -645,6 +654,40 @@ int mgr_pack_tiles(const void* src, int64_t row_bytes, int64_t n, const void* de
     HIP_OK(mgr::launch_pack(src, row_bytes, n, dest, nbins, drop_bin, tile_rows, ws, dst,
                             redirect_bin, redirect_dst, (hipStream_t)stream, ids_src, ids_dst,
                             ids_redirect_dst));
+    return MGR_OK;
+}
+
+int64_t mgr_onepass_workspace_bytes(int64_t n, int nbins) {
+    if (n < 0 || nbins < 1 || nbins > MGR_MAX_BINS) return -1;
+    return mgr::onepass_workspace_bytes(n, nbins);
+}
+
+int mgr_partition_onepass(const mgr_plan* plan, const mgr_plan* fine_plan, void* data,
+                          int64_t row_bytes, int64_t pos_offset, int pos_dtype, int64_t n,
+                          int periodic, void* out, uint16_t* fine_out, int64_t cap_rows,
+                          int64_t* bin_counts, void* workspace, void* stream) {
+    if (!plan) return fail(MGR_EINVAL, "null plan");
+    if (n < 0 || cap_rows < 0) return fail(MGR_EINVAL, "n %lld, cap_rows %lld", (long long)n,
+                                           (long long)cap_rows);
+    if (!bin_counts || (n > 0 && (!data || !out || !workspace)))
+        return fail(MGR_EINVAL, "null data/out/bin_counts/workspace");
+    mgr::Geom g = plan->g;
+    if (pos_dtype != MGR_F32 && pos_dtype != MGR_F64)
+        return fail(MGR_EUNSUPPORTED, "one-pass partition: float32 / float64 positions only");
+    pos_modes(g, pos_dtype);
+    mgr::FineGeom fg;
+    if (fine_plan) {
+        int rc = fine_geom(plan, fine_plan, g, fg);
+        if (rc) return rc;
+        if (n > 0 && !fine_out) return fail(MGR_EINVAL, "fine_plan without fine_out");
+    }
+    const hipError_t e = mgr::launch_onepass(g, fine_plan ? &fg : nullptr, data, row_bytes,
+                                             pos_offset, pos_dtype, n, periodic, out, fine_out,
+                                             cap_rows, bin_counts, workspace, (hipStream_t)stream);
+    if (e == hipErrorNotSupported)
+        return fail(MGR_EUNSUPPORTED, "one-pass partition: shape not taken (3-D, <= 64 bins, "
+                    "4-byte-multiple rows of <= 128 B holding the positions, 16-byte aligned data)");
+    HIP_OK(e);
     return MGR_OK;
 }
 

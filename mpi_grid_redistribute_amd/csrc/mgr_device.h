@@ -735,6 +735,79 @@ __device__ __forceinline__ void wave_copy(uint8_t* __restrict__ d, const uint8_t
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
+// ------------------------------------------------ image stores (packs)
+typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Store through an address held as an integer: a global-address-space
+// pointer, so the compiler emits global_store (a plain pointer would be flat).
+template <typename T>
+__device__ __forceinline__ void gstore(unsigned long long a, T v) {
+    *(__attribute__((address_space(1))) T*)a = v;
+}
+
+// One 16-byte unit (image bytes [x, x + 16)) of a destination-sorted LDS
+// image to its output: a bin's rows are one run of the image, and the unit's
+// bytes go to gaddr[bin] + x.  A unit inside one run is one 16-byte store;
+// a unit straddling two runs goes dword by dword.  For rows wider than 16 B
+// a unit covers at most two rows (x / RB and (x + 15) / RB), so both run
+// addresses are fetched up front, side by side -- no LDS lookup per dword on
+// the straddling path (the lookups were a chain of dependent LDS reads per
+// dword).  DROP: a zero address is a dropped bin, not written.
+template <int RB, bool DROP, typename BinT>
+__device__ __forceinline__ void store_img_unit(const uint8_t* __restrict__ img,
+                                               const BinT* ibin,
+                                               const unsigned long long* gaddr, int x,
+                                               int nbytes) {
+    const u32x4_t q = *(const u32x4_t*)(img + x);
+    const int r0 = x / RB, r1 = min(x + 15, nbytes - 1) / RB;
+    const int bf = ibin[r0], bl = ibin[r1];
+    const unsigned long long af = gaddr[bf], al = gaddr[bl];
+    if (x + 16 <= nbytes && bf == bl) {
+        if (!DROP || af) gstore<u32x4_a4>(af + x, q);
+        return;
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const int xd = x + 4 * d;
+        if (xd >= nbytes) break;
+        unsigned long long a;
+        if constexpr (RB > 16) a = xd < (r0 + 1) * RB ? af : al;
+        else a = gaddr[ibin[xd / RB]];   // narrow rows: up to 4 rows in a unit
+        if (!DROP || a) gstore<uint32_t>(a + xd, q[d]);
+    }
+}
+
+// A wave's 64 * RPW rows of RB bytes (compile time), parked in LDS in row
+// order at `rows`, permuted in place into the destination-ordered image (row
+// 64 q + lane -> slot[q]), then the image streamed out (store_img_unit,
+// gaddr[bin] = the address of the bin's image slot 0 in the output, 0 = not
+// written).  The multi-field pack runs it per field, the one-pass partition
+// once per wave.
+template <int RB, int RPW>
+__device__ __forceinline__ void image_pass(uint8_t* rows, const uint8_t* ibin,
+                                           const unsigned long long* gaddr, const int* slot,
+                                           const bool* valid, int nrows, int lane) {
+    constexpr int DW = RB / 4;
+    uint32_t* w32 = (uint32_t*)rows;
+    uint32_t row[RPW][DW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q)
+        if (valid[q]) {
+#pragma unroll
+            for (int p = 0; p < DW; ++p) row[q][p] = w32[(64 * q + lane) * DW + p];
+        }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < RPW; ++q)
+        if (valid[q]) {
+#pragma unroll
+            for (int p = 0; p < DW; ++p) w32[slot[q] * DW + p] = row[q][p];
+        }
+    wave_sync();
+    const int nbytes = nrows * RB;
+    for (int x = 16 * lane; x < nbytes; x += 1024) store_img_unit<RB, true>(rows, ibin, gaddr, x, nbytes);
+}
+
 // ------------------------------------------------- flag-set selections
 // The halo's selections read 16-bit face flags in chunks of kSelChunk rows:
 // lane l holds rows [16 l, 16 l + 16) of a chunk as 8 packed words (two

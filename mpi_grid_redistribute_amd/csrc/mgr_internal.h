@@ -98,7 +98,7 @@ int nbits_for(int nbins);
 // Kernel ids for the profiler.
 enum KernelId { K_BIN_COUNT, K_SCAN, K_PACK, K_CELL_IDS, K_BIN_IDS, K_CELLNUM_IDX, K_SYNTH,
                 K_EXCHANGE, K_HALO, K_BIN_FINE, K_COUNT_IDS, K_PACK_FINE, K_PACK_NARROW,
-                K_HALO_PACK, K_NUM_KERNELS };
+                K_HALO_PACK, K_ONEPASS, K_NUM_KERNELS };
 const char* kernel_name(int k);
 void prof_begin(hipStream_t s, int k);
 void prof_end(hipStream_t s, int k);
@@ -146,6 +146,14 @@ int pack_tile_rows(int64_t row_bytes, int nbins);
 hipError_t launch_tile_offsets(const Workspace& ws, int nbins, const int64_t* tiles, int ntiles,
                                int64_t* out, hipStream_t s);
 int ranked_tile_rows(int64_t row_bytes, int nbins);
+// The plan's geometry class for bin_row_fast (kGeoAny / kGeoF32 / kGeoF64).
+int geo_kind(const Geom& g, bool pos_f32);
+// One-pass source partition (mgr_onepass.hip, mgr_partition_onepass).
+int64_t onepass_workspace_bytes(int64_t n, int nbins);
+hipError_t launch_onepass(const Geom& g, const FineGeom* fg, void* data, int64_t row_bytes,
+                          int64_t pos_off, int pos_dtype, int64_t n, int periodic, void* out,
+                          uint16_t* fine_out, int64_t cap, int64_t* bin_counts, void* workspace,
+                          hipStream_t s);
 hipError_t launch_halo_flags(const void* pos, int pos_dtype, int64_t n, int64_t stride, int dim,
                              const double* hi, const double* lo, uint16_t* flags, hipStream_t s);
 

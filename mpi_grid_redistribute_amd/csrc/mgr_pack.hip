@@ -432,47 +432,6 @@ hipError_t launch_msel_pack(int nfields, const void* const* srcs, const int64_t*
 // run's (4-byte aligned) place in the output, a unit straddling two runs is
 // stored dword by dword.  Plain 4-byte units would need RB/4 load and RB/4
 // store instructions per round instead of ~RB/16.
-typedef unsigned int u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-
-// Store through an address held as an integer: a global-address-space
-// pointer, so the compiler emits global_store (a plain pointer would be flat).
-template <typename T>
-__device__ __forceinline__ void gstore(unsigned long long a, T v) {
-    *(__attribute__((address_space(1))) T*)a = v;
-}
-
-// One 16-byte unit (image bytes [x, x + 16)) of a destination-sorted LDS
-// image to its output: a bin's rows are one run of the image, and the unit's
-// bytes go to gaddr[bin] + x.  A unit inside one run is one 16-byte store;
-// a unit straddling two runs goes dword by dword.  For rows wider than 16 B
-// a unit covers at most two rows (x / RB and (x + 15) / RB), so both run
-// addresses are fetched up front, side by side -- no LDS lookup per dword on
-// the straddling path (the lookups were a chain of dependent LDS reads per
-// dword).  DROP: a zero address is a dropped bin, not written.
-template <int RB, bool DROP, typename BinT>
-__device__ __forceinline__ void store_img_unit(const uint8_t* __restrict__ img,
-                                               const BinT* ibin,
-                                               const unsigned long long* gaddr, int x,
-                                               int nbytes) {
-    const u32x4_t q = *(const u32x4_t*)(img + x);
-    const int r0 = x / RB, r1 = min(x + 15, nbytes - 1) / RB;
-    const int bf = ibin[r0], bl = ibin[r1];
-    const unsigned long long af = gaddr[bf], al = gaddr[bl];
-    if (x + 16 <= nbytes && bf == bl) {
-        if (!DROP || af) gstore<u32x4_a4>(af + x, q);
-        return;
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const int xd = x + 4 * d;
-        if (xd >= nbytes) break;
-        unsigned long long a;
-        if constexpr (RB > 16) a = xd < (r0 + 1) * RB ? af : al;
-        else a = gaddr[ibin[xd / RB]];   // narrow rows: up to 4 rows in a unit
-        if (!DROP || a) gstore<uint32_t>(a + xd, q[d]);
-    }
-}
-
 template <int RB, int RPW, bool SEL>
 __global__ __launch_bounds__(1024) void pack_img_kernel(
     const uint8_t* __restrict__ src, int64_t n, const uint8_t* __restrict__ dest, int nb,
@@ -626,14 +585,16 @@ __global__ __launch_bounds__(1024) void pack_img_kernel(
 // 128 rows (two 64-row rounds), per-bin bases exchanged through LDS behind
 // one barrier.  Every field's 128 rows (128 * rb bytes, 16-byte aligned) are
 // copied into wave-private LDS by LDS-DMA (global_load_lds_dwordx4: no
-// registers, so any number of fields up to kFieldsLds bytes), the rows'
-// image slots (destination-major, stable) are written as an inverse
-// permutation (slot -> row) plus the bin of every slot, and each field's
-// destination-ordered image is streamed out in 16-byte units gathered from
-// the LDS rows: a unit inside one bin's run is one 16-byte store to the
-// run's (4-byte aligned) place, a unit straddling two runs goes dword by
-// dword.  Row bytes of every field are 4-byte multiples; the optional 2-byte
-// side field (fine cells) is stored per row as in pack_img_kernel.
+// registers, every field's loads in flight at once), and each field in turn
+// is permuted in place into its destination-ordered image (a row's slot is
+// shared by all fields) and streamed out in 16-byte units (store_img_unit: a
+// unit inside one bin's run is one 16-byte store to the run's 4-byte-aligned
+// place, a unit straddling two runs goes dword by dword).  Field row sizes
+// of 4..64 bytes (4-byte multiples) run a pass with the size at compile time
+// (LDS accesses at immediate offsets, division by a constant); wider ones a
+// generic pass that gathers the image's dwords through the inverse
+// permutation.  The optional 2-byte side field (fine cells) is stored per
+// row as in pack_img_kernel.
 constexpr int kFieldsMax = 8;          // fields per launch
 constexpr int kFieldsWR = 128;         // rows per wave
 struct PackFieldsArgs {
@@ -641,11 +602,50 @@ struct PackFieldsArgs {
     uint8_t* dst[kFieldsMax];
     uint8_t* red[kFieldsMax];
     int rb[kFieldsMax];          // row bytes, 4-byte multiples
-    uint32_t rinv[kFieldsMax];   // floor(2^32 / rb) + 1: x / rb == umulhi(x, rinv) for x < 2^18
     int loff[kFieldsMax];        // byte offset of field f's rows in a wave's LDS area
     int nf;
     int wave_lds;                // LDS bytes per wave
 };
+// a wave's LDS after the fields' rows: per-bin output address (one field at
+// a time), per-bin image row offset, slot -> wave row, slot -> bin
+constexpr int kFieldsTail = 64 * 8 + 64 * 8 + 2 * kFieldsWR;
+
+// Any 4-byte-multiple row size (the generic pass): every 16-byte unit of the
+// image gathered dword by dword from the rows in row order through the
+// inverse permutation (slot -> row); rowoff[bin] = the output row of the
+// bin's image slot 0.
+__device__ __forceinline__ void fields_pass_any(const uint8_t* rows, int rb, const uint8_t* inv,
+                                                const uint8_t* ibin, const long long* rowoff,
+                                                unsigned long long dbase, unsigned long long rbase,
+                                                int redirect_bin, int drop_bin, int nrows,
+                                                int lane) {
+    const uint32_t rinv = (uint32_t)(0x100000000ull / (unsigned)rb + 1);   // x / rb, x < 2^18
+    const int nbytes = nrows * rb;
+    auto addr = [&](int bb) -> unsigned long long {
+        return (bb == redirect_bin ? rbase : dbase) + (unsigned long long)(rowoff[bb] * rb);
+    };
+    for (int x = 16 * lane; x < nbytes; x += 1024) {
+        int s[4];
+        u32x4_t q;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int xd = min(x + 4 * d, nbytes - 4);
+            s[d] = (int)__umulhi((unsigned)xd, rinv);
+            q[d] = *(const uint32_t*)(rows + (int)inv[s[d]] * rb + (xd - s[d] * rb));
+        }
+        const int bf = ibin[s[0]], bl = ibin[s[3]];
+        if (x + 16 <= nbytes && bf == bl) {
+            if (bf != drop_bin) gstore<u32x4_a4>(addr(bf) + x, q);
+        } else {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const int xd = x + 4 * d;
+                const int bd = ibin[s[d]];
+                if (xd < nbytes && bd != drop_bin) gstore<uint32_t>(addr(bd) + xd, q[d]);
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(1024) void pack_fields_kernel(
     PackFieldsArgs fa, int64_t n, const uint8_t* __restrict__ dest, int nb, int nbits,
@@ -659,9 +659,11 @@ __global__ __launch_bounds__(1024) void pack_fields_kernel(
     const int nw = blockDim.x >> 6;
     int* s_cnt = (int*)smem;                                    // [nw][64]
     uint8_t* wl = smem + nw * 64 * 4 + w * fa.wave_lds;         // the fields' rows
-    long long* rowoff = (long long*)(wl + fa.wave_lds - 64 * 8 - 2 * WR);   // [64]
-    uint8_t* inv = (uint8_t*)(rowoff + 64);                     // image slot -> wave row
-    uint8_t* ibin = inv + WR;                                   // image slot -> bin
+    uint8_t* tail = wl + fa.wave_lds - kFieldsTail;
+    unsigned long long* gaddr = (unsigned long long*)tail;      // [64]
+    long long* rowoff = (long long*)(tail + 64 * 8);            // [64]
+    uint8_t* inv = tail + 64 * 16;                              // slot -> wave row
+    uint8_t* ibin = inv + WR;                                   // slot -> bin
     const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
     const int64_t row0 = tile * (int64_t)tile_rows + (int64_t)WR * w;
     const int nrows = __builtin_amdgcn_readfirstlane((int)max((int64_t)0, min((int64_t)WR, n - row0)));
@@ -719,57 +721,48 @@ __global__ __launch_bounds__(1024) void pack_fields_kernel(
     // wave image order: exclusive prefix of the wave's bin counts
     const int excl = wave_incl_dpp(cnt) - cnt;
     int run = excl;   // lane b: bin b's next image slot, round by round
+    int slot[RPW];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         // (shuffles in uniform control flow: a bpermute from a lane outside
         // the exec mask does not read that lane's value)
-        const int slot = __shfl(run, (int)b[q], 64) + (valid[q] ? rank_in(pe[q]) : 0);
-        const long long gr = id_src ? __shfl(tbase - excl, (int)b[q], 64) + slot : 0;
+        slot[q] = __shfl(run, (int)b[q], 64) + (valid[q] ? rank_in(pe[q]) : 0);
+        const long long gr = id_src ? __shfl(tbase - excl, (int)b[q], 64) + slot[q] : 0;
         run += cq[q];
         if (valid[q]) {
-            inv[slot] = (uint8_t)(64 * q + lane);
-            ibin[slot] = (uint8_t)b[q];
+            inv[slot[q]] = (uint8_t)(64 * q + lane);
+            ibin[slot[q]] = (uint8_t)b[q];
             if (id_src && (int)b[q] != drop_bin)
                 ((int)b[q] == redirect_bin ? id_red : id_dst)[gr] = (uint16_t)idv[q];
         }
     }
-    if (lane < nb) rowoff[lane] = tbase - excl;   // output row of image slot 0, bin lane
-    wave_sync();
-    // every field's image, gathered from the LDS rows through the inverse
-    // permutation, streamed out in 16-byte units
-#pragma unroll
-    for (int f = 0; f < kFieldsMax; ++f) {
-        if (f >= fa.nf) break;
-        const int rb = fa.rb[f];
-        const uint32_t rinv = fa.rinv[f];
-        const uint8_t* rows = wl + fa.loff[f];
-        const unsigned long long dbase = (unsigned long long)fa.dst[f];
-        const unsigned long long rbase = (unsigned long long)fa.red[f];
-        const int nbytes = nrows * rb;
-        auto addr = [&](int bb) -> unsigned long long {
-            return (bb == redirect_bin ? rbase : dbase) + (unsigned long long)(rowoff[bb] * rb);
-        };
-        for (int x = 16 * lane; x < nbytes; x += 1024) {
-            int s[4];
-            u32x4_t q;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const int xd = min(x + 4 * d, nbytes - 4);
-                s[d] = (int)__umulhi((unsigned)xd, rinv);
-                const int o = xd - s[d] * rb;
-                q[d] = *(const uint32_t*)(rows + (int)inv[s[d]] * rb + o);
-            }
-            const int bf = ibin[s[0]], bl = ibin[s[3]];
-            if (x + 16 <= nbytes && bf == bl) {
-                if (bf != drop_bin) gstore<u32x4_a4>(addr(bf) + x, q);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const int xd = x + 4 * d;
-                    const int bd = ibin[s[d]];
-                    if (xd < nbytes && bd != drop_bin) gstore<uint32_t>(addr(bd) + xd, q[d]);
-                }
-            }
+    const long long ro = tbase - excl;   // lane b: output row of bin b's image slot 0
+    if (lane < nb) rowoff[lane] = ro;
+    // per-lane copies of the fields' run-time values (lane f: field f), read
+    // with readlane: a kernel-argument array indexed at run time would be a
+    // memory load (msel_pack_kernel)
+    const int lrb = lane < fa.nf ? fa.rb[lane] : 0;
+    const int lloff = lane < fa.nf ? fa.loff[lane] : 0;
+    const unsigned long long ldst = lane < fa.nf ? (unsigned long long)fa.dst[lane] : 0ull;
+    const unsigned long long lred = lane < fa.nf ? (unsigned long long)fa.red[lane] : 0ull;
+#pragma unroll 1
+    for (int f = 0; f < fa.nf; ++f) {
+        const int rb = __builtin_amdgcn_readlane(lrb, f);
+        uint8_t* rows = wl + __builtin_amdgcn_readlane(lloff, f);
+        const unsigned long long dbase = readlane64(ldst, f), rbase = readlane64(lred, f);
+        wave_sync();   // the previous field's stores have read gaddr
+        if (lane < nb)
+            gaddr[lane] = lane == drop_bin ? 0ull
+                          : (lane == redirect_bin ? rbase : dbase) + (unsigned long long)(ro * rb);
+        wave_sync();
+        switch (rb) {
+#define MGR_FP(RB_) case RB_: image_pass<RB_, kFieldsWR / 64>(rows, ibin, gaddr, slot, valid, nrows, lane); break;
+            MGR_FP(4) MGR_FP(8) MGR_FP(12) MGR_FP(16) MGR_FP(20) MGR_FP(24) MGR_FP(28) MGR_FP(32)
+            MGR_FP(36) MGR_FP(40) MGR_FP(44) MGR_FP(48) MGR_FP(52) MGR_FP(56) MGR_FP(60) MGR_FP(64)
+#undef MGR_FP
+            default:
+                fields_pass_any(rows, rb, inv, ibin, rowoff, dbase, rbase, redirect_bin, drop_bin,
+                                nrows, lane);
         }
     }
 }
@@ -1234,7 +1227,10 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if (lds > 160 * 1024) return hipErrorNotSupported;
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
-    int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
+    // as many resident workgroups per CU as the tile image lets the LDS hold
+    // (36-byte rows: one; the 4..16-byte fields of a SoA payload: two to four)
+    const int per_cu = max(1, min(4, (160 * 1024) / lds));
+    int64_t grid = ((int64_t)device_cus() * per_cu + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;
 #define MGR_PRT(RB_, TR_)                                                                     \
@@ -1370,7 +1366,7 @@ hipError_t launch_pack_fields(int nf, const void* const* srcs, const int64_t* ro
     const bool shape = !h.pack_generic && nbins <= 64 && dest_bytes(nbins) == 1 &&
                        tile_rows % kFieldsWR == 0 && nw >= 1 && nw <= 16;
     // rows of one wave's fields, within the LDS a workgroup may take
-    const int budget = (160 * 1024 - nw * 256) / max(nw, 1) - (64 * 8 + 2 * kFieldsWR);
+    const int budget = (160 * 1024 - nw * 256) / max(nw, 1) - kFieldsTail;
     std::vector<int> fast, slow;
     for (int f = 0; f < nf; ++f) {
         uintptr_t a = (uintptr_t)dsts[f] | (uintptr_t)row_bytes[f];
@@ -1397,12 +1393,11 @@ hipError_t launch_pack_fields(int nf, const void* const* srcs, const int64_t* ro
             fa.dst[fa.nf] = (uint8_t*)dsts[f];
             fa.red[fa.nf] = reds ? (uint8_t*)reds[f] : nullptr;
             fa.rb[fa.nf] = rb;
-            fa.rinv[fa.nf] = (uint32_t)(0x100000000ull / (unsigned)rb + 1);
             fa.loff[fa.nf] = rows;
             rows += kFieldsWR * rb;   // a multiple of 512 bytes
             ++fa.nf;
         }
-        fa.wave_lds = rows + 64 * 8 + 2 * kFieldsWR;
+        fa.wave_lds = rows + kFieldsTail;
         const int lds = nw * 64 * 4 + nw * fa.wave_lds;
         ensure_lds(pack_fields_kernel, lds);
         prof_begin(s, K_PACK);

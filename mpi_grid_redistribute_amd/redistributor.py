@@ -44,6 +44,7 @@ from .halo import DeviceSelect, exchange_overload, halo_capacity, thresholds
 
 
 _WRITE_BACK = {"changed": _lib.MGR_WRITE_BACK_CHANGED, "all": _lib.MGR_WRITE_BACK_ALL}
+_TORCH_POS = {_lib.MGR_F32: torch.float32, _lib.MGR_F64: torch.float64}
 
 
 class _Plan:
@@ -955,6 +956,126 @@ class GridPartitioner:
         if fine_cells is None:
             return outs, counts
         return outs, fid_out.view(torch.int16)[:n], counts
+
+    def partition_onepass_device(self, data_flat, row_bytes, pos_tensor, periodic=True,
+                                 stream=None, fine_cells=None, cap_rows=None):
+        """The local stage in ONE read of the records (mgr_partition_onepass):
+        ``pos_tensor`` is the (n, >= 3) float32 / float64 position view INSIDE
+        the records of ``data_flat`` (uint8 device tensor of n * row_bytes, e.g.
+        config 5's 36-byte records and their f32 positions, S9), wrapped in
+        place.  The output is the reference's send_buff list (redist.py:195-
+        198): bin b's rows, in order, from row b * cap of ``out`` (its fine
+        cells from fine_out[b * cap]).  Returns (out, fine_out or None, counts,
+        cap) device tensors without a host sync; a count above cap means the
+        bin did not fit (the caller redoes the partition: partition_lists
+        does), -1 counts a failed look-back.  ``cap_rows``: rows per bin region
+        (default 1.25 x the mean + 4096).  MgrError (MGR_EUNSUPPORTED) for
+        shapes the one-pass kernel does not take."""
+        n = int(pos_tensor.shape[0])
+        esz = pos_tensor.element_size()
+        off = pos_tensor.data_ptr() - data_flat.data_ptr() if n else 0
+        if n and (pos_tensor.stride(0) * esz != row_bytes or pos_tensor.stride(1) != 1
+                  or off < 0 or off + 3 * esz > row_bytes):
+            raise ValueError("pos_tensor must be the position view inside the records")
+        cap = int(cap_rows) if cap_rows is not None else (5 * n) // (4 * self.nbins) + 4096
+        key = ("onepass", n, int(row_bytes), cap, fine_cells is not None)
+        if key not in self._cache:
+            wsb = _lib.load().mgr_onepass_workspace_bytes(n, self.nbins)
+            ws = torch.empty(max(int(wsb), 8), dtype=torch.uint8, device=self._dev)
+            out = torch.empty(max(self.nbins * cap * int(row_bytes), 1), dtype=torch.uint8,
+                              device=self._dev)
+            fo = (torch.empty(max(self.nbins * cap, 1), dtype=torch.int16, device=self._dev)
+                  if fine_cells is not None else None)
+            counts = torch.empty(self.nbins, dtype=torch.int64, device=self._dev)
+            self._cache = {key: (ws, out, fo, counts)}
+        ws, out, fo, counts = self._cache[key]
+        self.last_counts = counts
+        fplan = self._fine_plan(fine_cells) if fine_cells is not None else None
+        _lib.call("mgr_partition_onepass", self._plan.h, fplan.h if fplan else None,
+                  _lib.ptr(data_flat), int(row_bytes), int(off), pos_code(pos_tensor.dtype), n,
+                  int(bool(periodic)), _lib.ptr(out), _lib.ptr(fo), cap, _lib.ptr(counts),
+                  _lib.ptr(ws), _lib.stream_handle(stream))
+        return out, fo, counts, cap
+
+    def partition_lists(self, data, position, periodic=True, fine_cells=None):
+        """The reference's send_buff list (redist.py:195-198: send_buff[i] =
+        data[rank_to_send == i], original order kept): one array per bin, in
+        the container type of ``data``; ``position`` wrapped in place (S1).
+        With ``fine_cells`` also every row's fine cell inside its bin's cell,
+        as a second list (uint16).  Records holding their own float32 /
+        float64 positions go through the one-pass kernel
+        (partition_onepass_device: every record read once); any other shape,
+        or a bin that outgrows its region, through the classic bin + scan +
+        pack (a redo re-bins the stored, already wrapped positions with
+        periodic = 0 -- identical bins, S2 -- so nothing is wrapped twice)."""
+        rows = Rows(data, self._dev)
+        pos = Positions(position, self.dim, self._dev, data_rows=rows)
+        n, rb = rows.n, rows.row_bytes
+        if pos.n != n:
+            raise ValueError("data and position row counts differ")
+        counts = None
+        onepass_pos = None
+        if n and pos.code in (_lib.MGR_F32, _lib.MGR_F64) and self.dim == 3:
+            esz = _lib.POS_ITEMSIZE[pos.code]
+            off = pos.addr - rows.flat.data_ptr()
+            if pos.stride * esz == rb and 0 <= off and off + 3 * esz <= rb and off % esz == 0:
+                # the positions as a view of the records' device bytes
+                base = rows.flat.view(_TORCH_POS[pos.code])
+                onepass_pos = torch.as_strided(
+                    base, (n, 3), (pos.stride, 1),
+                    (pos.addr - base.untyped_storage().data_ptr()) // esz)
+        if onepass_pos is not None:
+            try:
+                out, fo, cnt_d, cap = self.partition_onepass_device(
+                    rows.flat, rb, onepass_pos, periodic, fine_cells=fine_cells)
+                counts = cnt_d.cpu().numpy()
+                pos.finish()
+                check_counts(counts, [])
+                if (counts > cap).any():
+                    counts = None          # a bin outgrew its region: the classic path
+                    periodic = False       # the positions are wrapped already (S2)
+                else:
+                    parts = [out[b * cap * rb:(b * cap + int(counts[b])) * rb]
+                             for b in range(self.nbins)]
+                    fparts = ([fo[b * cap:b * cap + int(counts[b])] for b in range(self.nbins)]
+                              if fo is not None else None)
+            except _lib.MgrError as e:
+                if "(-4)" not in str(e):      # MGR_EUNSUPPORTED: the classic path
+                    raise
+        if counts is None:
+            tile_rows, ws, dest = _scratch(n, self.nbins, rb, self._dev)
+            stream = _lib.stream_handle()
+            cnt_d = torch.empty(self.nbins, dtype=torch.int64, device=self._dev)
+            fid = fido = None
+            if fine_cells is None:
+                _lib.call("mgr_bin_count", self._plan.h, ctypes.c_void_p(pos.addr), pos.code, n,
+                          pos.stride, int(bool(periodic)), _lib.ptr(dest), tile_rows,
+                          _lib.ptr(ws), stream)
+            else:
+                fid = torch.empty(max(n, 1), dtype=torch.int16, device=self._dev)
+                fido = torch.empty(max(n, 1), dtype=torch.int16, device=self._dev)
+                _lib.call("mgr_bin_count_fine", self._plan.h, self._fine_plan(fine_cells).h,
+                          ctypes.c_void_p(pos.addr), pos.code, n, pos.stride, int(bool(periodic)),
+                          _lib.ptr(dest), _lib.ptr(fid), tile_rows, _lib.ptr(ws), stream)
+            pos.finish()
+            _lib.call("mgr_scan", n, self.nbins, tile_rows, _lib.ptr(ws), _lib.ptr(cnt_d), stream)
+            out = torch.empty(max(n * rb, 1), dtype=torch.uint8, device=self._dev)
+            _lib.call("mgr_pack_fields", 1, _ptrs([rows.flat.data_ptr()]), _i64s([rb]), n,
+                      _lib.ptr(dest), self.nbins, -1, tile_rows, _lib.ptr(ws),
+                      _ptrs([out.data_ptr()]), -1, None, _lib.ptr(fid), _lib.ptr(fido), None,
+                      0, -1, stream)
+            counts = cnt_d.cpu().numpy()
+            check_counts(counts, [])
+            st = np.concatenate([[0], np.cumsum(counts)])
+            parts = [out[int(st[b]) * rb:int(st[b + 1]) * rb] for b in range(self.nbins)]
+            fparts = ([fido[int(st[b]):int(st[b + 1])] for b in range(self.nbins)]
+                      if fine_cells is not None else None)
+        res = [rows.wrap(p, int(c)) for p, c in zip(parts, counts)]
+        if fine_cells is None:
+            return res
+        if isinstance(data, torch.Tensor) and data.is_cuda:
+            return res, fparts            # int16 tensors holding the uint16 cells
+        return res, [f.cpu().numpy().view(np.uint16) for f in fparts]
 
     def _fine_plan(self, fine_cells):
         key = tuple(int(x) for x in fine_cells)
