@@ -401,9 +401,9 @@ def main():
                     help="SoA payload: the fields as separate arrays moved by one multi-field "
                          "pack (config 5: pos f32 x3, vel f32 x3, mass f32, id i64; configs "
                          "2-4: pos f64 x3 + id i64); the position array is field 0")
-    ap.add_argument("--onepass", action="store_true",
-                    help="config 5 at one GPU: the source partition by the one-pass kernel "
-                         "(records read once, the send_buff list of per-destination regions)")
+    ap.add_argument("--classic", action="store_true",
+                    help="config 5 at one GPU: the source partition by bin + scan + pack (the "
+                         "records read twice) instead of the one-pass kernel")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="bare --gpus N > 1 (no WORLD_SIZE): seconds before the rank "
                          "processes are killed")
@@ -445,6 +445,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = args.config or (3 if multi else 2)
+    onepass = cfg == 5 and not multi and not args.soa and not args.classic
     chunks = args.chunks or None      # None: the product's own choice
     if multi and cfg == 2:
         cfg = 3
@@ -491,12 +492,25 @@ def main():
                 recv.reshape(-1), 36, rpos, fine_cells=[8, 8, 8])
             recv_fids = recv_fids.clone()
 
-            if args.onepass:
+            if not args.classic:
+                # the one-pass source partition (mgr_partition_onepass): every
+                # record read once, the output the send_buff list itself
+                # (redist.py:195-198: per-destination regions)
                 workload = workload.replace("_local_partition", "_onepass_partition")
 
+                last = {}
+
                 def step():
-                    part.partition_onepass_device(flat, 36, pos, fine_cells=[8, 8, 8])
+                    last["r"] = part.partition_onepass_device(flat, 36, pos, fine_cells=[8, 8, 8])
                     R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=recv_fids)
+
+                def onepass_check():
+                    # every bin fit its region (a count above cap would need the
+                    # classic redo, GridPartitioner.partition_lists)
+                    _, _, cnt, cap = last["r"]
+                    c = cnt.cpu().numpy()
+                    return {"bin_counts_max": int(c.max()), "region_rows": int(cap),
+                            "fits": bool((c >= 0).all() and (c <= cap).all())}
             else:
                 def step():
                     part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])
@@ -624,7 +638,7 @@ def main():
             if _lib.alg_read(k):   # host-counted bytes (the halo's selections)
                 kernels[k]["alg_bytes_per_launch"] = _lib.alg_read(k) / cnt
     missing = [k for k in list(row_bytes_per_kernel(cfg, bool(args.overload > 0),
-                                                    soa=args.soa, onepass=args.onepass)) + ["scan"]
+                                                    soa=args.soa, onepass=onepass)) + ["scan"]
                if k not in kernels]
     if missing:
         # detail pass (not timed): the kernels left out of the timed region
@@ -640,6 +654,7 @@ def main():
             if cnt:
                 kernels[k] = {"avg_ms": ms / cnt, "launches": cnt, "in_timed_region": False}
     _lib.profile_select(None)
+    onepass_info = onepass_check() if onepass else None
     # the count matrix's max/mean (load imbalance of the
     # redistribution: rows each destination receives, max over mean) -- the
     # N=1 line's 1 x 8 row of virtual destinations, or the N>1 ranks' count rows
@@ -716,7 +731,7 @@ def main():
     fine_tr = (int(_lib.load().mgr_ranked_tile_rows(12 if args.soa else 36, 512)) if cfg == 5
                else 2048)
     for k, b in row_bytes_per_kernel(cfg, bool(args.overload > 0), fine_tr, world=world,
-                                     soa=args.soa, onepass=args.onepass).items():
+                                     soa=args.soa, onepass=onepass).items():
         if k in kernels and "alg_bytes_per_launch" not in kernels[k]:   # host-counted first
             e = kernels[k]
             per_step = e["launches"] / e["steps"] if e.get("steps") else 1
@@ -765,6 +780,7 @@ def main():
             "rccl": rccl,
             "exchange_ab": exchange_ab,
             "n1_same_workload_ms": n1_same_ms,
+            "onepass": onepass_info,
             "count_skew": skew,
             "cpu_baseline": cpu,
             "cpu_baseline_cfg1": cpu_1,

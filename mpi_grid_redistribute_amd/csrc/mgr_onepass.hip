@@ -49,7 +49,7 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
     constexpr int WR = kOneWR, RPW = WR / 64, NW = kOneNW;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_cnt[NW][64];
-    __shared__ long long s_base[64];
+    __shared__ long long s_base[64], s_agg[64];
     __shared__ int s_tile, s_poison;
     OnePassCtl* ctl = (OnePassCtl*)(words + T * g.nbins);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -128,34 +128,56 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
     }
     s_cnt[w][lane] = cnt;
     __syncthreads();
-    // wave 0, lane b: the tile's count of bin b, published, then the earlier
-    // tiles' counts of b by look-back (each lane walks its own bin's chain)
-    if (w == 0) {
-        uint64_t poison = 0;
-        if (lane < nb) {
-            long long agg = 0;
+    // the tile's count of every bin, published at once (wave 0, lane b) so
+    // later tiles can look past this one before its prefix is known
+    if (w == 0 && lane < nb) {
+        long long agg = 0;
 #pragma unroll
-            for (int j = 0; j < NW; ++j) agg += s_cnt[j][lane];
-            uint64_t* my = words + tile * nb + lane;
-            long long excl = 0;
-            if (tile == 0) {
-                flag_store(my, kScanInc | (uint64_t)agg);
-            } else {
-                flag_store(my, kScanAgg | (uint64_t)agg);
-                for (int64_t j = tile - 1; j >= 0; --j) {
-                    const uint64_t v = flag_poll(words + j * nb + lane, 1, poison ? 0 : spins);
-                    excl += (long long)(v & kScanVal);
-                    if (v & kScanPoison) poison = kScanPoison;
-                    if ((v >> 62) >= 2) break;
-                }
-                flag_store(my, kScanInc | poison | (uint64_t)(excl + agg));
-            }
-            s_base[lane] = excl;
-            if (tile == T - 1) bin_counts[lane] = poison ? -1 : excl + agg;
+        for (int j = 0; j < NW; ++j) agg += s_cnt[j][lane];
+        s_agg[lane] = agg;
+        flag_store(words + tile * nb + lane, (tile == 0 ? kScanInc : kScanAgg) | (uint64_t)agg);
+    }
+    __syncthreads();
+    // the earlier tiles' counts of every bin, by wave 0: lane k * nbp + b
+    // reads bin b's word of tile base - k (nbp = bins rounded up to a power of
+    // two, a window of 64 / nbp tiles per bin and round trip: 8 for 8 bins),
+    // summing up to the nearest inclusive prefix.  (A/B, round 6: one wave per
+    // bin reading 64 tiles per round trip measured slower -- every look-back
+    // word is an agent-scope load past the XCD's L2 -- and one lane per bin
+    // polling one tile at a time too.)
+    if (w == 0) {
+        const int nbp = nb <= 1 ? 1 : 1 << (32 - __clz(nb - 1));
+        const int win = 64 / nbp;
+        const int bb = lane & (nbp - 1), k = lane / nbp;
+        unsigned long long grp = 0;   // the lanes of one bin: bits bb, bb + nbp, ...
+        for (int j = 0; j < win; ++j) grp |= 1ull << (j * nbp);
+        grp <<= bb;
+        bool done = bb >= nb || tile == 0;
+        long long excl = 0;
+        uint64_t poison = 0;
+        for (int64_t base = tile - 1;; base -= win) {
+            const int64_t idx = base - k;
+            uint64_t v = kScanInc;
+            if (!done && idx >= 0) v = flag_poll(words + idx * nb + bb, 1, poison ? 0 : spins);
+            const unsigned long long im = __ballot(!done && (v >> 62) >= 2) & grp;
+            const int first = im ? __ffsll((long long)im) - 1 : 64;   // nearest inclusive of my bin
+            const bool used = !done && lane <= first;
+            long long x = used ? (long long)(v & kScanVal) : 0;
+            if (__ballot(used && (v & kScanPoison)) & grp) poison = kScanPoison;
+            for (int o = nbp; o < 64; o <<= 1) x += __shfl_xor(x, o, 64);
+            excl += x;
+            if (im) done = true;
+            if (__ballot(!done) == 0ull) break;
         }
-        if (__ballot(poison != 0) && lane == 0) {
-            s_poison = 1;
-            __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0 && bb < nb) {
+            if (tile > 0)
+                flag_store(words + tile * nb + bb, kScanInc | poison | (uint64_t)(excl + s_agg[bb]));
+            s_base[bb] = excl;
+            if (tile == T - 1) bin_counts[bb] = poison ? -1 : excl + s_agg[bb];
+            if (poison) {
+                s_poison = 1;
+                __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
     __syncthreads();

@@ -176,6 +176,108 @@ __global__ __launch_bounds__(1024) void pack_coop_kernel(
     }
 }
 
+// Multi-field (SoA) pack in the cooperative shape of pack_coop_kernel, for
+// the common field signatures (compile time): one wave per 64-row round,
+// the round ranked ONCE for every field (ballot match, per-bin bases through
+// LDS behind one barrier), then every field's rows moved straight from
+// registers -- unit-transposed: lane l loads the W-byte units 64 k + l of
+// the field's round (each load instruction reads 64 W contiguous bytes), the
+// unit's row gets its slot by shfl, same-bin rows of a round land in
+// consecutive slots (contiguous runs that L2 merges with the neighbouring
+// rounds').  No LDS image: a few instructions per field and round, where the
+// image kernel (pack_fields_kernel) spends a permutation and a 16-byte unit
+// walk per field.  CF<U>: one field, U = W * 32 + UPR (UPR = row_bytes / W
+// units of W bytes), 0 = no field.
+template <int U>
+struct CoopField {
+    static constexpr int W = U >> 5, UPR = U & 31;
+    using T = typename Unit<(W ? W : 4)>::T;
+    T v[UPR ? UPR : 1];
+    __device__ __forceinline__ void load(const uint8_t* __restrict__ src, int64_t row0, int nr,
+                                         int lane) {
+        if constexpr (U != 0) {
+            const T* __restrict__ sp = (const T*)src + row0 * UPR;
+#pragma unroll
+            for (int k = 0; k < UPR; ++k)
+                if (64 * k + lane < nr * UPR) v[k] = sp[64 * k + lane];
+        }
+    }
+    // tgt: this lane's row's slot (bit 62: the redirect output), < 0: not written
+    __device__ __forceinline__ void store(uint8_t* __restrict__ dst, uint8_t* __restrict__ red,
+                                          long long tgt, int nr, int lane) const {
+        if constexpr (U != 0) {
+            T* __restrict__ d_u = (T*)dst;
+            T* __restrict__ r_u = (T*)red;
+#pragma unroll
+            for (int k = 0; k < UPR; ++k) {
+                const int u = 64 * k + lane;
+                const int r = u / UPR, part = u - r * UPR;
+                const long long t = __shfl(tgt, r, 64);
+                if (u < nr * UPR && t >= 0) {
+                    T* o = (t >> 62) ? r_u : d_u;
+                    o[(t & ((1ll << 62) - 1)) * UPR + part] = v[k];
+                }
+            }
+        }
+    }
+};
+
+struct CoopFieldPtrs {
+    const uint8_t* src[4];
+    uint8_t* dst[4];
+    uint8_t* red[4];
+};
+
+template <int U0, int U1, int U2, int U3>
+__global__ __launch_bounds__(1024) void pack_coop_fields_kernel(
+    CoopFieldPtrs fp, int64_t n, const uint8_t* __restrict__ dest, int nb, int nbits,
+    int drop_bin, const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts,
+    int64_t T, int64_t t0, int64_t tn, int tile_rows, int redirect_bin, int xcd,
+    const uint32_t* __restrict__ scan_err, const uint16_t* __restrict__ id_src,
+    uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red) {
+    __shared__ int s_cnt[kCoopMaxRounds][64];
+    const int w = threadIdx.x >> 6, lane = lane_id();
+    const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
+    const int64_t row0 = tile * (int64_t)tile_rows + 64 * w;
+    const int nr = (int)max((int64_t)0, min((int64_t)64, n - row0));
+    // the destination bytes first, waited for, then every field's loads
+    // (pack_coop_kernel: 0.77 vs 0.86 ms against issuing everything at once)
+    const unsigned b = lane < nr ? (unsigned)dest[row0 + lane] : 0u;
+    const unsigned idv = id_src && lane < nr ? (unsigned)id_src[row0 + lane] : 0u;
+    long long tbase = 0;
+    if (lane < nb) tbase = seg_start(offsets, bin_starts, T, tile, lane, redirect_bin);
+    CoopField<U0> f0;
+    CoopField<U1> f1;
+    CoopField<U2> f2;
+    CoopField<U3> f3;
+    f0.load(fp.src[0], row0, nr, lane);
+    f1.load(fp.src[1], row0, nr, lane);
+    f2.load(fp.src[2], row0, nr, lane);
+    f3.load(fp.src[3], row0, nr, lane);
+    // rank inside the round; lane l counts bin l
+    const bool valid = lane < nr;
+    unsigned long long pe = __ballot(valid), mine = pe;
+    for (int i = 0; i < nbits; ++i) {
+        const unsigned long long m = __ballot((b >> i) & 1u);
+        pe &= ((b >> i) & 1u) ? m : ~m;
+        mine &= ((lane >> i) & 1) ? m : ~m;
+    }
+    if (!valid) pe = 0ull;
+    s_cnt[w][lane] = __popcll(mine);
+    __syncthreads();
+    if (scan_failed(scan_err)) return;
+    for (int j = 0; j < w; ++j) tbase += s_cnt[j][lane];
+    const long long base = __shfl(tbase, (int)b, 64);
+    long long tgt = -1;
+    if (valid && (int)b != drop_bin)
+        tgt = (base + rank_in(pe)) | ((int)b == redirect_bin ? (1ll << 62) : 0ll);
+    if (id_src && tgt >= 0) ((tgt >> 62) ? id_red : id_dst)[tgt & ((1ll << 62) - 1)] = (uint16_t)idv;
+    f0.store(fp.dst[0], fp.red[0], tgt, nr, lane);
+    f1.store(fp.dst[1], fp.red[1], tgt, nr, lane);
+    f2.store(fp.dst[2], fp.red[2], tgt, nr, lane);
+    f3.store(fp.dst[3], fp.red[3], tgt, nr, lane);
+}
+
 // Multi-selection pack (the halo's sends, msel counts + mgr_scan with nbins
 // = nsets), up to kSelFields fields of the same rows in one launch.  Set k's
 // rows of field f go, in row order, to dsts[f][k] (null: set k is not
@@ -1227,10 +1329,10 @@ hipError_t launch_pack_ranked(const void* src, int64_t row_bytes, int64_t n, con
     if (lds > 160 * 1024) return hipErrorNotSupported;
     prof_begin(s, K_PACK_FINE);
     hipError_t e = hipErrorNotSupported;
-    // as many resident workgroups per CU as the tile image lets the LDS hold
-    // (36-byte rows: one; the 4..16-byte fields of a SoA payload: two to four)
-    const int per_cu = max(1, min(4, (160 * 1024) / lds));
-    int64_t grid = ((int64_t)device_cus() * per_cu + 7) / 8 * 8;
+    // one persistent workgroup per CU (A/B, round 6: as many per CU as the LDS
+    // holds -- two to four for the 4..12-byte fields of a SoA payload --
+    // measured slower, 0.41 vs 0.36 ms per field launch at 64M rows)
+    int64_t grid = ((int64_t)device_cus() + 7) / 8 * 8;
     const int64_t need = (ws.T + 7) / 8 * 8;
     if (grid > need) grid = need;
 #define MGR_PRT(RB_, TR_)                                                                     \
@@ -1345,6 +1447,53 @@ hipError_t launch_pack(const void* src, int64_t row_bytes, int64_t n, const void
                             redirect_bin, ids_red, s, nullptr);
 }
 
+// The cooperative multi-field kernel for a field signature it is built for
+// (hipErrorNotSupported otherwise): each field's unit width -- the widest of
+// 16/8/4 bytes dividing its row and every pointer -- and units per row.
+static int coop_unit(const void* src, int64_t rb, const void* dst, const void* red) {
+    uintptr_t a = (uintptr_t)src | (uintptr_t)dst | (uintptr_t)rb;
+    if (red) a |= (uintptr_t)red;
+    const int W = (a & 15) == 0 ? 16 : (a & 7) == 0 ? 8 : (a & 3) == 0 ? 4 : 0;
+    if (!W || rb / W > 16) return -1;
+    return W * 32 + (int)(rb / W);
+}
+
+static hipError_t pack_coop_fields(int nf, const void* const* srcs, const int64_t* row_bytes,
+                                   int64_t n, const void* dest, int nbins, int drop_bin,
+                                   int tile_rows, const Workspace& ws, void* const* dsts,
+                                   int redirect_bin, void* const* reds, hipStream_t s,
+                                   const uint16_t* ids_src, uint16_t* ids_dst, uint16_t* ids_red) {
+    int u[4] = {0, 0, 0, 0};
+    CoopFieldPtrs fp{};
+    for (int f = 0; f < nf; ++f) {
+        u[f] = coop_unit(srcs[f], row_bytes[f], dsts[f], reds ? reds[f] : nullptr);
+        if (u[f] < 0) return hipErrorNotSupported;
+        fp.src[f] = (const uint8_t*)srcs[f];
+        fp.dst[f] = (uint8_t*)dsts[f];
+        fp.red[f] = reds ? (uint8_t*)reds[f] : nullptr;
+    }
+    auto sig = [&](int a, int b, int c, int d) { return u[0] == a && u[1] == b && u[2] == c && u[3] == d; };
+    constexpr int F4x1 = 4 * 32 + 1, F4x3 = 4 * 32 + 3, F8x1 = 8 * 32 + 1, F8x3 = 8 * 32 + 3,
+                  F16x2 = 16 * 32 + 2, F4x9 = 4 * 32 + 9, F16x1 = 16 * 32 + 1, F8x2 = 8 * 32 + 2;
+    const int threads = tile_rows;   // one wave per 64-row round
+#define MGR_PCF(A, B, C, D)                                                                          {                                                                                                    prof_begin(s, K_PACK);                                                                           hipLaunchKernelGGL((pack_coop_fields_kernel<A, B, C, D>), dim3((unsigned)ws.tn),                                     dim3(threads), 0, s, fp, n, (const uint8_t*)dest, nbins,                                          nbits_for(nbins), drop_bin, ws.offsets, ws.bin_starts, ws.T, ws.t0,                               ws.tn, tile_rows, redirect_bin, kXcdPackChunk, ws.scan_err, ids_src,                              ids_dst, ids_red);                                                             prof_end(s, K_PACK);                                                                             return hipGetLastError();                                                                    }
+    // config 5's fields as arrays: pos f32 x3, vel f32 x3, mass f32, id i64
+    if (sig(F4x3, F4x3, F4x1, F8x1)) MGR_PCF(F4x3, F4x3, F4x1, F8x1)
+    // f64 positions + i64 ids; 32-byte records + their f64 positions (return_positions)
+    if (sig(F8x3, F8x1, 0, 0)) MGR_PCF(F8x3, F8x1, 0, 0)
+    if (sig(F16x2, F8x3, 0, 0)) MGR_PCF(F16x2, F8x3, 0, 0)
+    // 36-byte records + their f32 positions (config 5 with return_positions)
+    if (sig(F4x9, F4x3, 0, 0)) MGR_PCF(F4x9, F4x3, 0, 0)
+    // positions f32 x3 + ids i64 / f64 x2 + i64
+    if (sig(F4x3, F8x1, 0, 0)) MGR_PCF(F4x3, F8x1, 0, 0)
+    if (sig(F16x1, F8x1, 0, 0)) MGR_PCF(F16x1, F8x1, 0, 0)
+    if (sig(F8x3, F8x3, F8x1, 0)) MGR_PCF(F8x3, F8x3, F8x1, 0)
+    if (sig(F4x3, F4x3, F8x1, 0)) MGR_PCF(F4x3, F4x3, F8x1, 0)
+    if (sig(F8x2, F8x1, 0, 0)) MGR_PCF(F8x2, F8x1, 0, 0)
+#undef MGR_PCF
+    return hipErrorNotSupported;
+}
+
 // mgr_pack_fields: several fields of the same rows, one ranking.  With one
 // field this is launch_pack (the coop / image kernels A/B'd for it).  With
 // more, the fields pack_fields_kernel takes (4-byte-multiple rows, 16-byte
@@ -1381,6 +1530,15 @@ hipError_t launch_pack_fields(int nf, const void* const* srcs, const int64_t* ro
         fast.clear();
     }
     bool side_done = ids_src == nullptr;
+    if (!h.fields_image && fast.size() == (size_t)nf && nf <= 4 &&
+        tile_rows <= 64 * kCoopMaxRounds && tile_rows / 64 <= 16) {
+        // every field in the cooperative multi-field kernel when the fields'
+        // signature is one it is built for
+        const hipError_t e = pack_coop_fields(nf, srcs, row_bytes, n, dest, nbins, drop_bin,
+                                              tile_rows, ws, dsts, redirect_bin, reds, s, ids_src,
+                                              ids_dst, ids_red);
+        if (e != hipErrorNotSupported) return e;
+    }
     size_t i = 0;
     while (i < fast.size()) {
         PackFieldsArgs fa{};

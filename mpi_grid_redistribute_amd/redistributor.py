@@ -197,13 +197,21 @@ def _results(fields, outs, m, multi):
 MAX_FIELDS = 16   # mgr.h MGR_MAX_FIELDS
 
 
+# The row size the tile policy sizes multi-field packs for: the cooperative
+# pack's 32-byte rows (512-row tiles up to 16 bins, 1024 up to 64).  A/B,
+# round 6, config 5's four arrays at 64M rows (profiles/round6/soa_ab.json):
+# 1.25 ms at 512-row tiles against 1.39 / 1.39 ms at 256 / 1024 (the LDS-image
+# kernel: 1.38-1.44 ms at 512-2048).
+_FIELDS_TILE_HINT = 32
+
+
 def _tile_hint(row_bytes, side=None):
     """The row size the tile policy (mgr_tile_rows) sizes tiles for: one
-    field's row bytes, or -- when several fields move together through the
-    multi-field kernel -- their sum (the bytes a tile of rows moves); a 2-byte
-    side field (index ``side``) rides along and does not count."""
+    field's row bytes, or _FIELDS_TILE_HINT when several fields move together
+    through the multi-field kernels; a 2-byte side field (index ``side``)
+    rides along and does not count."""
     rb = [int(b) for i, b in enumerate(row_bytes) if i != side]
-    return max(sum(rb) if len(rb) > 1 else max(rb + [1]), 1)
+    return _FIELDS_TILE_HINT if len(rb) > 1 else max(rb + [1])
 
 
 def _ptrs(addrs):

@@ -161,17 +161,30 @@ def _field_set(kind, n, rng):
         return [rng.integers(0, 1 << 30, (n, 1 + i % 4)).astype(np.int32) for i in range(10)]
     if kind == "big":        # rows too wide for one launch's LDS together
         return [rng.integers(0, 1 << 30, (n, 32)).astype(np.int32) for _ in range(4)]
+    if kind == "pos_id":     # configs 2-4 as arrays: f64 positions + i64 ids
+        return [rng.normal(size=(n, 3)), np.arange(n, dtype=np.int64)]
     if kind == "unaligned":  # a 12-byte field starting 4 bytes into its buffer
         base = rng.integers(0, 1 << 30, (n * 3 + 1,)).astype(np.int32)
         return [base, rng.normal(size=(n, 3)).astype(np.float32)]
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["cfg5", "wide", "narrow", "many", "big", "unaligned"])
+@pytest.mark.parametrize("image", [0, 1])
+@pytest.mark.parametrize("kind", ["cfg5", "wide", "narrow", "many", "big", "unaligned", "pos_id"])
 @pytest.mark.parametrize("topo", [[2, 2, 2], [4, 4, 4], [2, 3, 1], [1]])
-def test_partition_fields_vs_c_oracle(kind, topo):
+def test_partition_fields_vs_c_oracle(kind, topo, image):
     """GridPartitioner.partition_by_position with a tuple payload == the C
-    oracle's partition of every field by the same destinations."""
+    oracle's partition of every field by the same destinations -- through the
+    cooperative multi-field kernel (the signatures it is built for) and, test
+    hook fields_image, the LDS-image kernel for the same fields."""
+    _lib.test_hook("fields_image", image)
+    try:
+        _partition_fields_case(kind, topo)
+    finally:
+        _lib.test_hook("fields_image", 0)
+
+
+def _partition_fields_case(kind, topo):
     rng = np.random.default_rng(len(kind) * 7 + sum(topo))
     n = 300_007
     dim = len(topo)
