@@ -18,13 +18,14 @@ import pmc_summary  # noqa: E402
 
 SRC, DST = sys.argv[1], sys.argv[2]
 TRAFFIC = "profiles/traffic.json"
-LINES = ("cfg2", "cfg4", "cfg5", "cfg3x", "halo")
+LINES = ("cfg2", "cfg4", "cfg5", "cfg5classic", "cfg5soa", "cfg2soa", "cfg3x", "halo")
 # rocprof kernel short name -> bench profiler name
 NAMES = {"bin_count_kernel": "bin_count", "pack_coop_kernel": "pack", "pack_img_kernel": "pack",
          "pack_kernel": "pack", "pack_ranked_kernel": "pack_fine", "pack_fine_kernel": "pack_fine",
          "rank_ids_kernel": "count_ids", "count_ids_kernel": "count_ids",
          "msel_pack_kernel": "halo_pack", "msel_count_kernel": "halo",
-         "scan_onepass_kernel": "scan"}
+         "scan_onepass_kernel": "scan", "pack_fields_kernel": "pack",
+         "pack_coop_fields_kernel": "pack", "onepass_partition_kernel": "onepass"}
 
 
 def bench_line(log):

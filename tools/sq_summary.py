@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """SQ/TA/TCC counter summary of the bench lines (profiles/<round>/sq_summary.md).
 
-Input: the rocprofv3 --pmc passes of scripts/gpu_pmc_cfg2.sh, gpu_pmc_cfg5.sh
-and gpu_pmc_halo.sh (gpurun_out/pmc2, pmc5, pmch: pass*_counter_collection.csv)
+Input: the rocprofv3 --pmc passes of scripts/gpu_pmc.sh (OUT=<line>
+PASSES=sq: gpurun_out/pmc_<line>/pass*_counter_collection.csv)
 and the bench JSON lines that tools/round_profiles.py copied next to the
 output (<line>_bench.json: algorithmic bytes per launch of each kernel).
 Per kernel and dispatch: wave cycles, the share of them spent waiting
@@ -24,10 +24,13 @@ import pmc_summary  # noqa: E402
 NAMES = {"bin_count_kernel": "bin_count", "pack_coop_kernel": "pack", "pack_img_kernel": "pack",
          "pack_kernel": "pack", "pack_ranked_kernel": "pack_fine", "rank_ids_kernel": "count_ids",
          "count_ids_kernel": "count_ids", "msel_pack_kernel": "halo_pack",
-         "msel_count_kernel": "halo", "scan_onepass_kernel": "scan"}
+         "msel_count_kernel": "halo", "scan_onepass_kernel": "scan", "pack_fields_kernel": "pack",
+         "pack_coop_fields_kernel": "pack", "onepass_partition_kernel": "onepass"}
 
 SRC, DST = sys.argv[1], sys.argv[2]
-LINES = (("cfg2", "pmc2"), ("cfg5", "pmc5"), ("halo", "pmch"))
+# scripts/gpu_pmc.sh OUT=<line> PASSES=sq writes gpurun_out/pmc_<line>/
+LINES = tuple((ln, f"pmc_{ln}") for ln in ("cfg2", "cfg5", "cfg5classic", "cfg5soa", "cfg2soa",
+                                           "halo"))
 
 
 def main():
@@ -48,7 +51,8 @@ def main():
                 continue   # this library's kernels only (not the input generators, torch, RCCL)
             wc = c["SQ_WAVE_CYCLES"]
             rd, wr = c.get("SQ_INSTS_VMEM_RD", 0.0), c.get("SQ_INSTS_VMEM_WR", 0.0)
-            name = "bin_fine" if (line, k) == ("cfg5", "bin_count_kernel") else NAMES.get(k, "")
+            name = ("bin_fine" if line.startswith("cfg5") and k == "bin_count_kernel"
+                    else NAMES.get(k, ""))
             alg = bench.get(name, {}).get("alg_bytes_per_launch")
             bpi = f"{alg / (rd + wr):.0f}" if alg and rd + wr else "--"
             lds = c.get("SQ_ACTIVE_INST_LDS", 0.0)
@@ -59,7 +63,7 @@ def main():
     os.makedirs(DST, exist_ok=True)
     with open(os.path.join(DST, "sq_summary.md"), "w") as f:
         f.write("# SQ counter summary (per dispatch, rocprofv3 --pmc, 3 passes per line; "
-                "scripts/gpu_pmc_cfg2.sh, gpu_pmc_cfg5.sh, gpu_pmc_halo.sh)\n\n")
+                "scripts/gpu_pmc.sh PASSES=sq)\n\n")
         f.write("\n".join(out) + "\n")
     print("\n".join(out))
 
