@@ -30,8 +30,10 @@ extern "C" {
  * the scan's last chunk, -1 = scan_spins; 0 = one look, which then reports
  * the forced race as a failed scan), "scan_poison_chunk" (the scan chunk with
  * this ticket publishes its prefix poisoned: a deterministic failed scan,
- * -1 = none), "fields_image" (1: multi-field packs take the LDS-image kernel
- * for every field signature, not the cooperative one).  Each call publishes a new immutable
+ * -1 = none), "fields_kernel" (multi-field packs: 0 the product's choice,
+ * 1 the per-wave LDS-image kernel, 2 the tile-image kernel, 3 the
+ * cooperative kernel -- each where it takes the fields, else the next).
+ * Each call publishes a new immutable
  * snapshot of every hook (the library's launches read one snapshot each);
  * < 0 for an unknown key or an out-of-range value.                         */
 int mgr_test_hook(const char* key, int64_t value);

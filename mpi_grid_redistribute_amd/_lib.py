@@ -193,7 +193,7 @@ HOOK_DEFAULTS = {"tile_rounds": 0, "scan_chunk": 2048, "scan_max_chunks": 1024,
                  "scan_spins": 1 << 24, "pack_img_all": 0, "rank_rows": 0, "bin_unstaged": 0,
                  "bin_generic": 0, "pack_generic": 0, "scan_delay_bin": -1,
                  "scan_delay_sleeps": 0, "scan_end_spins": -1, "scan_poison_chunk": -1,
-                 "fields_image": 0}
+                 "fields_kernel": 0}
 
 
 # --------------------------------------------------------------- profiler

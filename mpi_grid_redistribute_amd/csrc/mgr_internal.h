@@ -183,7 +183,8 @@ struct Hooks {
     int scan_delay_sleeps = 0;
     int scan_end_spins = -1;
     int scan_poison_chunk = -1;   // >= 0: that scan chunk publishes poisoned (a failed scan)
-    int fields_image = 0;         // multi-field packs: the LDS-image kernel for every signature
+    int fields_kernel = 0;        // multi-field packs: 0 product choice, 1 per-wave image,
+                                  // 2 tile image, 3 cooperative (where they take the fields)
 };
 // The scan kernel's copy of the race-test hooks (kernel argument).
 struct ScanTest {

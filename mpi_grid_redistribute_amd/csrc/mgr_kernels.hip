@@ -57,7 +57,7 @@ int set_hook(const char* key, int64_t v) {
     else if (!strcmp(key, "scan_delay_sleeps") && in(0, 1 << 16)) h->scan_delay_sleeps = (int)v;
     else if (!strcmp(key, "scan_end_spins") && in(-1, 1 << 30)) h->scan_end_spins = (int)v;
     else if (!strcmp(key, "scan_poison_chunk") && in(-1, 1 << 30)) h->scan_poison_chunk = (int)v;
-    else if (!strcmp(key, "fields_image") && in(0, 1)) h->fields_image = (int)v;
+    else if (!strcmp(key, "fields_kernel") && in(0, 3)) h->fields_kernel = (int)v;
     else return -1;
     g_hooks.store(h.get(), std::memory_order_release);
     kept.push_back(std::move(h));

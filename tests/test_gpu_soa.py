@@ -169,19 +169,19 @@ def _field_set(kind, n, rng):
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("image", [0, 1])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
 @pytest.mark.parametrize("kind", ["cfg5", "wide", "narrow", "many", "big", "unaligned", "pos_id"])
 @pytest.mark.parametrize("topo", [[2, 2, 2], [4, 4, 4], [2, 3, 1], [1]])
-def test_partition_fields_vs_c_oracle(kind, topo, image):
+def test_partition_fields_vs_c_oracle(kind, topo, kernel):
     """GridPartitioner.partition_by_position with a tuple payload == the C
     oracle's partition of every field by the same destinations -- through the
-    cooperative multi-field kernel (the signatures it is built for) and, test
-    hook fields_image, the LDS-image kernel for the same fields."""
-    _lib.test_hook("fields_image", image)
+    per-wave LDS-image, the tile-image and the cooperative multi-field kernels
+    (test hook fields_kernel; each where it takes the fields)."""
+    _lib.test_hook("fields_kernel", kernel)
     try:
         _partition_fields_case(kind, topo)
     finally:
-        _lib.test_hook("fields_image", 0)
+        _lib.test_hook("fields_kernel", 0)
 
 
 def _partition_fields_case(kind, topo):

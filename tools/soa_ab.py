@@ -47,11 +47,11 @@ def main():
     fplan = P._fine_plan([8, 8, 8])
     s = _lib.stream_handle()
     out = {}
-    variants = json.loads(os.environ.get("AB_VARIANTS", '[[0, 0], [8, 0], [8, 1], [16, 0], [16, 1]]'))
+    variants = json.loads(os.environ.get("AB_VARIANTS", '[[0, 0], [8, 2], [16, 2], [8, 3], [8, 1]]'))
     for rounds, img in variants:
-        label = f"rounds{rounds}_img{img}"
+        label = f"rounds{rounds}_kernel{img}"
         _lib.test_hook("tile_rounds", rounds)
-        _lib.test_hook("fields_image", img)
+        _lib.test_hook("fields_kernel", img)
         tr, ws, dest = _scratch(N, 8, 36, torch.device("cuda"))
         counts = torch.empty(8, dtype=torch.int64, device="cuda")
         fid = torch.empty(N, dtype=torch.int16, device="cuda")
@@ -96,7 +96,7 @@ def main():
         out[label]["fields_equal_perfield"] = all(torch.equal(a, b) for a, b in zip(ref, outs))
         del outs, o36
     _lib.test_hook("tile_rounds", 0)
-    _lib.test_hook("fields_image", 0)
+    _lib.test_hook("fields_kernel", 0)
     # destination side: ranked pack per field vs the 36-byte record
     ids = fido[:N]
     R1 = mgr.MPIGridRedistributor(None, [1, 1, 1], [0.5] * 3)
