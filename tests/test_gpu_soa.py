@@ -226,6 +226,34 @@ def test_pack_fields_tile_shapes(tile_rounds):
         assert np.array_equal(_bytes(got[i]), _bytes(exp)), i
 
 
+@pytest.mark.parametrize("kind", ["cfg5", "wide", "narrow", "many", "big", "pos_id",
+                                  "cfg5_3", "pair"])
+@pytest.mark.parametrize("nfine", [[8, 8, 8], [4, 4, 4], [3, 5, 7]])
+def test_fine_sort_fields_vs_stable_sort(kind, nfine):
+    """MPIGridRedistributor.fine_cell_sort of a SoA payload by given fine ids
+    == numpy's stable argsort of the ids applied to every field (one rank +
+    scan, the ranked pack per field; the generic pack for rows it does not
+    take), with a partial last tile."""
+    rng = np.random.default_rng(len(kind) * 11 + sum(nfine))
+    n = 250_007
+    base = "cfg5" if kind in ("cfg5_3", "pair") else kind
+    fl = _field_set(base, n, rng)
+    if kind == "cfg5_3":
+        fl = fl[:3]             # pos, vel, mass: the (3, 3, 1) signature
+    elif kind == "pair":
+        fl = [fl[2], fl[2].copy()]   # two 4-byte fields: (1, 1)
+    nb = int(np.prod(nfine))
+    ids = rng.integers(0, nb, n).astype(np.uint16)
+    order = np.argsort(ids, kind="stable")
+    R = MPIGridRedistributor(None, [1, 1, 1], [1.0] * 3)
+    t = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in fl]
+    pos = torch.zeros((n, 3), dtype=torch.float32, device="cuda")
+    got, off = R.fine_cell_sort(t, pos, nfine, fine_ids=torch.from_numpy(ids.view(np.int16)).cuda())
+    assert np.array_equal(np.diff(off.cpu().numpy()), np.bincount(ids, minlength=nb))
+    for i, x in enumerate(fl):
+        assert np.array_equal(_bytes(got[i]), _bytes(np.ascontiguousarray(x)[order])), (kind, i)
+
+
 def test_partition_fields_device_cfg5_fine():
     """The bench's SoA config-5 source step (partition_fields_device with
     fine cells): every field partitioned, the fine ids beside them, equal to

@@ -105,6 +105,25 @@ def main():
     out["dest_sort_soa"] = timed(lambda: R1.fine_cell_sort(dst_soa, dst_soa[0], [8, 8, 8],
                                                            fine_ids=ids))
     out["dest_sort_aos"] = timed(lambda: R1.fine_cell_sort(drec, dpos, [8, 8, 8], fine_ids=ids))
+    # the dest sort's kernels (library HIP events): a ranked pack launch per
+    # field against the 36-byte record's one
+    for label, fn in (("soa", lambda: R1.fine_cell_sort(dst_soa, dst_soa[0], [8, 8, 8],
+                                                       fine_ids=ids)),
+                      ("aos", lambda: R1.fine_cell_sort(drec, dpos, [8, 8, 8], fine_ids=ids))):
+        fn()
+        torch.cuda.synchronize()
+        _lib.profile_enable(True)
+        _lib.profile_reset()
+        for _ in range(ITERS):
+            fn()
+        torch.cuda.synchronize()
+        rec_k = {}
+        for k in ("count_ids", "scan", "pack_fine"):
+            ms, cnt = _lib.profile_read(k)
+            if cnt:
+                rec_k[k] = {"ms_per_call": round(ms / ITERS, 4), "launches_per_call": cnt / ITERS}
+        _lib.profile_enable(False)
+        out[f"dest_kernels_{label}"] = rec_k
     print(json.dumps(out), flush=True)
 
 
