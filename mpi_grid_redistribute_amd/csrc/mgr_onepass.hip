@@ -40,16 +40,19 @@ int64_t onepass_workspace_bytes(int64_t n, int nbins) {
     return (onepass_tiles(n) * (int64_t)nbins) * 8 + (int64_t)sizeof(OnePassCtl) + 8;
 }
 
-template <typename PosT, bool kP, int SIDE, int GEO>
-__global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
+static int onepass_lds_bytes(int nw, int rb, int nb) {
+    const int nbe = (nb + 1) & ~1;
+    return nw * (kOneWR * rb + 8 * nbe + 2 * kOneWR) + 16 * nbe + 4 * nw * nb;
+}
+
+template <typename PosT, bool kP, int SIDE, int GEO, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8))) void onepass_partition_kernel(
     uint8_t* __restrict__ data, int rb, int pos_off, int64_t n, Geom g, FineGeom fg,
     uint8_t* __restrict__ out, uint16_t* __restrict__ fine_out, int64_t cap,
     int64_t* __restrict__ bin_counts, uint64_t* __restrict__ words, int64_t T, int spins,
     int write_all) {
-    constexpr int WR = kOneWR, RPW = WR / 64, NW = kOneNW;
+    constexpr int WR = kOneWR, RPW = WR / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_cnt[NW][64];
-    __shared__ long long s_base[64], s_agg[64];
     __shared__ int s_tile, s_poison;
     OnePassCtl* ctl = (OnePassCtl*)(words + T * g.nbins);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
@@ -61,13 +64,23 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
     }
     __syncthreads();
     const int64_t tile = s_tile;
-    const int wave_lds = WR * rb + 64 * 16 + 2 * WR;   // rows, then gaddr, rowoff, inv, ibin
+    // LDS (onepass_lds_bytes): per wave its rows, the bins' output addresses,
+    // the inverse permutation and the slots' bins; then the waves' bin counts
+    // and the tile's bases and counts -- sized by the bins, so 8-bin 36-byte
+    // rows take < 40 KiB and, with <= 64 VGPRs (amdgpu_waves_per_eu(8)), four
+    // workgroups fit a CU: a tile waiting on its look-back leaves three to keep
+    // memory busy (A/B, 64M config-5 rows: 1.19-1.20 ms against 1.39 with the
+    // 64-entry tables and three per CU; 512-row tiles, eight per CU: 1.60)
+    const int nbe = (nb + 1) & ~1;
+    const int wave_lds = WR * rb + 8 * nbe + 2 * WR;
     uint8_t* wl = smem + w * wave_lds;
     unsigned long long* gaddr = (unsigned long long*)(wl + WR * rb);   // WR * rb: a multiple of 512
-    long long* rowoff = (long long*)(gaddr + 64);
-    uint8_t* inv = (uint8_t*)(rowoff + 64);
+    uint8_t* inv = (uint8_t*)(gaddr + nbe);
     uint8_t* ibin = inv + WR;
-    const int64_t row0 = tile * (int64_t)kOneTile + (int64_t)WR * w;
+    long long* s_base = (long long*)(smem + NW * wave_lds);
+    long long* s_agg = s_base + nbe;
+    int* s_cnt = (int*)(s_agg + nbe);   // [NW][nb]
+    const int64_t row0 = tile * (int64_t)(WR * NW) + (int64_t)WR * w;
     const int nrows = __builtin_amdgcn_readfirstlane(
         (int)max((int64_t)0, min((int64_t)WR, n - row0)));
     const int nbytes = nrows * rb;
@@ -126,14 +139,14 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
         cq[q] = __popcll(mine);
         cnt += cq[q];
     }
-    s_cnt[w][lane] = cnt;
+    if (lane < nb) s_cnt[w * nb + lane] = cnt;
     __syncthreads();
     // the tile's count of every bin, published at once (wave 0, lane b) so
     // later tiles can look past this one before its prefix is known
     if (w == 0 && lane < nb) {
         long long agg = 0;
 #pragma unroll
-        for (int j = 0; j < NW; ++j) agg += s_cnt[j][lane];
+        for (int j = 0; j < NW; ++j) agg += s_cnt[j * nb + lane];
         s_agg[lane] = agg;
         flag_store(words + tile * nb + lane, (tile == 0 ? kScanInc : kScanAgg) | (uint64_t)agg);
     }
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
     long long tbase = 0;
     if (lane < nb) {
         tbase = s_base[lane];
-        for (int j = 0; j < w; ++j) tbase += s_cnt[j][lane];
+        for (int j = 0; j < w; ++j) tbase += s_cnt[j * nb + lane];
     }
     const int excl = wave_incl_dpp(cnt) - cnt;   // the bins' image starts (bin-major)
     int run = excl;
@@ -209,7 +222,6 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
     // and redoes the partition)
     const long long ro = tbase - excl;
     if (lane < nb) {
-        rowoff[lane] = ro;
         gaddr[lane] = tbase + cnt > cap ? 0ull
                       : (unsigned long long)(out + ((int64_t)lane * cap + ro) * rb);
     }
@@ -249,17 +261,19 @@ __global__ __launch_bounds__(kOneNW * 64) void onepass_partition_kernel(
 template <typename PosT, bool kP, int SIDE>
 static hipError_t onepass_t(const Geom& g, const FineGeom& fg, void* data, int rb, int pos_off,
                             int64_t n, void* out, uint16_t* fine_out, int64_t cap,
-                            int64_t* bin_counts, uint64_t* words, int64_t T, hipStream_t s) {
+                            int64_t* bin_counts, uint64_t* words, hipStream_t s) {
     const Hooks& h = hooks();   // one snapshot for the launch
-    auto k = onepass_partition_kernel<PosT, kP, SIDE, kGeoAny>;
+    constexpr int NW = kOneNW;
+    auto k = onepass_partition_kernel<PosT, kP, SIDE, kGeoAny, NW>;
     if constexpr (kP) {
         const int geo = h.bin_generic ? kGeoAny : geo_kind(g, sizeof(PosT) == 4);
-        if (geo == kGeoF32) k = onepass_partition_kernel<PosT, kP, SIDE, kGeoF32>;
-        else if (geo == kGeoF64) k = onepass_partition_kernel<PosT, kP, SIDE, kGeoF64>;
+        if (geo == kGeoF32) k = onepass_partition_kernel<PosT, kP, SIDE, kGeoF32, NW>;
+        else if (geo == kGeoF64) k = onepass_partition_kernel<PosT, kP, SIDE, kGeoF64, NW>;
     }
-    const int lds = kOneNW * (kOneWR * rb + 64 * 16 + 2 * kOneWR);
+    const int64_t T = onepass_tiles(n);
+    const int lds = onepass_lds_bytes(NW, rb, g.nbins);
     ensure_lds(k, lds);
-    hipLaunchKernelGGL(k, dim3((unsigned)T), dim3(64 * kOneNW), (size_t)lds, s, (uint8_t*)data, rb,
+    hipLaunchKernelGGL(k, dim3((unsigned)T), dim3(64 * NW), (size_t)lds, s, (uint8_t*)data, rb,
                        pos_off, n, g, fg, (uint8_t*)out, fine_out, cap, bin_counts, words, T,
                        h.scan_spins, g.write_back_all);
     return hipGetLastError();
@@ -268,14 +282,14 @@ static hipError_t onepass_t(const Geom& g, const FineGeom& fg, void* data, int r
 template <typename PosT>
 static hipError_t onepass_d(const Geom& g, const FineGeom* fg, void* data, int rb, int pos_off,
                             int64_t n, int periodic, void* out, uint16_t* fine_out, int64_t cap,
-                            int64_t* bin_counts, uint64_t* words, int64_t T, hipStream_t s) {
+                            int64_t* bin_counts, uint64_t* words, hipStream_t s) {
     FineGeom f{};
     if (fg) f = *fg;
     if (periodic)
-        return fg ? onepass_t<PosT, true, kSideFine>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, T, s)
-                  : onepass_t<PosT, true, kSideNone>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, T, s);
-    return fg ? onepass_t<PosT, false, kSideFine>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, T, s)
-              : onepass_t<PosT, false, kSideNone>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, T, s);
+        return fg ? onepass_t<PosT, true, kSideFine>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, s)
+                  : onepass_t<PosT, true, kSideNone>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, s);
+    return fg ? onepass_t<PosT, false, kSideFine>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, s)
+              : onepass_t<PosT, false, kSideNone>(g, f, data, rb, pos_off, n, out, fine_out, cap, bin_counts, words, s);
 }
 
 hipError_t launch_onepass(const Geom& g, const FineGeom* fg, void* data, int64_t row_bytes,
@@ -288,16 +302,15 @@ hipError_t launch_onepass(const Geom& g, const FineGeom* fg, void* data, int64_t
         row_bytes > 128 || pos_off < 0 || pos_off % psz || pos_off + 3 * psz > row_bytes ||
         ((uintptr_t)data & 15) || ((uintptr_t)out & 3) || ((uintptr_t)fine_out & 1) || cap < 0)
         return hipErrorNotSupported;
-    const int64_t T = onepass_tiles(n);
     if (n <= 0) return hipMemsetAsync(bin_counts, 0, (size_t)g.nbins * 8, s);
     uint64_t* words = (uint64_t*)workspace;
     hipError_t e = hipMemsetAsync(words, 0, (size_t)onepass_workspace_bytes(n, g.nbins), s);
     if (e != hipSuccess) return e;
     prof_begin(s, K_ONEPASS);
     e = psz == 4 ? onepass_d<float>(g, fg, data, (int)row_bytes, (int)pos_off, n, periodic, out,
-                                    fine_out, cap, bin_counts, words, T, s)
+                                    fine_out, cap, bin_counts, words, s)
                  : onepass_d<double>(g, fg, data, (int)row_bytes, (int)pos_off, n, periodic, out,
-                                     fine_out, cap, bin_counts, words, T, s);
+                                     fine_out, cap, bin_counts, words, s);
     prof_end(s, K_ONEPASS);
     return e;
 }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Config-5 kernel A/B (GPU): per-kernel HIP-event times of the source-side
 partition of 64M 36-byte records with and without the fine-cell side field,
-and of the destination-side fine sort, for test-hook variants
+the one-pass partition (mgr_partition_onepass) and the destination-side
+fine sort, for test-hook variants
 (CF5_VARIANTS, JSON list, include/mgr_instrument.h; CF5_REPEAT interleaved
 repeats).  Library builds are compared by scripts/gpu_libs_ab.sh."""
 import json
@@ -16,7 +17,8 @@ from mpi_grid_redistribute_amd import _lib  # noqa: E402
 
 N = int(os.environ.get("CF5_N", 1 << 26))
 ITERS = int(os.environ.get("CF5_ITERS", 10))
-KERNELS = ("bin_count", "bin_fine", "scan", "pack", "count_ids", "pack_fine", "pack_narrow")
+KERNELS = ("bin_count", "bin_fine", "scan", "pack", "count_ids", "pack_fine", "pack_narrow",
+           "onepass")
 
 
 def timed(fn):
@@ -61,6 +63,8 @@ def main():
             res = {"variant": v,
                    "src_plain": timed(lambda: part.partition_device(flat, 36, pos)),
                    "src_fine": timed(lambda: part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])),
+                   "src_onepass": timed(lambda: part.partition_onepass_device(
+                       flat, 36, pos, fine_cells=[8, 8, 8])),
                    "dst_sort": timed(lambda: R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=fids))}
             print(json.dumps(res), flush=True)
             for k in v:
