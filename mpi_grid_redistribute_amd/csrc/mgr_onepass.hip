@@ -70,7 +70,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8))) vo
     // rows take < 40 KiB and, with <= 64 VGPRs (amdgpu_waves_per_eu(8)), four
     // workgroups fit a CU: a tile waiting on its look-back leaves three to keep
     // memory busy (A/B, 64M config-5 rows: 1.19-1.20 ms against 1.39 with the
-    // 64-entry tables and three per CU; 512-row tiles, eight per CU: 1.60)
+    // 64-entry tables and three per CU; 512-row tiles, eight per CU: 1.60; a
+    // persistent grid taking tiles by ticket: 1.40, and 2.64 with the next
+    // ticket taken during the look-back -- the held tile delays its successors)
     const int nbe = (nb + 1) & ~1;
     const int wave_lds = WR * rb + 8 * nbe + 2 * WR;
     uint8_t* wl = smem + w * wave_lds;
