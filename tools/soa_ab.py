@@ -39,9 +39,15 @@ def timed(fn):
 
 
 def main():
-    soa = mgr.synth_wide_soa(N, seed=1)
-    rec, rpos = mgr.synth_wide(N, seed=1)
-    rbs = [12, 12, 4, 8]
+    cfg2 = os.environ.get("AB_FIELDS", "cfg5") == "cfg2"   # config 2's f64 positions + ids
+    if cfg2:
+        rpos, rec = mgr.synth_uniform(N, seed=1)
+        soa = (rpos.contiguous(), rec[:, 24:32].contiguous().view(torch.int64).reshape(-1))
+        rbs, arb = [24, 8], 32
+    else:
+        soa = mgr.synth_wide_soa(N, seed=1)
+        rec, rpos = mgr.synth_wide(N, seed=1)
+        rbs, arb = [12, 12, 4, 8], 36
     flats = [t.reshape(-1).view(torch.uint8) for t in soa]
     P = mgr.GridPartitioner([2, 2, 2], [1.0] * 3)
     fplan = P._fine_plan([8, 8, 8])
@@ -56,20 +62,26 @@ def main():
         counts = torch.empty(8, dtype=torch.int64, device="cuda")
         fid = torch.empty(N, dtype=torch.int16, device="cuda")
         fido = torch.empty(N, dtype=torch.int16, device="cuda")
-        _lib.call("mgr_bin_count_fine", P._plan.h, fplan.h, _lib.ptr(soa[0]), _lib.MGR_F32, N, 3,
-                  1, _lib.ptr(dest), _lib.ptr(fid), tr, _lib.ptr(ws), s)
+        if cfg2:
+            _lib.call("mgr_bin_count", P._plan.h, _lib.ptr(soa[0]), _lib.MGR_F64, N, 3, 1,
+                      _lib.ptr(dest), tr, _lib.ptr(ws), s)
+        else:
+            _lib.call("mgr_bin_count_fine", P._plan.h, fplan.h, _lib.ptr(soa[0]), _lib.MGR_F32, N,
+                      3, 1, _lib.ptr(dest), _lib.ptr(fid), tr, _lib.ptr(ws), s)
         _lib.call("mgr_scan", N, 8, tr, _lib.ptr(ws), _lib.ptr(counts), s)
         outs = [torch.empty(N * b, dtype=torch.uint8, device="cuda") for b in rbs]
-        o36 = torch.empty(N * 36, dtype=torch.uint8, device="cuda")
+        o36 = torch.empty(N * arb, dtype=torch.uint8, device="cuda")
+
+        side = (None, None) if cfg2 else (_lib.ptr(fid), _lib.ptr(fido))
 
         def fields():
-            _lib.call("mgr_pack_fields", 4, _ptrs([f.data_ptr() for f in flats]), _i64s(rbs), N,
-                      _lib.ptr(dest), 8, -1, tr, _lib.ptr(ws), _ptrs([o.data_ptr() for o in outs]),
-                      -1, None, _lib.ptr(fid), _lib.ptr(fido), None, 0, -1, s)
+            _lib.call("mgr_pack_fields", len(rbs), _ptrs([f.data_ptr() for f in flats]), _i64s(rbs),
+                      N, _lib.ptr(dest), 8, -1, tr, _lib.ptr(ws),
+                      _ptrs([o.data_ptr() for o in outs]), -1, None, side[0], side[1], None, 0, -1, s)
 
         def perfield():
             for i, (f, b, o) in enumerate(zip(flats, rbs, outs)):
-                if i == 0:
+                if i == 0 and not cfg2:
                     _lib.call("mgr_pack_ids", _lib.ptr(f), b, N, _lib.ptr(dest), 8, -1, tr,
                               _lib.ptr(ws), _lib.ptr(o), -1, None, _lib.ptr(fid), _lib.ptr(fido),
                               None, s)
@@ -78,8 +90,12 @@ def main():
                               _lib.ptr(ws), _lib.ptr(o), -1, None, s)
 
         def aos():
-            _lib.call("mgr_pack_ids", _lib.ptr(rec), 36, N, _lib.ptr(dest), 8, -1, tr,
-                      _lib.ptr(ws), _lib.ptr(o36), -1, None, _lib.ptr(fid), _lib.ptr(fido), None, s)
+            if cfg2:
+                _lib.call("mgr_pack", _lib.ptr(rec), arb, N, _lib.ptr(dest), 8, -1, tr,
+                          _lib.ptr(ws), _lib.ptr(o36), -1, None, s)
+            else:
+                _lib.call("mgr_pack_ids", _lib.ptr(rec), arb, N, _lib.ptr(dest), 8, -1, tr,
+                          _lib.ptr(ws), _lib.ptr(o36), -1, None, side[0], side[1], None, s)
 
         def copy():
             for f, o in zip(flats, outs):
@@ -97,6 +113,9 @@ def main():
         del outs, o36
     _lib.test_hook("tile_rounds", 0)
     _lib.test_hook("fields_kernel", 0)
+    if cfg2:
+        print(json.dumps(out), flush=True)
+        return
     # destination side: ranked pack per field vs the 36-byte record
     ids = fido[:N]
     R1 = mgr.MPIGridRedistributor(None, [1, 1, 1], [0.5] * 3)
