@@ -25,7 +25,8 @@ NAMES = {"bin_count_kernel": "bin_count", "pack_coop_kernel": "pack", "pack_img_
          "pack_kernel": "pack", "pack_ranked_kernel": "pack_fine", "rank_ids_kernel": "count_ids",
          "count_ids_kernel": "count_ids", "msel_pack_kernel": "halo_pack",
          "msel_count_kernel": "halo", "scan_onepass_kernel": "scan", "pack_fields_kernel": "pack",
-         "pack_coop_fields_kernel": "pack", "onepass_partition_kernel": "onepass"}
+         "pack_coop_fields_kernel": "pack", "pack_fields_tile_kernel": "pack",
+         "onepass_partition_kernel": "onepass"}
 
 SRC, DST = sys.argv[1], sys.argv[2]
 # scripts/gpu_pmc.sh OUT=<line> PASSES=sq writes gpurun_out/pmc_<line>/
