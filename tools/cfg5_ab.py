@@ -65,6 +65,7 @@ def main():
                    "src_fine": timed(lambda: part.partition_device(flat, 36, pos, fine_cells=[8, 8, 8])),
                    "src_onepass": timed(lambda: part.partition_onepass_device(
                        flat, 36, pos, fine_cells=[8, 8, 8])),
+                   "src_onepass_plain": timed(lambda: part.partition_onepass_device(flat, 36, pos)),
                    "dst_sort": timed(lambda: R1.fine_cell_sort(recv, rpos, [8, 8, 8], fine_ids=fids))}
             print(json.dumps(res), flush=True)
             for k in v:
