@@ -907,7 +907,7 @@ __device__ __forceinline__ void tile_field_store(const uint8_t* img, const uint8
         store_img_unit<RB, true>(img, ibin, gaddr, x, tile_bytes);
 }
 
-__global__ __launch_bounds__(1024) void pack_fields_tile_kernel(
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void pack_fields_tile_kernel(
     PackFieldsArgs fa, int64_t n, const uint8_t* __restrict__ dest, int nb, int nbits,
     int drop_bin, const int64_t* __restrict__ offsets, const int64_t* __restrict__ bin_starts,
     int64_t T, int64_t t0, int64_t tn, int tile_rows, int redirect_bin, int xcd,
@@ -915,13 +915,15 @@ __global__ __launch_bounds__(1024) void pack_fields_tile_kernel(
     uint16_t* __restrict__ id_dst, uint16_t* __restrict__ id_red, int img_bytes) {
     constexpr int WR = kFieldsWR, RPW = WR / 64;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_cnt[16][64];
     __shared__ unsigned long long s_gaddr[64];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = lane_id();
     const int nw = blockDim.x >> 6;
     uint8_t* img = smem;                                        // [img_bytes]
     uint8_t* ibin = smem + img_bytes;                           // [tile_rows]
     uint8_t* wl = ibin + align16(tile_rows) + w * fa.wave_lds;  // the wave's staged rows
+    // the waves' bin counts [nw][64], after the staging (sized by the waves,
+    // so six 512-row workgroups of config 5's SoA fields fit a CU's LDS)
+    int (*s_cnt)[64] = (int (*)[64])(ibin + align16(tile_rows) + nw * fa.wave_lds);
     const int64_t tile = t0 + (xcd ? xcd_tile_c(blockIdx.x, tn, xcd) : (int64_t)blockIdx.x);
     const int64_t tile0 = tile * (int64_t)tile_rows;
     const int64_t row0 = tile0 + (int64_t)WR * w;
@@ -1722,7 +1724,7 @@ hipError_t launch_pack_fields(int nf, const void* const* srcs, const int64_t* ro
         }
         fa.wave_lds = rows;
         const int img = align16(tile_rows * max_rb);
-        const int lds = img + align16(tile_rows) + nw * fa.wave_lds;
+        const int lds = img + align16(tile_rows) + nw * fa.wave_lds + nw * 64 * 4;
         if (lds <= 150 * 1024) {
             ensure_lds(pack_fields_tile_kernel, lds);
             prof_begin(s, K_PACK);
